@@ -1,0 +1,217 @@
+"""Benchmark: block-Lanczos iterations/sec + SpMM achieved HBM GB/s vs peak
+(BASELINE.json metric), n = 10M, nnz = 1e8, b = 16, fp64, on MI355X.
+
+    python bench.py [--gpus N] [--steps K] [--warmup W]
+
+A "step" is one block-Lanczos iteration (fused SpMM pass + alpha finish +
+update pass + beta sqrtm) over the whole synthetic operator, inputs resident in
+HBM.  N = 1: config C3 on one GPU.  N > 1 (launched by torch.distributed.run):
+weak scaling -- every rank owns a 10M-row slab of an N*10M-row banded operator,
+row-partitioned, with an RCCL all-gather of the Krylov block each iteration;
+`value` counts slab-iterations/s summed over ranks.  rank 0 prints one JSON line.
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import sys
+import time
+
+import numpy as np
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, ROOT)
+import __graft_entry__ as ge  # noqa: E402
+
+HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec (MI355X_MICROARCH.md)
+FP64_PEAK_TFS = 78.6
+
+
+def log(*a):
+    print(*a, file=sys.stderr, flush=True)
+
+
+def spmm_bytes(n, nnz, b, sv=8):
+    """Reference's A + 2B model + row_ptr: z(s_v+4) + (n+1)8 + 2 n b s_v."""
+    return nnz * (sv + 4) + (n + 1) * 8 + 2 * n * b * sv
+
+
+def fused_pass_bytes(n, nnz, b, sv=8):
+    """Algorithmic bytes of one k_fused_spmm16 launch: A, the Krylov block read
+    once, Q_{j-1} read, Q_j and W' written (DESIGN.md "Roofline")."""
+    return nnz * (sv + 4) + (n + 1) * 8 + 4 * n * b * sv
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=20)
+    ap.add_argument("--warmup", type=int, default=3)
+    ap.add_argument("--n", type=int, default=10_000_000, help="rows per GPU")
+    ap.add_argument("--nnz-per-row", type=float, default=10.0)
+    ap.add_argument("--halfwidth", type=int, default=4096)
+    ap.add_argument("--b", type=int, default=16)
+    ap.add_argument("--unfused", action="store_true")
+    ap.add_argument("--cpu-iters", type=int, default=3)
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--spmm-reps", type=int, default=20)
+    args = ap.parse_args()
+
+    import torch
+    import torch.distributed as dist
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    if world != args.gpus:
+        log(f"note: --gpus {args.gpus} but WORLD_SIZE={world}; using WORLD_SIZE")
+    torch.cuda.set_device(local)
+    if world > 1:
+        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+
+    lz = ge.load_package()
+    h = lz.Handle(local)
+    b, n = args.b, args.n
+    seed = 20261015
+    t_gen = time.time()
+    if world == 1:
+        A = lz.gen_banded(n, args.nnz_per_row, args.halfwidth, seed)
+    else:
+        A = lz.gen_banded_local(n * world, rank * n, (rank + 1) * n, args.nnz_per_row, args.halfwidth, seed)
+    B = lz.uniform_B(n, b, seed + rank)
+    log(f"[rank {rank}] generated n={A.n} nnz={A.nnz} in {time.time() - t_gen:.1f}s")
+    Ad = lz.CsrDevice.from_host(A, n_cols=n * world)
+    Bd = torch.from_numpy(B).cuda()
+    kw = dict(dtype=torch.float64, device="cuda")
+    m_max = max(args.steps, args.warmup, 1)
+    q = torch.zeros(m_max * b, **kw)
+    alpha = torch.zeros(m_max, b, b, **kw)
+    beta = torch.zeros(m_max + 1, b, b, **kw)
+    Q0, Q1, W = (torch.zeros(n, b, **kw) for _ in range(3))
+    lc = 84 if rank == 0 else -1
+
+    if world == 1:
+        def run(m):
+            h.block_lanczos_blas(Ad, Bd, m, 84, q, alpha, beta, Q0, Q1, W, fused=not args.unfused)
+    else:
+        uid = [lz.comm_unique_id() if rank == 0 else None]
+        dist.broadcast_object_list(uid, src=0)
+        h.comm_init(world, rank, uid[0])
+        X_full = torch.zeros(n * world, b, **kw)
+
+        def run(m):
+            h.block_lanczos_dist(Ad, n, n * world, Bd, m, 84, 0, q, alpha, beta, Q0, W, X_full)
+
+    # ---- warmup
+    if args.warmup > 0:
+        run(args.warmup)
+    torch.cuda.synchronize()
+
+    # ---- timed region: exactly K steps
+    h.prof_enable(True)
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    run(args.steps)
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    t1 = time.perf_counter()
+    elapsed = t1 - t0
+    spmm_ms, spmm_cnt = h.prof_read(h.PROF_SPMM_PASS)
+    upd_ms, upd_cnt = h.prof_read(h.PROF_UPDATE_PASS)
+    small_ms, small_cnt = h.prof_read(h.PROF_SMALL)
+    gram_ms, gram_cnt = h.prof_read(h.PROF_GRAM)
+    h.prof_enable(False)
+    if world > 1:
+        t = torch.tensor([elapsed], dtype=torch.float64, device="cuda")
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        elapsed = float(t.item())
+    assert torch.isfinite(alpha[: args.steps]).all(), "non-finite alpha"
+
+    # ---- plain SpMM kernel (the BASELINE headline kernel), same operator
+    plain = None
+    if world == 1 and args.spmm_reps > 0:
+        Y = torch.empty(n, b, **kw)
+        h.spmm(Ad, Q0, Y)
+        torch.cuda.synchronize()
+        h.prof_enable(True)
+        for _ in range(args.spmm_reps):
+            h.spmm(Ad, Q0, Y)
+        torch.cuda.synchronize()
+        ms, cnt = h.prof_read(h.PROF_SPMM)
+        h.prof_enable(False)
+        t_avg = ms / cnt * 1e-3
+        gbs = spmm_bytes(n, A.nnz, b) / t_avg / 1e9
+        plain = {"kernel": "k_spmm_rm<double,16>", "avg_ms": round(ms / cnt, 4),
+                 "bytes_per_launch": spmm_bytes(n, A.nnz, b), "achieved_GBs": round(gbs, 1),
+                 "frac_of_hbm_peak": round(gbs / HBM_PEAK_GBS, 4)}
+
+    # ---- CPU baseline: the oracle (C, OpenMP) on this operator, rank 0, N = 1
+    cpu = None
+    if world == 1 and rank == 0 and not args.no_cpu_baseline:
+        orc = ge.load_oracle()
+        iters = max(1, args.cpu_iters)
+        t_cpu = orc.time_block_iters(A, B, iters)
+        cpu = {"value": round(iters / t_cpu, 4), "unit": "iters/s", "cores": orc.num_threads(),
+               "kind": "port",
+               "sample": f"{iters} block-Lanczos iterations (after the start-up step) of the same "
+                         f"n={n} nnz={A.nnz} b={b} fp64 operator, oracle/lz_oracle.c OpenMP"}
+
+    if rank == 0:
+        K = args.steps
+        value = world * K / elapsed
+        fused = not args.unfused
+        t_pass = spmm_ms / max(spmm_cnt, 1) * 1e-3 if spmm_cnt else None
+        if fused and t_pass:
+            ach = fused_pass_bytes(n, A.nnz, b) / t_pass / 1e9
+            roof = {"bound": "hbm", "kernel": "k_fused_spmm16", "achieved": round(ach, 1),
+                    "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": round(ach / HBM_PEAK_GBS, 4),
+                    "traffic": None, "avg_ms": round(t_pass * 1e3, 4),
+                    "bytes_per_launch": fused_pass_bytes(n, A.nnz, b)}
+        elif plain:
+            roof = {"bound": "hbm", "kernel": plain["kernel"], "achieved": plain["achieved_GBs"],
+                    "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": plain["frac_of_hbm_peak"], "traffic": None}
+        else:
+            roof = None
+        iter_min_bytes = A.nnz * 12 + (n + 1) * 8 + 8 * n * b * 8
+        out = {
+            "metric": "block-Lanczos iters/sec + SpMM achieved HBM GB/s vs peak, n=10M nnz=1e8 b=16",
+            "value": round(value, 3),
+            "unit": "iters/s",
+            "n_gpus": world,
+            "steps": K,
+            "warmup": args.warmup,
+            "ms_per_step": round(elapsed / K * 1e3, 4),
+            "higher_is_better": True,
+            "scaling": "weak",
+            "vs_baseline": None,
+            "dtype": "f64",
+            "data": "synthetic (splitmix64 banded-random symmetric CSR, seed 20261015)",
+            "config": {"workload": "C3 block Lanczos b=16 fp64, banded-random symmetric CSR "
+                                   f"n={n} per GPU, nnz~{args.nnz_per_row:g}/row, halfwidth {args.halfwidth}",
+                       "n_per_gpu": n, "nnz_per_gpu": A.nnz, "b": b, "m_timed": K,
+                       "path": "fused" if fused else "unfused",
+                       "parallelism": "single" if world == 1 else f"rows{world}+rccl_allgather"},
+            "roofline": roof,
+            "cpu_baseline": cpu,
+            "extra": {
+                "plain_spmm": plain,
+                "kernel_ms_per_step": {"fused_spmm_pass": round(spmm_ms / K, 4),
+                                       "update_pass": round(upd_ms / K, 4),
+                                       "finish_sqrtm": round(small_ms / K, 4),
+                                       "gram": round(gram_ms / K, 4)},
+                "iteration_frac_of_roofline": round(iter_min_bytes / (elapsed / K) / 1e9 / HBM_PEAK_GBS, 4),
+                "iteration_min_bytes": iter_min_bytes,
+            },
+        }
+        print(json.dumps(out), flush=True)
+    h.close()
+    if world > 1:
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

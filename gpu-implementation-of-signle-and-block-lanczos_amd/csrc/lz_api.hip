@@ -1,0 +1,524 @@
+// lz_api.hip -- the extern "C" boundary of liblz_hip.so (include/lz_hip.h)
+// plus the device-resident Lanczos methods behind it.
+#include <rccl/rccl.h>
+
+#include <cstdarg>
+#include <cstring>
+#include <utility>
+
+#include "lz_common.hpp"
+#include "lz_internal.hpp"
+#include "lz_kernels.hpp"
+
+namespace lz {
+
+static thread_local char g_err[1024] = "";
+
+int prof_begin(lz_handle *h, int cls)
+{
+    if (!h->prof || h->ev_used + 2 > h->ev_cap) return -1;
+    const int idx = h->ev_used;
+    if (hipEventRecord(h->ev_pool[idx], h->stream) != hipSuccess) return -1;
+    h->ev_class[idx / 2] = cls;
+    h->ev_used += 2;
+    return idx;
+}
+
+void prof_end(lz_handle *h, int idx)
+{
+    if (idx >= 0) (void)hipEventRecord(h->ev_pool[idx + 1], h->stream);
+}
+
+void set_error(const char *fmt, ...)
+{
+    va_list ap;
+    va_start(ap, fmt);
+    vsnprintf(g_err, sizeof(g_err), fmt, ap);
+    va_end(ap);
+}
+
+static int check_csr(int64_t n, int64_t nnz, const int64_t *rp, const int32_t *col,
+                     const void *val)
+{
+    LZ_ARG_CHECK(n >= 0 && nnz >= 0, "negative size");
+    LZ_ARG_CHECK(rp != nullptr, "row_ptr is NULL");
+    LZ_ARG_CHECK(nnz == 0 || (col != nullptr && val != nullptr), "col/val NULL");
+    return LZ_OK;
+}
+
+template <typename T>
+__global__ void k_axpy(int64_t n, T a, const T *__restrict__ x, T *__restrict__ y)
+{
+    for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n;
+         i += (int64_t)gridDim.x * blockDim.x)
+        y[i] = fma(a, x[i], y[i]);
+}
+
+template <typename T>
+static int axpy(lz_handle *h, int64_t n, T a, const T *x, T *y)
+{
+    const int grid = (int)std::max<int64_t>(1, std::min<int64_t>(ceil_div(n, 256), h->n_cu * 8));
+    hipLaunchKernelGGL((k_axpy<T>), dim3(grid), dim3(256), 0, h->stream, n, a, x, y);
+    LZ_LAUNCH_CHECK();
+    return LZ_OK;
+}
+
+// ---------------------------------------------------------- block Lanczos
+// Reference op order, one kernel (or kernel pair) per reference call
+// (methods/block_lanczos.hpp:104-166).  Any b <= 32, fp64 or fp32.
+template <typename T>
+static int block_lanczos_unfused(lz_handle *h, int64_t n, const int64_t *rp, const int32_t *col,
+                                 const T *val, int b, int m, int64_t lc, const T *B, T *q, T *alpha,
+                                 T *beta, T *Q0, T *Q1, T *W)
+{
+    const int64_t bb = (int64_t)b * b;
+    T *binv = beta + (int64_t)m * bb;  // the reference's beta[m]
+    int P = 0;
+    // beta[0] = sqrtm(B'B), beta[m] = inverse            (:106-111)
+    LZ_TRY(gram_partials<T>(h, n, b, B, B, b, &P));
+    LZ_TRY(sqrtm_pair<T>(h, b, nullptr, P, beta, binv, nullptr));
+    LZ_TRY(tsmm<T>(h, n, b, T(0), T(1), B, binv, Q0, b));          // Q0 = B*beta_inv (:114)
+    LZ_TRY(copy_row<T>(h, b, Q0, b, 0, lc, q));                     // (:118)
+    LZ_TRY(spmm_rm<T>(h, n, rp, col, val, b, Q0, b, W, b));          // W = A*Q0 (:121)
+    LZ_TRY(gram_partials<T>(h, n, b, W, Q0, b, &P));                 // alpha[0] (:124)
+    LZ_TRY(gram_finish<T>(h, b, P, 1, alpha));
+    LZ_TRY(tsmm<T>(h, n, b, T(1), T(-1), Q0, alpha, W, b));          // W -= Q0*alpha (:128)
+    for (int j = 1; j < m; ++j) {
+        T *bj = beta + j * bb, *aj = alpha + j * bb;
+        LZ_TRY(gram_partials<T>(h, n, b, W, W, b, &P));              // (:137)
+        LZ_TRY(sqrtm_pair<T>(h, b, nullptr, P, bj, binv, nullptr));  // (:142)
+        LZ_TRY(tsmm<T>(h, n, b, T(0), T(1), W, binv, Q1, b));        // Q1 = W*beta_inv (:145)
+        LZ_TRY(spmm_rm<T>(h, n, rp, col, val, b, Q1, b, W, b));      // W = A*Q1 (:149)
+        LZ_TRY(tsmm<T>(h, n, b, T(1), T(-1), Q0, bj, W, b));         // W -= Q0*beta (:152)
+        LZ_TRY(gram_partials<T>(h, n, b, W, Q1, b, &P));             // alpha[j] (:155)
+        LZ_TRY(gram_finish<T>(h, b, P, 1, aj));
+        LZ_TRY(tsmm<T>(h, n, b, T(1), T(-1), Q1, aj, W, b));         // W -= Q1*alpha (:159)
+        std::swap(Q0, Q1);                                           // Q0 = Q1 (:162), no copy
+        LZ_TRY(copy_row<T>(h, b, Q0, b, 0, lc, q + j * b));          // (:165)
+    }
+    return LZ_OK;
+}
+
+// Fused device-resident iteration, b = 16 fp64 (lz_fused.hip).
+static int block_lanczos_fused16(lz_handle *h, int64_t n, const int64_t *rp, const int32_t *col,
+                                 const double *val, int m, int64_t lc, const double *B, double *q,
+                                 double *alpha, double *beta, double *Q0, double *Q1, double *W)
+{
+    constexpr int64_t bb = 256;
+    double *binv = beta + m * bb;
+    int P = 0;
+    LZ_TRY(gram_partials<double>(h, n, 16, B, B, 16, &P));
+    LZ_TRY(sqrtm_pair<double>(h, 16, nullptr, P, beta, binv, nullptr));
+    const double *res_in = B;
+    double *bufs[2] = {W, Q1};  // the residual alternates; Q_j lives in Q0
+    for (int j = 0; j < m; ++j) {
+        double *res_out = bufs[j & 1];
+        LZ_TRY(fused_spmm16(h, n, rp, col, val, res_in, res_in, Q0, res_out, binv,
+                            j ? beta + j * bb : nullptr, lc, q + j * 16, &P));
+        LZ_TRY(gram_finish<double>(h, 16, P, 1, alpha + j * bb));
+        LZ_TRY(fused_update16(h, n, res_out, Q0, alpha + j * bb, &P));
+        if (j + 1 < m)
+            LZ_TRY(sqrtm_pair<double>(h, 16, nullptr, P, beta + (j + 1) * bb, binv, nullptr));
+        res_in = res_out;
+    }
+    return LZ_OK;
+}
+
+// ------------------------------------------------------------------ FDTD
+template <typename T>
+static int fdtd_block(lz_handle *h, int64_t n, const int64_t *rp, const int32_t *col, const T *val,
+                      int b, const T *U0, int64_t steps, double T_end, int64_t lc, T *U, T *D,
+                      T *out)
+{
+    const T dt = (T)(T_end / (double)steps);   // fdtd.hpp:41
+    LZ_HIP_TRY(hipMemcpyAsync(U, U0, sizeof(T) * n * b, hipMemcpyDeviceToDevice, h->stream));
+    for (int64_t s = 0; s < steps; ++s) {
+        LZ_TRY(spmm_rm<T>(h, n, rp, col, val, b, U, b, D, b));      // fdtd.hpp:48
+        LZ_TRY(axpy<T>(h, n * b, dt, D, U));                         // fdtd.hpp:49
+    }
+    return copy_row<T>(h, b, U, b, 0, lc, out);                      // fdtd.hpp:52
+}
+
+// ------------------------------------------------------------ multi-GPU
+static ncclComm_t comm_of(lz_handle *h) { return reinterpret_cast<ncclComm_t>(h->comm); }
+
+#define LZ_NCCL_TRY(expr)                                                            \
+    do {                                                                             \
+        ncclResult_t r_ = (expr);                                                    \
+        if (r_ != ncclSuccess) {                                                     \
+            ::lz::set_error("%s -> %s", #expr, ncclGetErrorString(r_));             \
+            return LZ_E_COMM;                                                        \
+        }                                                                            \
+    } while (0)
+
+// b = 16 fp64 row-partitioned iteration.  Per step: ncclAllGather of the
+// residual slab into X_full, the fused SpMM pass on local rows, two b x b
+// ncclAllReduce (alpha and Gram partial sums), sqrtm redundantly on every rank.
+static int block_lanczos_dist16(lz_handle *h, int64_t n_local, int64_t n_pad, const int64_t *rp,
+                                const int32_t *col, const double *val, int m, int64_t lc_local,
+                                const double *B, double *q, double *alpha, double *beta, double *Q0,
+                                double *W, double *X)
+{
+    constexpr int64_t bb = 256;
+    ncclComm_t comm = comm_of(h);
+    double *binv = beta + m * bb;
+    double *slab = h->scratch;  // one reduced b x b slab, all-reduced in place
+    const double *own = X + (int64_t)h->rank * n_pad * 16;
+    int P = 0;
+    // beta_0 from the global Gram of B
+    LZ_TRY(gram_partials<double>(h, n_local, 16, B, B, 16, &P));
+    LZ_TRY(gram_finish<double>(h, 16, P, 0, slab));
+    LZ_NCCL_TRY(ncclAllReduce(slab, slab, bb, ncclDouble, ncclSum, comm, h->stream));
+    LZ_TRY(sqrtm_pair<double>(h, 16, nullptr, 1, beta, binv, nullptr, slab));
+    LZ_NCCL_TRY(ncclAllGather(B, X, n_pad * 16, ncclDouble, comm, h->stream));
+    for (int j = 0; j < m; ++j) {
+        LZ_TRY(fused_spmm16(h, n_local, rp, col, val, X, own, Q0, W, binv,
+                            j ? beta + j * bb : nullptr, lc_local, q + j * 16, &P));
+        LZ_TRY(gram_finish<double>(h, 16, P, 0, slab));
+        LZ_NCCL_TRY(ncclAllReduce(slab, slab, bb, ncclDouble, ncclSum, comm, h->stream));
+        LZ_TRY(gram_finish<double>(h, 16, 1, 1, alpha + j * bb, slab));
+        LZ_TRY(fused_update16(h, n_local, W, Q0, alpha + j * bb, &P));
+        if (j + 1 < m) {
+            LZ_TRY(gram_finish<double>(h, 16, P, 0, slab));
+            LZ_NCCL_TRY(ncclAllReduce(slab, slab, bb, ncclDouble, ncclSum, comm, h->stream));
+            LZ_TRY(sqrtm_pair<double>(h, 16, nullptr, 1, beta + (j + 1) * bb, binv, nullptr, slab));
+            LZ_NCCL_TRY(ncclAllGather(W, X, n_pad * 16, ncclDouble, comm, h->stream));
+        }
+    }
+    return LZ_OK;
+}
+
+}  // namespace lz
+
+using namespace lz;
+
+#define LZ_HANDLE_CHECK(h)                                                          \
+    do {                                                                            \
+        if (!(h)) {                                                                 \
+            set_error("handle is NULL");                                           \
+            return LZ_E_STATE;                                                      \
+        }                                                                           \
+        LZ_HIP_TRY(hipSetDevice((h)->device));                                      \
+    } while (0)
+
+extern "C" {
+
+const char *lz_last_error(void) { return g_err; }
+const char *lz_version(void) { return "lz_hip 0.1 gfx950"; }
+
+int lz_device_ok(int device)
+{
+    int count = 0;
+    if (hipGetDeviceCount(&count) != hipSuccess || device < 0 || device >= count) return 0;
+    hipDeviceProp_t prop;
+    if (hipGetDeviceProperties(&prop, device) != hipSuccess) return 0;
+    return std::strncmp(prop.gcnArchName, "gfx950", 6) == 0 ? 1 : 0;
+}
+
+int lz_init(int device, lz_handle **out)
+{
+    LZ_ARG_CHECK(out != nullptr, "out handle pointer is NULL");
+    *out = nullptr;
+    int count = 0;
+    LZ_HIP_TRY(hipGetDeviceCount(&count));
+    LZ_ARG_CHECK(device >= 0 && device < count, "device index");
+    LZ_HIP_TRY(hipSetDevice(device));
+    lz_handle *h = new lz_handle();
+    h->device = device;
+    hipDeviceProp_t prop;
+    LZ_HIP_TRY(hipGetDeviceProperties(&prop, device));
+    if (std::strncmp(prop.gcnArchName, "gfx950", 6) != 0) {
+        set_error("device %d is %s, liblz_hip.so is built for gfx950 only", device,
+                  prop.gcnArchName);
+        delete h;
+        return LZ_E_HIP;
+    }
+    h->n_cu = prop.multiProcessorCount;
+    LZ_HIP_TRY(hipMalloc(&h->partials, sizeof(double) * (size_t)kMaxPartials * kMaxB * kMaxB));
+    LZ_HIP_TRY(hipMalloc(&h->scratch, sizeof(double) * 8 * kMaxB * kMaxB));
+    *out = h;
+    return LZ_OK;
+}
+
+int lz_finalize(lz_handle *h)
+{
+    if (!h) return LZ_OK;
+    (void)hipSetDevice(h->device);
+    if (h->comm) ncclCommDestroy(comm_of(h));
+    if (h->ev_pool) {
+        for (int i = 0; i < h->ev_cap; ++i) (void)hipEventDestroy(h->ev_pool[i]);
+        delete[] h->ev_pool;
+    }
+    (void)hipFree(h->partials);
+    (void)hipFree(h->scratch);
+    delete h;
+    return LZ_OK;
+}
+
+int lz_prof_enable(lz_handle *h, int on)
+{
+    LZ_HANDLE_CHECK(h);
+    if (on && !h->ev_pool) {
+        h->ev_cap = 8192;
+        h->ev_pool = new hipEvent_t[h->ev_cap];
+        for (int i = 0; i < h->ev_cap; ++i) LZ_HIP_TRY(hipEventCreate(&h->ev_pool[i]));
+    }
+    h->prof = on != 0;
+    h->ev_used = 0;
+    return LZ_OK;
+}
+
+int lz_prof_read(lz_handle *h, int cls, double *ms_total, int *count)
+{
+    LZ_HANDLE_CHECK(h);
+    LZ_ARG_CHECK(ms_total && count, "NULL outputs");
+    *ms_total = 0.0;
+    *count = 0;
+    if (!h->ev_pool || h->ev_used == 0) return LZ_OK;
+    LZ_HIP_TRY(hipEventSynchronize(h->ev_pool[h->ev_used - 1]));
+    for (int i = 0; i < h->ev_used; i += 2) {
+        if (h->ev_class[i / 2] != cls) continue;
+        float ms = 0.f;
+        LZ_HIP_TRY(hipEventElapsedTime(&ms, h->ev_pool[i], h->ev_pool[i + 1]));
+        *ms_total += ms;
+        *count += 1;
+    }
+    return LZ_OK;
+}
+
+int lz_set_stream(lz_handle *h, void *stream)
+{
+    LZ_HANDLE_CHECK(h);
+    h->stream = reinterpret_cast<hipStream_t>(stream);
+    return LZ_OK;
+}
+
+int lz_csr_spmm(lz_handle *h, int64_t n_rows, int64_t n_cols, int64_t nnz, const int64_t *rp,
+                const int32_t *col, const void *val, lz_dtype dtype, int b, const void *X,
+                int64_t ldx, lz_layout layout, void *Y, int64_t ldy)
+{
+    LZ_HANDLE_CHECK(h);
+    LZ_TRY(check_csr(n_rows, nnz, rp, col, val));
+    LZ_ARG_CHECK(b >= 1 && b <= kMaxB, "b in [1,64]");
+    LZ_ARG_CHECK(X && Y, "X/Y NULL");
+    if (layout == LZ_ROW_MAJOR) {
+        LZ_ARG_CHECK(ldx >= b && ldy >= b, "row-major ld >= b");
+        if (dtype == LZ_F64)
+            return spmm_rm<double>(h, n_rows, rp, col, (const double *)val, b, (const double *)X,
+                                   ldx, (double *)Y, ldy);
+        return spmm_rm<float>(h, n_rows, rp, col, (const float *)val, b, (const float *)X, ldx,
+                              (float *)Y, ldy);
+    }
+    LZ_ARG_CHECK(ldx >= n_cols && ldy >= n_rows, "column-major ld >= rows");
+    if (dtype == LZ_F64)
+        return spmm_cm<double>(h, n_rows, rp, col, (const double *)val, b, (const double *)X, ldx,
+                               (double *)Y, ldy);
+    return spmm_cm<float>(h, n_rows, rp, col, (const float *)val, b, (const float *)X, ldx,
+                          (float *)Y, ldy);
+}
+
+int lz_csr_spmv(lz_handle *h, int64_t n_rows, int64_t n_cols, int64_t nnz, const int64_t *rp,
+                const int32_t *col, const void *val, lz_dtype dtype, const void *x, void *y)
+{
+    LZ_HANDLE_CHECK(h);
+    LZ_TRY(check_csr(n_rows, nnz, rp, col, val));
+    LZ_ARG_CHECK(x && y, "x/y NULL");
+    (void)n_cols;
+    if (dtype == LZ_F64)
+        return spmv<double>(h, n_rows, rp, col, (const double *)val, (const double *)x,
+                            (double *)y, nnz);
+    return spmv<float>(h, n_rows, rp, col, (const float *)val, (const float *)x, (float *)y, nnz);
+}
+
+int lz_gram(lz_handle *h, int64_t n, int b, lz_dtype dtype, const void *W, int64_t ld, void *R)
+{
+    LZ_HANDLE_CHECK(h);
+    LZ_ARG_CHECK(W && R && b >= 1 && b <= kMaxB && ld >= b && n >= 0, "gram args");
+    int P = 0;
+    if (dtype == LZ_F64) {
+        LZ_TRY(gram_partials<double>(h, n, b, (const double *)W, (const double *)W, ld, &P));
+        return gram_finish<double>(h, b, P, 0, (double *)R);
+    }
+    LZ_TRY(gram_partials<float>(h, n, b, (const float *)W, (const float *)W, ld, &P));
+    return gram_finish<float>(h, b, P, 0, (float *)R);
+}
+
+int lz_sym_cross_gram(lz_handle *h, int64_t n, int b, lz_dtype dtype, const void *W, const void *Q,
+                      int64_t ld, void *R)
+{
+    LZ_HANDLE_CHECK(h);
+    LZ_ARG_CHECK(W && Q && R && b >= 1 && b <= kMaxB && ld >= b && n >= 0, "cross gram args");
+    int P = 0;
+    if (dtype == LZ_F64) {
+        LZ_TRY(gram_partials<double>(h, n, b, (const double *)W, (const double *)Q, ld, &P));
+        return gram_finish<double>(h, b, P, 1, (double *)R);
+    }
+    LZ_TRY(gram_partials<float>(h, n, b, (const float *)W, (const float *)Q, ld, &P));
+    return gram_finish<float>(h, b, P, 1, (float *)R);
+}
+
+int lz_tsmm(lz_handle *h, int64_t n, int b, lz_dtype dtype, double beta, double alpha,
+            const void *Q, const void *S, void *W, int64_t ld)
+{
+    LZ_HANDLE_CHECK(h);
+    LZ_ARG_CHECK(Q && S && W && Q != W, "tsmm pointers (Q must not alias W)");
+    if (dtype == LZ_F64)
+        return tsmm<double>(h, n, b, beta, alpha, (const double *)Q, (const double *)S,
+                            (double *)W, ld);
+    return tsmm<float>(h, n, b, (float)beta, (float)alpha, (const float *)Q, (const float *)S,
+                       (float *)W, ld);
+}
+
+int lz_sqrtm_pair(lz_handle *h, int b, lz_dtype dtype, const void *G, void *beta, void *beta_inv,
+                  void *eigval)
+{
+    LZ_HANDLE_CHECK(h);
+    LZ_ARG_CHECK(G && b >= 1 && b <= 32, "sqrtm args");
+    if (dtype == LZ_F64)
+        return sqrtm_pair<double>(h, b, (const double *)G, 0, (double *)beta, (double *)beta_inv,
+                                  (double *)eigval);
+    return sqrtm_pair<float>(h, b, (const float *)G, 0, (float *)beta, (float *)beta_inv,
+                             (float *)eigval);
+}
+
+int lz_copy_row(lz_handle *h, int b, lz_dtype dtype, const void *Q, int64_t ld, lz_layout layout,
+                int64_t lc, void *q, int64_t start)
+{
+    LZ_HANDLE_CHECK(h);
+    LZ_ARG_CHECK(Q && q && b >= 1 && b <= kMaxB && lc >= 0, "copy_row args");
+    if (dtype == LZ_F64)
+        return copy_row<double>(h, b, (const double *)Q, ld, layout == LZ_COL_MAJOR, lc,
+                                (double *)q + start);
+    return copy_row<float>(h, b, (const float *)Q, ld, layout == LZ_COL_MAJOR, lc,
+                           (float *)q + start);
+}
+
+static int block_args(int64_t n, int64_t nnz, const int64_t *rp, const int32_t *col,
+                      const void *val, int b, int m, int64_t lc, const void *B, void *q,
+                      void *alpha, void *beta, void *Q0, void *Q1, void *W)
+{
+    LZ_TRY(check_csr(n, nnz, rp, col, val));
+    LZ_ARG_CHECK(n >= 1, "n >= 1");
+    LZ_ARG_CHECK(b >= 1 && b <= 32, "block Lanczos supports 1 <= b <= 32");
+    LZ_ARG_CHECK(m >= 1, "m >= 1");
+    LZ_ARG_CHECK(lc >= 0 && lc < n, "lc must be a row index");
+    LZ_ARG_CHECK(B && q && alpha && beta && Q0 && Q1 && W, "NULL buffer");
+    LZ_ARG_CHECK(Q0 != Q1 && Q0 != W && Q1 != W && B != Q0 && B != Q1 && B != W,
+                 "B, Q0, Q1, W must be distinct buffers");
+    return LZ_OK;
+}
+
+int lz_block_lanczos_unfused(lz_handle *h, int64_t n, int64_t nnz, const int64_t *rp,
+                             const int32_t *col, const void *val, lz_dtype dtype, int b, int m,
+                             int64_t lc, const void *B, void *q, void *alpha, void *beta, void *Q0,
+                             void *Q1, void *W)
+{
+    LZ_HANDLE_CHECK(h);
+    LZ_TRY(block_args(n, nnz, rp, col, val, b, m, lc, B, q, alpha, beta, Q0, Q1, W));
+    if (dtype == LZ_F64)
+        return block_lanczos_unfused<double>(h, n, rp, col, (const double *)val, b, m, lc,
+                                             (const double *)B, (double *)q, (double *)alpha,
+                                             (double *)beta, (double *)Q0, (double *)Q1,
+                                             (double *)W);
+    return block_lanczos_unfused<float>(h, n, rp, col, (const float *)val, b, m, lc,
+                                        (const float *)B, (float *)q, (float *)alpha,
+                                        (float *)beta, (float *)Q0, (float *)Q1, (float *)W);
+}
+
+int lz_block_lanczos(lz_handle *h, int64_t n, int64_t nnz, const int64_t *rp, const int32_t *col,
+                     const void *val, lz_dtype dtype, int b, int m, int64_t lc, const void *B,
+                     void *q, void *alpha, void *beta, void *Q0, void *Q1, void *W)
+{
+    LZ_HANDLE_CHECK(h);
+    LZ_TRY(block_args(n, nnz, rp, col, val, b, m, lc, B, q, alpha, beta, Q0, Q1, W));
+    if (dtype == LZ_F64 && b == 16)
+        return block_lanczos_fused16(h, n, rp, col, (const double *)val, m, lc,
+                                     (const double *)B, (double *)q, (double *)alpha,
+                                     (double *)beta, (double *)Q0, (double *)Q1, (double *)W);
+    return lz_block_lanczos_unfused(h, n, nnz, rp, col, val, dtype, b, m, lc, B, q, alpha, beta,
+                                    Q0, Q1, W);
+}
+
+int lz_vector_lanczos(lz_handle *h, int64_t n, int64_t nnz, const int64_t *rp, const int32_t *col,
+                      const void *val, lz_dtype dtype, int m, int64_t lc, const void *bvec,
+                      void *q, void *alpha, void *beta, void *q0, void *q1, void *w)
+{
+    LZ_HANDLE_CHECK(h);
+    LZ_TRY(check_csr(n, nnz, rp, col, val));
+    LZ_ARG_CHECK(dtype == LZ_F64, "vector Lanczos: fp64 only");
+    LZ_ARG_CHECK(n >= 1 && m >= 1 && lc >= 0 && lc < n, "vector Lanczos sizes");
+    LZ_ARG_CHECK(bvec && q && alpha && beta && q0 && q1 && w, "NULL buffer");
+    LZ_ARG_CHECK(bvec != q0 && bvec != q1 && bvec != w && q0 != q1 && q0 != w && q1 != w,
+                 "b, q0, q1, w must be distinct buffers");
+    return vector_lanczos_dev(h, n, nnz, rp, col, (const double *)val, m, lc,
+                              (const double *)bvec, (double *)q, (double *)alpha, (double *)beta,
+                              (double *)q0, (double *)q1, (double *)w);
+}
+
+int lz_fdtd_block(lz_handle *h, int64_t n, int64_t nnz, const int64_t *rp, const int32_t *col,
+                  const void *val, lz_dtype dtype, int b, const void *U0, int64_t steps,
+                  double T_end, int64_t lc, void *U, void *D, void *out)
+{
+    LZ_HANDLE_CHECK(h);
+    LZ_TRY(check_csr(n, nnz, rp, col, val));
+    LZ_ARG_CHECK(steps >= 1 && lc >= 0 && lc < n && U0 && U && D && out, "fdtd args");
+    if (dtype == LZ_F64)
+        return fdtd_block<double>(h, n, rp, col, (const double *)val, b, (const double *)U0, steps,
+                                  T_end, lc, (double *)U, (double *)D, (double *)out);
+    return fdtd_block<float>(h, n, rp, col, (const float *)val, b, (const float *)U0, steps,
+                             T_end, lc, (float *)U, (float *)D, (float *)out);
+}
+
+int lz_comm_unique_id(unsigned char out[128])
+{
+    static_assert(sizeof(ncclUniqueId) == 128, "ncclUniqueId size");
+    ncclUniqueId id;
+    LZ_NCCL_TRY(ncclGetUniqueId(&id));
+    std::memcpy(out, &id, 128);
+    return LZ_OK;
+}
+
+int lz_comm_init(lz_handle *h, int nranks, int rank, const unsigned char id[128])
+{
+    LZ_HANDLE_CHECK(h);
+    LZ_ARG_CHECK(nranks >= 1 && rank >= 0 && rank < nranks && id, "comm args");
+    ncclUniqueId uid;
+    std::memcpy(&uid, id, 128);
+    ncclComm_t c;
+    LZ_NCCL_TRY(ncclCommInitRank(&c, nranks, uid, rank));
+    h->comm = c;
+    h->nranks = nranks;
+    h->rank = rank;
+    return LZ_OK;
+}
+
+int lz_comm_destroy(lz_handle *h)
+{
+    LZ_HANDLE_CHECK(h);
+    if (h->comm) ncclCommDestroy(comm_of(h));
+    h->comm = nullptr;
+    h->nranks = 1;
+    h->rank = 0;
+    return LZ_OK;
+}
+
+int lz_block_lanczos_dist(lz_handle *h, int64_t n_local, int64_t n_pad, int64_t n_global,
+                          int64_t nnz_local, const int64_t *rp, const int32_t *col,
+                          const void *val, lz_dtype dtype, int b, int m, int64_t lc_local,
+                          int lc_rank, const void *B_local, void *q, void *alpha, void *beta,
+                          void *Q0, void *Q1, void *W, void *X_full)
+{
+    LZ_HANDLE_CHECK(h);
+    LZ_ARG_CHECK(h->comm != nullptr, "lz_comm_init first");
+    LZ_TRY(check_csr(n_local, nnz_local, rp, col, val));
+    LZ_ARG_CHECK(dtype == LZ_F64 && b == 16, "distributed path: b = 16 fp64");
+    LZ_ARG_CHECK(n_pad >= n_local && n_pad * h->nranks >= n_global && m >= 1, "dist sizes");
+    LZ_ARG_CHECK(B_local && q && alpha && beta && Q0 && W && X_full, "NULL buffer");
+    (void)Q1;
+    const int64_t lc = (lc_rank == h->rank) ? lc_local : -1;
+    return block_lanczos_dist16(h, n_local, n_pad, rp, col, (const double *)val, m, lc,
+                                (const double *)B_local, (double *)q, (double *)alpha,
+                                (double *)beta, (double *)Q0, (double *)W, (double *)X_full);
+}
+
+}  // extern "C"

@@ -1,0 +1,84 @@
+// lz_common.hpp -- shared definitions of liblz_hip.so (gfx950 only).
+#pragma once
+#include <hip/hip_runtime.h>
+
+#include <cstdint>
+#include <cstdio>
+#include <string>
+
+#include "lz_hip.h"
+
+namespace lz {
+
+// thread-local last error (lz_last_error)
+void set_error(const char *fmt, ...);
+
+#define LZ_HIP_TRY(expr)                                                          \
+    do {                                                                          \
+        hipError_t e_ = (expr);                                                   \
+        if (e_ != hipSuccess) {                                                   \
+            ::lz::set_error("%s:%d %s -> %s", __FILE__, __LINE__, #expr,          \
+                            hipGetErrorString(e_));                               \
+            return LZ_E_HIP;                                                      \
+        }                                                                         \
+    } while (0)
+
+#define LZ_ARG_CHECK(cond, msg)                                                   \
+    do {                                                                          \
+        if (!(cond)) {                                                            \
+            ::lz::set_error("argument error: %s (%s)", msg, #cond);             \
+            return LZ_E_ARG;                                                      \
+        }                                                                         \
+    } while (0)
+
+#define LZ_LAUNCH_CHECK()                                                         \
+    do {                                                                          \
+        hipError_t e_ = hipGetLastError();                                        \
+        if (e_ != hipSuccess) {                                                   \
+            ::lz::set_error("%s:%d kernel launch -> %s", __FILE__, __LINE__,      \
+                            hipGetErrorString(e_));                               \
+            return LZ_E_HIP;                                                      \
+        }                                                                         \
+    } while (0)
+
+#define LZ_TRY(expr)                                                              \
+    do {                                                                          \
+        int rc_ = (expr);                                                         \
+        if (rc_ != LZ_OK) return rc_;                                             \
+    } while (0)
+
+constexpr int kWave = 64;        // CDNA wavefront
+constexpr int kMaxPartials = 2048;  // per-workgroup partial b x b slabs kept in the handle
+constexpr int kMaxB = 64;
+
+__host__ __device__ inline int64_t ceil_div(int64_t a, int64_t b) { return (a + b - 1) / b; }
+
+}  // namespace lz
+
+// The opaque handle (lz_handle in the C ABI).
+struct lz_handle {
+    int device = 0;
+    hipStream_t stream = nullptr;
+    int n_cu = 256;
+    // device workspace: per-workgroup partial b x b sums (double), b x b
+    // scratch matrices and a few scalars.
+    double *partials = nullptr;   // kMaxPartials * kMaxB * kMaxB doubles
+    double *scratch = nullptr;    // 8 * kMaxB * kMaxB doubles
+    void *comm = nullptr;         // ncclComm_t when lz_comm_init was called
+    int nranks = 1, rank = 0;
+    // optional per-kernel-class timing with hipEvents on the handle's stream
+    // (lz_prof_enable / lz_prof_read): events recorded around each launch of
+    // the class, elapsed times summed at read time.
+    bool prof = false;
+    hipEvent_t *ev_pool = nullptr;
+    int ev_cap = 0, ev_used = 0;
+    int ev_class[4096];
+};
+
+namespace lz {
+enum ProfClass { PROF_SPMM_PASS = 0, PROF_UPDATE_PASS = 1, PROF_SMALL = 2, PROF_GRAM = 3,
+                 PROF_TSMM = 4, PROF_SPMM = 5, PROF_NCLASS = 6 };
+// bracket one launch: returns the event index of the start (-1 when off)
+int prof_begin(lz_handle *h, int cls);
+void prof_end(lz_handle *h, int idx);
+}  // namespace lz

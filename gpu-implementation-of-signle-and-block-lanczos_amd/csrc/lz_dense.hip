@@ -1,0 +1,453 @@
+// lz_dense.hip -- tall-skinny block-orthogonalisation kernels for gfx950.
+//
+// Replaces the reference's cuBLAS/cuSOLVER calls of block_lanczos_blas
+// (utils/lib_utils.hpp:28-202,649-745) and its hand-written float kernels
+// tt::mm_tt, tt2::mm_tt2, ts::mm_ts*, sqrtm::My_sqrtm_cusolver
+// (kernels/mm_tt.hpp, mm_tt2.hpp, mm_ts.hpp, my_sqrtm_cusolver.hpp).
+//
+// Layout: n x b row-major blocks.  For b = 16 fp64 the products run on the
+// f64 matrix cores (v_mfma_f64_16x16x4_f64):
+//   * Gram X^T Y: a 4-row chunk of a row-major block is exactly 64 contiguous
+//     doubles, and "lane l holds element l" is both MFMA operand layouts when
+//     the contraction runs over rows -- one coalesced 8-B load per operand.
+//   * Q*S: the contraction runs over columns, so each wave transposes a
+//     16x16 tile through a private LDS tile (row stride 17 doubles, conflict
+//     free for ds_read_b64) and the MFMA result lands in the row-major chunk
+//     layout again, so W is read/written with coalesced 8-B accesses.
+// Other (b, dtype): portable LDS-tiled VALU kernels.
+// Every reduction is a fixed-order two-stage reduction (per-workgroup slabs,
+// then one workgroup) -- bitwise reproducible run to run, no float atomics.
+#include "lz_common.hpp"
+#include "lz_internal.hpp"
+#include "lz_kernels.hpp"
+
+namespace lz {
+
+// ============================================================== Gram slabs
+template <bool SAME>
+__global__ __launch_bounds__(512) void k_gram16_f64(int64_t n, const double *__restrict__ X,
+                                                    const double *__restrict__ Y,
+                                                    double *__restrict__ part)
+{
+    __shared__ double red[8][256];
+    const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+    const int64_t nel = n * 16;
+    const int64_t nch = ceil_div(n, 4);
+    XcdSched s(ceil_div(nch, 8));
+    d4_t acc = {0.0, 0.0, 0.0, 0.0};
+    constexpr int U = 8;
+    for (int64_t u = s.begin; u < s.end; u += U * s.step) {
+        double xa[U], ya[U];
+#pragma unroll
+        for (int t = 0; t < U; ++t) {
+            const int64_t uu = u + t * s.step;
+            const int64_t e = (uu * 8 + w) * 64 + lane;
+            const bool ok = (uu < s.end) && (e < nel);
+            xa[t] = ok ? X[e] : 0.0;
+            ya[t] = SAME ? xa[t] : (ok ? Y[e] : 0.0);
+        }
+#pragma unroll
+        for (int t = 0; t < U; ++t) acc = mfma16(xa[t], ya[t], acc);
+    }
+#pragma unroll
+    for (int r = 0; r < 4; ++r) red[w][((lane >> 4) + 4 * r) * 16 + (lane & 15)] = acc[r];
+    __syncthreads();
+    if (threadIdx.x < 256) {
+        double sum = 0.0;
+#pragma unroll
+        for (int ww = 0; ww < 8; ++ww) sum += red[ww][threadIdx.x];
+        part[(int64_t)blockIdx.x * 256 + threadIdx.x] = sum;
+    }
+}
+
+template <typename T>
+__global__ __launch_bounds__(256) void k_gram_gen(int64_t n, int b, const T *__restrict__ X,
+                                                  const T *__restrict__ Y, int64_t ld,
+                                                  double *__restrict__ part)
+{
+    constexpr int TR = 16;
+    __shared__ double xs[TR * kMaxB], ys[TR * kMaxB];
+    const int bb = b * b, tid = threadIdx.x;
+    double acc[16];
+#pragma unroll
+    for (int k = 0; k < 16; ++k) acc[k] = 0.0;
+    XcdSched s(ceil_div(n, TR));
+    for (int64_t u = s.begin; u < s.end; u += s.step) {
+        for (int e = tid; e < TR * b; e += 256) {
+            const int r = e / b, c = e % b;
+            const int64_t row = u * TR + r;
+            xs[e] = row < n ? (double)X[row * ld + c] : 0.0;
+            ys[e] = row < n ? (double)Y[row * ld + c] : 0.0;
+        }
+        __syncthreads();
+#pragma unroll
+        for (int k = 0; k < 16; ++k) {
+            const int e = tid + 256 * k;
+            if (e < bb) {
+                const int i = e / b, j = e % b;
+                double a = acc[k];
+                for (int r = 0; r < TR; ++r) a = fma(xs[r * b + i], ys[r * b + j], a);
+                acc[k] = a;
+            }
+        }
+        __syncthreads();
+    }
+#pragma unroll
+    for (int k = 0; k < 16; ++k) {
+        const int e = tid + 256 * k;
+        if (e < bb) part[(int64_t)blockIdx.x * bb + e] = acc[k];
+    }
+}
+
+template <typename T>
+__global__ __launch_bounds__(256) void k_gram_finish(int b, const double *__restrict__ part, int P,
+                                                     int mode, T *__restrict__ R)
+{
+    __shared__ double g[kMaxB * kMaxB];
+    const int bb = b * b;
+    for (int e = threadIdx.x; e < bb; e += 256) {
+        double s = 0.0;
+        for (int p = 0; p < P; ++p) s += part[(int64_t)p * bb + e];
+        g[e] = s;
+    }
+    __syncthreads();
+    for (int e = threadIdx.x; e < bb; e += 256) {
+        const int i = e / b, j = e % b;
+        const double v = mode ? 0.5 * (g[i * b + j] + g[j * b + i]) : g[e];
+        R[e] = (T)v;
+    }
+}
+
+template <typename T>
+int gram_partials(lz_handle *h, int64_t n, int b, const T *X, const T *Y, int64_t ld, int *nparts)
+{
+    LZ_ARG_CHECK(b >= 1 && b <= kMaxB, "b out of range");
+    if constexpr (std::is_same<T, double>::value) {
+        if (b == 16 && ld == 16) {
+            const int64_t units = ceil_div(ceil_div(n, 4), 8);
+            const int grid = (int)std::max<int64_t>(1, std::min<int64_t>(units, h->n_cu));
+            if (X == Y)
+                {
+                const int ev_ = prof_begin(h, PROF_GRAM);
+                hipLaunchKernelGGL((k_gram16_f64<true>), dim3(grid), dim3(512), 0, h->stream, n, X,
+                                   Y, h->partials);
+                prof_end(h, ev_);
+                }
+            else
+                {
+                const int ev_ = prof_begin(h, PROF_GRAM);
+                hipLaunchKernelGGL((k_gram16_f64<false>), dim3(grid), dim3(512), 0, h->stream, n,
+                                   X, Y, h->partials);
+                prof_end(h, ev_);
+                }
+            LZ_LAUNCH_CHECK();
+            *nparts = grid;
+            return LZ_OK;
+        }
+    }
+    const int64_t units = ceil_div(n, 16);
+    const int grid = (int)std::max<int64_t>(1, std::min<int64_t>(units, (int64_t)h->n_cu * 2));
+    {
+    const int ev_ = prof_begin(h, PROF_GRAM);
+    hipLaunchKernelGGL((k_gram_gen<T>), dim3(grid), dim3(256), 0, h->stream, n, b, X, Y, ld,
+                       h->partials);
+    prof_end(h, ev_);
+    }
+    LZ_LAUNCH_CHECK();
+    *nparts = grid;
+    return LZ_OK;
+}
+
+template <typename T>
+int gram_finish(lz_handle *h, int b, int nparts, int mode, T *R, const double *slabs)
+{
+    {
+    const int ev_ = prof_begin(h, PROF_SMALL);
+    hipLaunchKernelGGL((k_gram_finish<T>), dim3(1), dim3(256), 0, h->stream, b,
+                       slabs ? slabs : h->partials, nparts, mode, R);
+    prof_end(h, ev_);
+    }
+    LZ_LAUNCH_CHECK();
+    return LZ_OK;
+}
+
+// ============================================================ sqrtm (Jacobi)
+// One workgroup.  Parallel (round-robin ordered) cyclic Jacobi on the b x b
+// symmetric matrix in LDS: each round applies b/2 disjoint rotations at once,
+// every element of A' = J^T A J and V' = V J computed by one thread from the
+// previous buffers (ping-pong, two barriers per round).  Then
+// beta = V sqrt|L| V^T and beta_inv = V |L|^-1/2 V^T as custom_mult2
+// (utils/lib_utils.hpp:649-694), which takes |lambda| exactly like this.
+template <typename T>
+__global__ __launch_bounds__(256) void k_sqrtm(int b, const T *__restrict__ Gin,
+                                               const double *__restrict__ part, int P,
+                                               T *__restrict__ beta, T *__restrict__ binv,
+                                               T *__restrict__ eig)
+{
+    constexpr int MB = 32;
+    __shared__ double Abuf[2][MB * MB], Vbuf[2][MB * MB];
+    __shared__ double cc[MB], ss[MB];
+    __shared__ int partner[MB];
+    __shared__ double red[2][256];
+    const int tid = threadIdx.x, bb = b * b;
+    double *A = Abuf[0], *An = Abuf[1], *V = Vbuf[0], *Vn = Vbuf[1];
+    for (int e = tid; e < bb; e += 256) {
+        double g;
+        if (P > 0) {
+            g = 0.0;
+            for (int p = 0; p < P; ++p) g += part[(int64_t)p * bb + e];
+        } else {
+            g = (double)Gin[e];
+        }
+        An[e] = g;
+    }
+    __syncthreads();
+    // symmetrise from the lower triangle (syevj with CUBLAS_FILL_MODE_LOWER)
+    for (int e = tid; e < bb; e += 256) {
+        const int i = e / b, j = e % b;
+        A[e] = (i < j) ? An[j * b + i] : An[e];
+        V[e] = (i == j) ? 1.0 : 0.0;
+    }
+    __syncthreads();
+    const int bo = b + (b & 1);  // even player count (index b = bye when b odd)
+    for (int sweep = 0; sweep < 40; ++sweep) {
+        double off = 0.0, tot = 0.0;
+        for (int e = tid; e < bb; e += 256) {
+            const double a2 = A[e] * A[e];
+            tot += a2;
+            if (e / b != e % b) off += a2;
+        }
+        red[0][tid] = off;
+        red[1][tid] = tot;
+        __syncthreads();
+        for (int st = 128; st > 0; st >>= 1) {
+            if (tid < st) {
+                red[0][tid] += red[0][tid + st];
+                red[1][tid] += red[1][tid + st];
+            }
+            __syncthreads();
+        }
+        const double offn = red[0][0], totn = red[1][0];
+        __syncthreads();
+        if (!(offn > 1e-300 + 1e-32 * totn)) break;  // block-uniform
+        for (int rnd = 0; rnd < bo - 1; ++rnd) {
+            if (tid < bo / 2) {
+                // circle method: position 0 fixed, others rotate
+                auto at = [&](int pos) { return pos == 0 ? 0 : 1 + (pos - 1 + rnd) % (bo - 1); };
+                int p = at(tid), q = at(bo - 1 - tid);
+                if (p > q) { const int t = p; p = q; q = t; }
+                if (q < b) {
+                    const double apq = A[p * b + q];
+                    double c = 1.0, s = 0.0;
+                    if (apq != 0.0) {
+                        const double tau = (A[q * b + q] - A[p * b + p]) / (2.0 * apq);
+                        const double t = (tau >= 0.0 ? 1.0 : -1.0) /
+                                         (fabs(tau) + sqrt(1.0 + tau * tau));
+                        c = 1.0 / sqrt(1.0 + t * t);
+                        s = t * c;
+                    }
+                    partner[p] = q; cc[p] = c; ss[p] = -s;
+                    partner[q] = p; cc[q] = c; ss[q] = s;
+                } else if (p < b) {
+                    partner[p] = p; cc[p] = 1.0; ss[p] = 0.0;
+                }
+            }
+            __syncthreads();
+            for (int e = tid; e < bb; e += 256) {
+                const int i = e / b, j = e % b;
+                const int ip = partner[i], jp = partner[j];
+                const double ai = cc[i], bi = (ip == i) ? 0.0 : ss[i];
+                const double aj = cc[j], bj = (jp == j) ? 0.0 : ss[j];
+                double v = ai * aj * A[i * b + j];
+                if (bj != 0.0) v += ai * bj * A[i * b + jp];
+                if (bi != 0.0) v += bi * aj * A[ip * b + j];
+                if (bi != 0.0 && bj != 0.0) v += bi * bj * A[ip * b + jp];
+                if ((jp == i && ip == j && i != j)) v = 0.0;  // annihilated pair
+                An[e] = v;
+                double vv = aj * V[i * b + j];
+                if (bj != 0.0) vv += bj * V[i * b + jp];
+                Vn[e] = vv;
+            }
+            __syncthreads();
+            double *t = A; A = An; An = t;
+            t = V; V = Vn; Vn = t;
+        }
+    }
+    // beta = V f(L) V^T
+    for (int e = tid; e < bb; e += 256) {
+        const int i = e / b, j = e % b;
+        double s1 = 0.0, s2 = 0.0;
+        for (int k = 0; k < b; ++k) {
+            const double l = fabs(A[k * b + k]);
+            const double sq = sqrt(l);
+            const double vv = V[i * b + k] * V[j * b + k];
+            s1 += vv * sq;
+            s2 += vv * (1.0 / sq);
+        }
+        if (beta) beta[e] = (T)s1;
+        if (binv) binv[e] = (T)s2;
+    }
+    if (eig && tid < b) {
+        const double lk = A[tid * b + tid];
+        int rank = 0;
+        for (int k = 0; k < b; ++k) {
+            const double lm = A[k * b + k];
+            rank += (lm < lk) || (lm == lk && k < tid);
+        }
+        eig[rank] = (T)lk;
+    }
+}
+
+template <typename T>
+int sqrtm_pair(lz_handle *h, int b, const T *G, int nparts, T *beta, T *beta_inv, T *eig,
+               const double *slabs)
+{
+    LZ_ARG_CHECK(b >= 1 && b <= 32, "sqrtm supports b <= 32");
+    {
+    const int ev_ = prof_begin(h, PROF_SMALL);
+    hipLaunchKernelGGL((k_sqrtm<T>), dim3(1), dim3(256), 0, h->stream, b, G,
+                       slabs ? slabs : h->partials, nparts, beta, beta_inv, eig);
+    prof_end(h, ev_);
+    }
+    LZ_LAUNCH_CHECK();
+    return LZ_OK;
+}
+
+// ==================================================================== Q * S
+__global__ __launch_bounds__(512) void k_tsmm16_f64(int64_t n, double sw, double sq,
+                                                    const double *__restrict__ Q,
+                                                    const double *__restrict__ S,
+                                                    double *__restrict__ W)
+{
+    __shared__ double tile[8][16 * 17];
+    const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+    double *T = tile[w];
+    double sb[4];
+#pragma unroll
+    for (int kc = 0; kc < 4; ++kc) sb[kc] = sq * S[(4 * kc + (lane >> 4)) * 16 + (lane & 15)];
+    const int64_t ntile = ceil_div(n, 16);
+    XcdSched s(ceil_div(ntile, 8));
+    for (int64_t u = s.begin; u < s.end; u += s.step) {
+        const int64_t r0 = (u * 8 + w) * 16;
+        if (r0 >= n) continue;  // wave-uniform
+        const int64_t qrow = r0 + (lane >> 2);
+        double qv[4] = {0.0, 0.0, 0.0, 0.0};
+        if (qrow < n) {
+            const double2 *src = reinterpret_cast<const double2 *>(Q + qrow * 16 + 4 * (lane & 3));
+            const double2 a = src[0], b2 = src[1];
+            qv[0] = a.x; qv[1] = a.y; qv[2] = b2.x; qv[3] = b2.y;
+        }
+        d4_t acc;
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+            const int64_t row = r0 + (lane >> 4) + 4 * r;
+            acc[r] = (sw != 0.0 && row < n) ? sw * W[r0 * 16 + 64 * r + lane] : 0.0;
+        }
+#pragma unroll
+        for (int i = 0; i < 4; ++i) T[(lane >> 2) * 17 + 4 * (lane & 3) + i] = qv[i];
+        wave_lds_sync();
+        double a[4];
+#pragma unroll
+        for (int kc = 0; kc < 4; ++kc) a[kc] = T[(lane & 15) * 17 + 4 * kc + (lane >> 4)];
+        wave_lds_sync();
+#pragma unroll
+        for (int kc = 0; kc < 4; ++kc) acc = mfma16(a[kc], sb[kc], acc);
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+            const int64_t row = r0 + (lane >> 4) + 4 * r;
+            if (row < n) W[r0 * 16 + 64 * r + lane] = acc[r];
+        }
+    }
+}
+
+template <typename T>
+__global__ __launch_bounds__(256) void k_tsmm_gen(int64_t n, int b, T sw, T sq,
+                                                  const T *__restrict__ Q, const T *__restrict__ S,
+                                                  T *__restrict__ W, int64_t ld)
+{
+    constexpr int TR = 16;
+    __shared__ T ssm[kMaxB * kMaxB];
+    __shared__ T qs[TR * kMaxB];
+    const int tid = threadIdx.x;
+    for (int e = tid; e < b * b; e += 256) ssm[e] = S[e];
+    XcdSched s(ceil_div(n, TR));
+    for (int64_t u = s.begin; u < s.end; u += s.step) {
+        __syncthreads();
+        for (int e = tid; e < TR * b; e += 256) {
+            const int r = e / b, c = e % b;
+            const int64_t row = u * TR + r;
+            qs[e] = row < n ? Q[row * ld + c] : T(0);
+        }
+        __syncthreads();
+        for (int e = tid; e < TR * b; e += 256) {
+            const int r = e / b, j = e % b;
+            const int64_t row = u * TR + r;
+            if (row >= n) continue;
+            T acc = T(0);
+            for (int i = 0; i < b; ++i) acc = fma(qs[r * b + i], ssm[i * b + j], acc);
+            T *wp = W + row * ld + j;
+            *wp = (sw == T(0)) ? sq * acc : fma(sw, *wp, sq * acc);
+        }
+    }
+}
+
+template <typename T>
+int tsmm(lz_handle *h, int64_t n, int b, T sw, T sq, const T *Q, const T *S, T *W, int64_t ld)
+{
+    LZ_ARG_CHECK(b >= 1 && b <= kMaxB && ld >= b, "tsmm shape");
+    if (n <= 0) return LZ_OK;
+    if constexpr (std::is_same<T, double>::value) {
+        if (b == 16 && ld == 16) {
+            const int64_t units = ceil_div(ceil_div(n, 16), 8);
+            const int grid = (int)std::max<int64_t>(1, std::min<int64_t>(units, h->n_cu * 2));
+            {
+            const int ev_ = prof_begin(h, PROF_TSMM);
+            hipLaunchKernelGGL(k_tsmm16_f64, dim3(grid), dim3(512), 0, h->stream, n, sw, sq, Q, S,
+                               W);
+            prof_end(h, ev_);
+            }
+            LZ_LAUNCH_CHECK();
+            return LZ_OK;
+        }
+    }
+    const int64_t units = ceil_div(n, 16);
+    const int grid = (int)std::max<int64_t>(1, std::min<int64_t>(units, (int64_t)h->n_cu * 4));
+    {
+    const int ev_ = prof_begin(h, PROF_TSMM);
+    hipLaunchKernelGGL((k_tsmm_gen<T>), dim3(grid), dim3(256), 0, h->stream, n, b, sw, sq, Q, S, W,
+                       ld);
+    prof_end(h, ev_);
+    }
+    LZ_LAUNCH_CHECK();
+    return LZ_OK;
+}
+
+// ================================================================ row probe
+template <typename T>
+__global__ void k_copy_row(int b, const T *__restrict__ Q, int64_t ld, int col_major, int64_t lc,
+                           T *__restrict__ q)
+{
+    const int c = threadIdx.x;
+    if (c < b) q[c] = col_major ? Q[lc + c * ld] : Q[lc * ld + c];
+}
+
+template <typename T>
+int copy_row(lz_handle *h, int b, const T *Q, int64_t ld, int col_major, int64_t lc, T *q)
+{
+    hipLaunchKernelGGL((k_copy_row<T>), dim3(1), dim3(64), 0, h->stream, b, Q, ld, col_major, lc,
+                       q);
+    LZ_LAUNCH_CHECK();
+    return LZ_OK;
+}
+
+#define LZ_DENSE_INST(T)                                                                       \
+    template int gram_partials<T>(lz_handle *, int64_t, int, const T *, const T *, int64_t,    \
+                                  int *);                                                      \
+    template int gram_finish<T>(lz_handle *, int, int, int, T *, const double *);              \
+    template int sqrtm_pair<T>(lz_handle *, int, const T *, int, T *, T *, T *, const double *);\
+    template int tsmm<T>(lz_handle *, int64_t, int, T, T, const T *, const T *, T *, int64_t); \
+    template int copy_row<T>(lz_handle *, int, const T *, int64_t, int, int64_t, T *);
+LZ_DENSE_INST(double)
+LZ_DENSE_INST(float)
+
+}  // namespace lz

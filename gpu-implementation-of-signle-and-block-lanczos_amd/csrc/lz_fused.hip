@@ -1,0 +1,385 @@
+// lz_fused.hip -- fused block-Lanczos passes (b = 16, fp64) and the fused
+// single-vector Lanczos passes, gfx950.
+//
+// The reference iteration (methods/block_lanczos.hpp:131-166) is seven
+// library calls per step, moving ~A + 13 n*b*8 bytes.  Here one step is two
+// streaming passes plus two one-workgroup kernels:
+//
+//   pass 1  k_fused_spmm16   Y = A*W (gather),  Q_j[r] = W[r]*beta_j^-1,
+//                            W'[r] = Y[r]*beta_j^-1 - Q_{j-1}[r]*beta_j,
+//                            slabs of Q_j^T W'            (A + ~5 n*b*8 bytes)
+//   finish  k_gram_finish    alpha_j = 0.5 (M + M^T)
+//   pass 2  k_fused_update16 W' -= Q_j*alpha_j, slabs of W'^T W'   (3 n*b*8)
+//   finish  k_sqrtm          beta_{j+1}, beta_{j+1}^-1 = sqrtm(W'^T W')
+//
+// using A*(W*beta^-1) = (A*W)*beta^-1, so the normalised block Q_j is formed
+// in the SpMM epilogue instead of in its own pass.  Q_j overwrites Q_{j-1} in
+// place (row r is read and written by the same wave), the residual alternates
+// between the W and Q1 buffers.  All epilogue products run on
+// v_mfma_f64_16x16x4_f64 (see lz_dense.hip for the operand layouts).
+#include "lz_common.hpp"
+#include "lz_internal.hpp"
+#include "lz_kernels.hpp"
+
+namespace lz {
+
+// load a 16 x 16 row-major fp64 tile starting at row r0 into the wave's LDS
+// tile (row stride 17) and return the MFMA A-operand fragments
+// a[kc] = tile[l & 15][4 kc + (l >> 4)].
+__device__ __forceinline__ void tile_to_aop(double *T, const double *__restrict__ src, int64_t r0,
+                                            int64_t n, int lane, double a[4])
+{
+    const int64_t row = r0 + (lane >> 2);
+    double v[4] = {0.0, 0.0, 0.0, 0.0};
+    if (row < n) {
+        const double2 *s2 = reinterpret_cast<const double2 *>(src + row * 16 + 4 * (lane & 3));
+        const double2 x = s2[0], y = s2[1];
+        v[0] = x.x; v[1] = x.y; v[2] = y.x; v[3] = y.y;
+    }
+#pragma unroll
+    for (int i = 0; i < 4; ++i) T[(lane >> 2) * 17 + 4 * (lane & 3) + i] = v[i];
+    wave_lds_sync();
+#pragma unroll
+    for (int kc = 0; kc < 4; ++kc) a[kc] = T[(lane & 15) * 17 + 4 * kc + (lane >> 4)];
+    wave_lds_sync();
+}
+
+// sum the 8 waves' 16x16 accumulators of the workgroup into its slab
+__device__ __forceinline__ void wg_slab(double (*red)[256], d4_t acc, int lane, int w,
+                                        double *__restrict__ part)
+{
+#pragma unroll
+    for (int r = 0; r < 4; ++r) red[w][((lane >> 4) + 4 * r) * 16 + (lane & 15)] = acc[r];
+    __syncthreads();
+    if (threadIdx.x < 256) {
+        double s = 0.0;
+#pragma unroll
+        for (int ww = 0; ww < 8; ++ww) s += red[ww][threadIdx.x];
+        part[(int64_t)blockIdx.x * 256 + threadIdx.x] = s;
+    }
+}
+
+__global__ __launch_bounds__(512) void k_fused_spmm16(
+    int64_t n, const int64_t *__restrict__ rp, const int32_t *__restrict__ col,
+    const double *__restrict__ val, const double *__restrict__ Wg,
+    const double *__restrict__ Wown, double *__restrict__ Qbuf,
+    double *__restrict__ Wn, const double *__restrict__ binv, const double *__restrict__ beta,
+    int64_t lc, double *__restrict__ qrow, double *__restrict__ part)
+{
+    __shared__ double tile[8][16 * 17];
+    __shared__ double red[8][256];
+    const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+    const int g = lane >> 3, p = lane & 7;
+    double *T = tile[w];
+    const bool has_prev = beta != nullptr;
+    double bi_op[4], nb_op[4];
+#pragma unroll
+    for (int kc = 0; kc < 4; ++kc) {
+        const int idx = (4 * kc + (lane >> 4)) * 16 + (lane & 15);
+        bi_op[kc] = binv[idx];
+        nb_op[kc] = has_prev ? -beta[idx] : 0.0;
+    }
+    d4_t macc = {0.0, 0.0, 0.0, 0.0};
+    const int64_t ntile = ceil_div(n, 16);
+    XcdSched s(ceil_div(ntile, 8));
+    for (int64_t u = s.begin; u < s.end; u += s.step) {
+        const int64_t r0 = (u * 8 + w) * 16;
+        if (r0 >= n) continue;  // wave-uniform
+        // ---- sparse gather: group g (8 lanes, 16 B each) owns rows r0+g, r0+g+8
+        double y[2][2];
+#pragma unroll
+        for (int rr = 0; rr < 2; ++rr) {
+            const int64_t row = r0 + g + 8 * rr;
+            const bool valid = row < n;
+            const int64_t k0 = valid ? rp[row] : 0, k1 = valid ? rp[row + 1] : 0;
+            double a0 = 0.0, a1 = 0.0;
+            for (int64_t kb = k0; kb < k1; kb += 8) {
+                const int64_t k = kb + p;
+                const bool in = k < k1;
+                const int c = in ? col[k] : 0;
+                const double v = in ? val[k] : 0.0;
+                const int cnt = (int)((k1 - kb) < 8 ? (k1 - kb) : 8);
+                double2 xs[8];
+                double vs[8];
+#pragma unroll
+                for (int t = 0; t < 8; ++t) {
+                    const int ct = __shfl(c, (g << 3) + t, 64);
+                    vs[t] = __shfl(v, (g << 3) + t, 64);
+                    xs[t] = *reinterpret_cast<const double2 *>(Wg + (int64_t)ct * 16 + 2 * p);
+                }
+#pragma unroll
+                for (int t = 0; t < 8; ++t) {
+                    if (t < cnt) {
+                        a0 = fma(vs[t], xs[t].x, a0);
+                        a1 = fma(vs[t], xs[t].y, a1);
+                    }
+                }
+            }
+            y[rr][0] = a0;
+            y[rr][1] = a1;
+        }
+        // ---- Y tile -> A operands
+#pragma unroll
+        for (int rr = 0; rr < 2; ++rr) {
+            T[(g + 8 * rr) * 17 + 2 * p] = y[rr][0];
+            T[(g + 8 * rr) * 17 + 2 * p + 1] = y[rr][1];
+        }
+        wave_lds_sync();
+        double ya[4], wa[4], qa[4] = {0.0, 0.0, 0.0, 0.0};
+#pragma unroll
+        for (int kc = 0; kc < 4; ++kc) ya[kc] = T[(lane & 15) * 17 + 4 * kc + (lane >> 4)];
+        wave_lds_sync();
+        tile_to_aop(T, Wown, r0, n, lane, wa);
+        if (has_prev) tile_to_aop(T, Qbuf, r0, n, lane, qa);
+        // ---- epilogue products on the matrix cores
+        d4_t q1 = {0.0, 0.0, 0.0, 0.0}, wn = {0.0, 0.0, 0.0, 0.0};
+#pragma unroll
+        for (int kc = 0; kc < 4; ++kc) q1 = mfma16(wa[kc], bi_op[kc], q1);
+#pragma unroll
+        for (int kc = 0; kc < 4; ++kc) wn = mfma16(ya[kc], bi_op[kc], wn);
+        if (has_prev) {
+#pragma unroll
+            for (int kc = 0; kc < 4; ++kc) wn = mfma16(qa[kc], nb_op[kc], wn);
+        }
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+            const int64_t row = r0 + (lane >> 4) + 4 * r;
+            if (row < n) {
+                Qbuf[r0 * 16 + 64 * r + lane] = q1[r];
+                Wn[r0 * 16 + 64 * r + lane] = wn[r];
+                if (row == lc) qrow[lane & 15] = q1[r];
+            }
+        }
+#pragma unroll
+        for (int r = 0; r < 4; ++r) macc = mfma16(q1[r], wn[r], macc);
+    }
+    wg_slab(red, macc, lane, w, part);
+}
+
+__global__ __launch_bounds__(512) void k_fused_update16(int64_t n, double *__restrict__ Wn,
+                                                        const double *__restrict__ Q,
+                                                        const double *__restrict__ alpha,
+                                                        double *__restrict__ part)
+{
+    __shared__ double tile[8][16 * 17];
+    __shared__ double red[8][256];
+    const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+    double *T = tile[w];
+    double na_op[4];
+#pragma unroll
+    for (int kc = 0; kc < 4; ++kc) na_op[kc] = -alpha[(4 * kc + (lane >> 4)) * 16 + (lane & 15)];
+    d4_t gacc = {0.0, 0.0, 0.0, 0.0};
+    const int64_t ntile = ceil_div(n, 16);
+    XcdSched s(ceil_div(ntile, 8));
+    for (int64_t u = s.begin; u < s.end; u += s.step) {
+        const int64_t r0 = (u * 8 + w) * 16;
+        if (r0 >= n) continue;
+        d4_t acc;
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+            const int64_t row = r0 + (lane >> 4) + 4 * r;
+            acc[r] = row < n ? Wn[r0 * 16 + 64 * r + lane] : 0.0;
+        }
+        double qa[4];
+        tile_to_aop(T, Q, r0, n, lane, qa);
+#pragma unroll
+        for (int kc = 0; kc < 4; ++kc) acc = mfma16(qa[kc], na_op[kc], acc);
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+            const int64_t row = r0 + (lane >> 4) + 4 * r;
+            if (row < n) Wn[r0 * 16 + 64 * r + lane] = acc[r];
+        }
+#pragma unroll
+        for (int r = 0; r < 4; ++r) gacc = mfma16(acc[r], acc[r], gacc);
+    }
+    wg_slab(red, gacc, lane, w, part);
+}
+
+int fused_spmm16(lz_handle *h, int64_t n, const int64_t *rp, const int32_t *col, const double *val,
+                 const double *Wg, const double *Wown, double *Qbuf, double *Wn, const double *binv,
+                 const double *beta, int64_t lc, double *qrow, int *nparts)
+{
+    const int64_t units = ceil_div(ceil_div(n, 16), 8);
+    const int grid = (int)std::max<int64_t>(1, std::min<int64_t>(units, h->n_cu * 2));
+    const int ev = prof_begin(h, PROF_SPMM_PASS);
+    hipLaunchKernelGGL(k_fused_spmm16, dim3(grid), dim3(512), 0, h->stream, n, rp, col, val, Wg,
+                       Wown, Qbuf, Wn, binv, beta, lc, qrow, h->partials);
+    prof_end(h, ev);
+    LZ_LAUNCH_CHECK();
+    *nparts = grid;
+    return LZ_OK;
+}
+
+int fused_update16(lz_handle *h, int64_t n, double *Wn, const double *Q, const double *alpha,
+                   int *nparts)
+{
+    const int64_t units = ceil_div(ceil_div(n, 16), 8);
+    const int grid = (int)std::max<int64_t>(1, std::min<int64_t>(units, h->n_cu * 2));
+    const int ev = prof_begin(h, PROF_UPDATE_PASS);
+    hipLaunchKernelGGL(k_fused_update16, dim3(grid), dim3(512), 0, h->stream, n, Wn, Q, alpha,
+                       h->partials);
+    prof_end(h, ev);
+    LZ_LAUNCH_CHECK();
+    *nparts = grid;
+    return LZ_OK;
+}
+
+// ===================================================== single-vector Lanczos
+// Two streaming passes per step; the scalar reductions are finished redundantly
+// (same fixed order, so the same bits) by every workgroup of the next pass, so
+// no separate reduction launch and no host round trip:
+//   k_vl_spmv    beta_j = sqrt(sum slabs); q_j[r] = w[r]/beta_j (in place over
+//                q_{j-1}[r] after reading it); w'[r] = (A w)[r]/beta_j -
+//                beta_j q_{j-1}[r]; slabs of w'.q_j
+//   k_vl_update  alpha_j = sum slabs; w' -= alpha_j q_j; slabs of w'.w'
+constexpr int kVlThreads = 512;
+
+__device__ __forceinline__ double block_sum_slabs(const double *__restrict__ part, int P,
+                                                  double *red)
+{
+    double s = 0.0;
+    for (int i = threadIdx.x; i < P; i += blockDim.x) s += part[i];
+    // fixed-shape tree: deterministic for fixed P and blockDim
+    red[threadIdx.x] = s;
+    __syncthreads();
+    for (int st = blockDim.x / 2; st > 0; st >>= 1) {
+        if ((int)threadIdx.x < st) red[threadIdx.x] += red[threadIdx.x + st];
+        __syncthreads();
+    }
+    const double r = red[0];
+    __syncthreads();
+    return r;
+}
+
+__device__ __forceinline__ void block_store_slab(double v, double *red, double *__restrict__ out)
+{
+    red[threadIdx.x] = v;
+    __syncthreads();
+    for (int st = blockDim.x / 2; st > 0; st >>= 1) {
+        if ((int)threadIdx.x < st) red[threadIdx.x] += red[threadIdx.x + st];
+        __syncthreads();
+    }
+    if (threadIdx.x == 0) out[blockIdx.x] = red[0];
+}
+
+// slabs of x.x (start of the recurrence, ||b||^2)
+__global__ __launch_bounds__(kVlThreads) void k_vl_sq(int64_t n, const double *__restrict__ x,
+                                                      double *__restrict__ part)
+{
+    __shared__ double red[kVlThreads];
+    double s = 0.0;
+    for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n;
+         i += (int64_t)gridDim.x * blockDim.x)
+        s = fma(x[i], x[i], s);
+    block_store_slab(s, red, part);
+}
+
+template <int LV>
+__global__ __launch_bounds__(kVlThreads) void k_vl_spmv(
+    int64_t n, const int64_t *__restrict__ rp, const int32_t *__restrict__ col,
+    const double *__restrict__ val, const double *__restrict__ w, double *__restrict__ qbuf,
+    double *__restrict__ wn, const double *__restrict__ part_in, int P, int has_prev, int64_t lc,
+    double *__restrict__ qrow, double *__restrict__ beta_out, double *__restrict__ part_out)
+{
+    __shared__ double red[kVlThreads];
+    const double bsq = block_sum_slabs(part_in, P, red);
+    const double beta = sqrt(bsq), rbeta = 1.0 / beta;
+    if (blockIdx.x == 0 && threadIdx.x == 0) *beta_out = beta;
+    constexpr int RB = kVlThreads / LV;
+    const int gi = threadIdx.x / LV, p = threadIdx.x % LV;
+    double dot = 0.0;
+    XcdSched sch(ceil_div(n, RB));
+    for (int64_t u = sch.begin; u < sch.end; u += sch.step) {
+        const int64_t row = u * RB + gi;
+        const bool valid = row < n;
+        const int64_t k0 = valid ? rp[row] : 0, k1 = valid ? rp[row + 1] : 0;
+        double acc = 0.0;
+        int64_t k = k0 + p;
+        for (; k + LV < k1; k += 2 * LV) {
+            const int c0 = col[k], c1 = col[k + LV];
+            const double v0 = val[k], v1 = val[k + LV];
+            acc = fma(v0, w[c0], acc);
+            acc = fma(v1, w[c1], acc);
+        }
+        if (k < k1) acc = fma(val[k], w[col[k]], acc);
+#pragma unroll
+        for (int off = LV / 2; off > 0; off >>= 1) acc += __shfl_xor(acc, off, 64);
+        if (valid && p == 0) {
+            const double qj = w[row] * rbeta;
+            double wv = acc * rbeta;
+            if (has_prev) wv = fma(-beta, qbuf[row], wv);
+            qbuf[row] = qj;
+            wn[row] = wv;
+            dot = fma(wv, qj, dot);
+            if (row == lc) *qrow = qj;
+        }
+    }
+    block_store_slab(dot, red, part_out);
+}
+
+__global__ __launch_bounds__(kVlThreads) void k_vl_update(int64_t n, double *__restrict__ wn,
+                                                          const double *__restrict__ q,
+                                                          const double *__restrict__ part_in,
+                                                          int P, double *__restrict__ alpha_out,
+                                                          double *__restrict__ part_out)
+{
+    __shared__ double red[kVlThreads];
+    const double alpha = block_sum_slabs(part_in, P, red);
+    if (blockIdx.x == 0 && threadIdx.x == 0) *alpha_out = alpha;
+    double s = 0.0;
+    for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n;
+         i += (int64_t)gridDim.x * blockDim.x) {
+        const double v = fma(-alpha, q[i], wn[i]);
+        wn[i] = v;
+        s = fma(v, v, s);
+    }
+    block_store_slab(s, red, part_out);
+}
+
+int vector_lanczos_dev(lz_handle *h, int64_t n, int64_t nnz, const int64_t *rp, const int32_t *col,
+                       const double *val, int m, int64_t lc, const double *b, double *q,
+                       double *alpha, double *beta, double *q0, double *q1, double *w)
+{
+    const double mean = n > 0 ? (double)nnz / (double)n : 10.0;
+    const int lv = mean <= 5 ? 4 : mean <= 12 ? 8 : mean <= 28 ? 16 : mean <= 60 ? 32 : 64;
+    const int grid = (int)std::max<int64_t>(
+        8, std::min<int64_t>(ceil_div(n, kVlThreads / lv), (int64_t)h->n_cu * 4));
+    const int gridu = (int)std::max<int64_t>(
+        8, std::min<int64_t>(ceil_div(n, kVlThreads), (int64_t)h->n_cu * 4));
+    // slabs: two alternating regions of h->partials
+    double *pa = h->partials, *pb = h->partials + 4096;
+    const int gsq = gridu;
+    hipLaunchKernelGGL(k_vl_sq, dim3(gsq), dim3(kVlThreads), 0, h->stream, n, b, pa);
+    LZ_LAUNCH_CHECK();
+    int P = gsq;
+    const double *wcur = b;
+    double *wbuf[2] = {w, q1};
+    int wi = 0;
+    for (int j = 0; j < m; ++j) {
+        double *wnext = wbuf[wi];
+#define LZ_VL_CASE(LV)                                                                          \
+    case LV:                                                                                    \
+        hipLaunchKernelGGL((k_vl_spmv<LV>), dim3(grid), dim3(kVlThreads), 0, h->stream, n, rp, \
+                           col, val, wcur, q0, wnext, pa, P, j > 0 ? 1 : 0, lc, q + j, beta + j, \
+                           pb);                                                                 \
+        break;
+        switch (lv) {
+            LZ_VL_CASE(4)
+            LZ_VL_CASE(8)
+            LZ_VL_CASE(16)
+            LZ_VL_CASE(32)
+            LZ_VL_CASE(64)
+        }
+#undef LZ_VL_CASE
+        LZ_LAUNCH_CHECK();
+        hipLaunchKernelGGL(k_vl_update, dim3(gridu), dim3(kVlThreads), 0, h->stream, n, wnext, q0,
+                           pb, grid, alpha + j, pa);
+        LZ_LAUNCH_CHECK();
+        P = gridu;
+        wcur = wnext;
+        wi ^= 1;
+    }
+    return LZ_OK;
+}
+
+}  // namespace lz

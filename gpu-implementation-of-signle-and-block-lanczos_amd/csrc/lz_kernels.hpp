@@ -1,0 +1,93 @@
+// lz_kernels.hpp -- device helpers shared by the gfx950 kernels.
+#pragma once
+#include <hip/hip_runtime.h>
+
+#include <cstdint>
+
+namespace lz {
+
+typedef double d4_t __attribute__((ext_vector_type(4)));
+typedef float f4_t __attribute__((ext_vector_type(4)));
+
+// XCD-contiguous work schedule.  Observed (speed only, never correctness):
+// workgroups are dealt round-robin over the 8 XCDs, so block b runs on XCD
+// b % 8.  Giving XCD x the contiguous unit range [U*x/8, U*(x+1)/8) keeps each
+// XCD's private L2 on a sliding window of rows, which is what a banded sparse
+// gather needs.  Every unit is visited exactly once for any grid size.
+struct XcdSched {
+    int64_t begin, end, step;
+    __device__ XcdSched(int64_t units)
+    {
+        const int64_t G = gridDim.x, b = blockIdx.x;
+        if (G < 8) {
+            begin = b; end = units; step = G;
+            return;
+        }
+        const int64_t x = b & 7, k = b >> 3;
+        const int64_t K = (G - x + 7) >> 3;  // blocks on this XCD
+        begin = units * x / 8 + k;
+        end = units * (x + 1) / 8;
+        step = K;
+    }
+};
+
+// wave-private LDS hand-off: make this wave's LDS writes visible to its own
+// later LDS reads (DS ops of one wave complete in order once lgkmcnt drains).
+__device__ __forceinline__ void wave_lds_sync()
+{
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_s_waitcnt(0xc07f);  // lgkmcnt(0)
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+}
+
+// 16-byte (or smaller) vector of VEC elements of T
+template <typename T, int VEC>
+struct Vec {
+    T v[VEC];
+};
+
+template <typename T, int VEC>
+__device__ __forceinline__ Vec<T, VEC> ldv(const T *p)
+{
+    Vec<T, VEC> r;
+    if constexpr (sizeof(T) * VEC == 16) {
+        const uint4 u = *reinterpret_cast<const uint4 *>(p);
+        __builtin_memcpy(&r, &u, 16);
+    } else if constexpr (sizeof(T) * VEC == 8) {
+        const uint2 u = *reinterpret_cast<const uint2 *>(p);
+        __builtin_memcpy(&r, &u, 8);
+    } else {
+#pragma unroll
+        for (int i = 0; i < VEC; ++i) r.v[i] = p[i];
+    }
+    return r;
+}
+
+template <typename T, int VEC>
+__device__ __forceinline__ void stv(T *p, const Vec<T, VEC> &r)
+{
+    if constexpr (sizeof(T) * VEC == 16) {
+        uint4 u;
+        __builtin_memcpy(&u, &r, 16);
+        *reinterpret_cast<uint4 *>(p) = u;
+    } else if constexpr (sizeof(T) * VEC == 8) {
+        uint2 u;
+        __builtin_memcpy(&u, &r, 8);
+        *reinterpret_cast<uint2 *>(p) = u;
+    } else {
+#pragma unroll
+        for (int i = 0; i < VEC; ++i) p[i] = r.v[i];
+    }
+}
+
+// v_mfma_f64_16x16x4_f64: D(16x16) += A(16x4) * B(4x16).
+// Lane l supplies A[l&15][l>>4] and B[l>>4][l&15]; D lane l holds
+// D[(l>>4) + 4*r][l&15], r = 0..3 -- i.e. for each r, element l of a
+// contiguous row-major 4x16 chunk.
+__device__ __forceinline__ d4_t mfma16(double a, double b, d4_t c)
+{
+    return __builtin_amdgcn_mfma_f64_16x16x4f64(a, b, c, 0, 0, 0);
+}
+
+}  // namespace lz

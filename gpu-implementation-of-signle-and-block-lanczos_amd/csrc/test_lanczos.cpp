@@ -1,0 +1,219 @@
+// test_lanczos.cpp -- the reference driver (test_lanczos.cu:131-362) rebuilt on
+// the C ABI: same CLI (-N grid, -m iterations) and output lines, plus
+// options for the block width, the operator and the validation run.
+//
+//   test_lanczos [-N 10] [-m 5] [--block 4] [--vector] [--unfused]
+//                [--matrix matrix_a|banded|powerlaw|file:PATH] [--n ROWS]
+//                [--nnz-per-row 10] [--halfwidth 4096] [--bug-compat-change-order]
+//                [--fdtd-steps 1000000] [--T-end 1] [--lc ROW] [--device 0]
+//
+// Defaults reproduce the reference run: block Lanczos, b = 4 (N_COL), fp64, on
+// the Yee operator of grid N with B from the glibc rand() stream and
+// lc = 1 + rand() % 100 drawn first.
+#include <hip/hip_runtime.h>
+
+#include <chrono>
+#include <cmath>
+#include <cstdio>
+#include <cstdlib>
+#include <cstring>
+#include <string>
+#include <vector>
+
+#include "lz_hip.h"
+#include "lz_host.h"
+
+#define CHECK(x)                                                                        \
+    do {                                                                                \
+        int rc_ = (x);                                                                  \
+        if (rc_ != 0) {                                                                 \
+            std::fprintf(stderr, "%s failed (%d): %s\n", #x, rc_, lz_last_error());     \
+            std::exit(1);                                                               \
+        }                                                                               \
+    } while (0)
+#define HCHECK(x)                                                                       \
+    do {                                                                                \
+        hipError_t e_ = (x);                                                            \
+        if (e_ != hipSuccess) {                                                         \
+            std::fprintf(stderr, "%s: %s\n", #x, hipGetErrorString(e_));                \
+            std::exit(1);                                                               \
+        }                                                                               \
+    } while (0)
+
+struct Csr {
+    int64_t n = 0, nnz = 0;
+    std::vector<int64_t> rp;
+    std::vector<int32_t> col;
+    std::vector<double> val;
+};
+
+static Csr matrix_a(int N, bool bug)
+{
+    int64_t n, slots;
+    CHECK(lzh_matrix_a_shape(N, &n, &slots));
+    std::vector<double> d(slots);
+    std::vector<uint32_t> ix(slots);
+    CHECK(lzh_matrix_a_ell(N, bug ? 1 : 0, d.data(), ix.data()));
+    Csr A;
+    A.n = n;
+    A.rp.resize(n + 1);
+    A.nnz = lzh_ell_to_csr_count(n, 4, d.data(), ix.data(), 0, A.rp.data());
+    A.col.resize(A.nnz);
+    A.val.resize(A.nnz);
+    CHECK(lzh_ell_to_csr_fill(n, 4, d.data(), ix.data(), 0, A.rp.data(), A.col.data(),
+                              A.val.data()));
+    return A;
+}
+
+template <typename T>
+static T *dev_copy(const std::vector<T> &h)
+{
+    T *d = nullptr;
+    HCHECK(hipMalloc(&d, sizeof(T) * std::max<size_t>(1, h.size())));
+    if (!h.empty()) HCHECK(hipMemcpy(d, h.data(), sizeof(T) * h.size(), hipMemcpyHostToDevice));
+    return d;
+}
+
+int main(int argc, char **argv)
+{
+    int N = 10, m = 5, b = 4, device = 0;
+    bool vector = false, unfused = false, bug = false;
+    std::string matrix = "matrix_a";
+    int64_t nrows = 1000000, halfwidth = 4096, fdtd_steps = 0, lc = -1;
+    double npr = 10.0, T_end = 1.0;
+    for (int i = 1; i < argc; ++i) {
+        std::string o = argv[i];
+        auto nxt = [&]() -> const char * {
+            if (i + 1 >= argc) { std::fprintf(stderr, "missing value for %s\n", o.c_str()); std::exit(2); }
+            return argv[++i];
+        };
+        if (o == "-N") N = (int)std::stod(nxt());
+        else if (o == "-m") m = (int)std::stod(nxt());
+        else if (o == "--block") b = std::atoi(nxt());
+        else if (o == "--vector") vector = true;
+        else if (o == "--unfused") unfused = true;
+        else if (o == "--matrix") matrix = nxt();
+        else if (o == "--n") nrows = (int64_t)std::stod(nxt());
+        else if (o == "--nnz-per-row") npr = std::stod(nxt());
+        else if (o == "--halfwidth") halfwidth = (int64_t)std::stod(nxt());
+        else if (o == "--bug-compat-change-order") bug = true;
+        else if (o == "--fdtd-steps") fdtd_steps = (int64_t)std::stod(nxt());
+        else if (o == "--T-end") T_end = std::stod(nxt());
+        else if (o == "--lc") lc = (int64_t)std::stod(nxt());
+        else if (o == "--device") device = std::atoi(nxt());
+        else { std::fprintf(stderr, "unknown option %s\n", o.c_str()); return 2; }
+    }
+    if (vector) b = 1;
+    if (lc < 0) lc = lzh_rand_lc(1);  // 1 + rand() % 100, test_lanczos.cu:326
+
+    Csr A;
+    if (matrix == "matrix_a") {
+        A = matrix_a(N, bug);
+    } else if (matrix == "banded" || matrix == "powerlaw") {
+        A.n = nrows;
+        A.rp.resize(nrows + 1);
+        A.nnz = matrix == "banded"
+                    ? lzh_gen_banded_count(nrows, npr, halfwidth, 20261015ULL, A.rp.data())
+                    : lzh_gen_powerlaw_count(nrows, npr, 2.1, 100000, 20261015ULL, A.rp.data());
+        A.col.resize(A.nnz);
+        A.val.resize(A.nnz);
+        if (matrix == "banded")
+            CHECK(lzh_gen_banded_fill(nrows, npr, halfwidth, 20261015ULL, A.rp.data(),
+                                      A.col.data(), A.val.data(), nullptr));
+        else
+            CHECK(lzh_gen_powerlaw_fill(nrows, npr, 2.1, 100000, 20261015ULL, A.rp.data(),
+                                        A.col.data(), A.val.data(), nullptr));
+    } else if (matrix.rfind("file:", 0) == 0) {
+        const std::string path = matrix.substr(5);
+        int64_t nc;
+        int dt;
+        CHECK(lzh_csr_read_header(path.c_str(), &A.n, &nc, &A.nnz, &dt));
+        if (dt != 0) { std::fprintf(stderr, "file must hold fp64 values\n"); return 2; }
+        A.rp.resize(A.n + 1);
+        A.col.resize(A.nnz);
+        A.val.resize(A.nnz);
+        CHECK(lzh_csr_read(path.c_str(), A.rp.data(), A.col.data(), A.val.data()));
+    } else {
+        std::fprintf(stderr, "unknown --matrix %s\n", matrix.c_str());
+        return 2;
+    }
+    const int64_t n = A.n;
+    if (lc >= n) lc = n - 1;
+    std::printf(" the size of the problem is \n%lld\n", (long long)n);
+
+    // B: glibc rand() stream after the lc draw (random_matrix_B), row-major n x b
+    std::vector<double> B((size_t)n * b);
+    CHECK(lzh_rand_B(n, b, 1, 1, 1, B.data()));
+
+    lz_handle *h = nullptr;
+    CHECK(lz_init(device, &h));
+    int64_t *d_rp = dev_copy(A.rp);
+    int32_t *d_col = dev_copy(A.col);
+    double *d_val = dev_copy(A.val);
+    double *d_B = dev_copy(B);
+    double *d_q0, *d_q1, *d_w, *d_q, *d_alpha, *d_beta;
+    const size_t blk = sizeof(double) * n * b;
+    HCHECK(hipMalloc(&d_q0, blk));
+    HCHECK(hipMalloc(&d_q1, blk));
+    HCHECK(hipMalloc(&d_w, blk));
+    HCHECK(hipMalloc(&d_q, sizeof(double) * m * b));
+    HCHECK(hipMalloc(&d_alpha, sizeof(double) * m * b * b));
+    HCHECK(hipMalloc(&d_beta, sizeof(double) * (m + 1) * b * b));
+    HCHECK(hipDeviceSynchronize());
+
+    std::printf(" start Lanczos \n");
+    auto t0 = std::chrono::steady_clock::now();
+    if (vector)
+        CHECK(lz_vector_lanczos(h, n, A.nnz, d_rp, d_col, d_val, LZ_F64, m, lc, d_B, d_q, d_alpha,
+                                d_beta, d_q0, d_q1, d_w));
+    else if (unfused)
+        CHECK(lz_block_lanczos_unfused(h, n, A.nnz, d_rp, d_col, d_val, LZ_F64, b, m, lc, d_B, d_q,
+                                       d_alpha, d_beta, d_q0, d_q1, d_w));
+    else
+        CHECK(lz_block_lanczos(h, n, A.nnz, d_rp, d_col, d_val, LZ_F64, b, m, lc, d_B, d_q,
+                               d_alpha, d_beta, d_q0, d_q1, d_w));
+    HCHECK(hipDeviceSynchronize());
+    auto t1 = std::chrono::steady_clock::now();
+    std::printf(" end Lanczos \n");
+    std::printf("elapsed time: %11.6f\n", std::chrono::duration<double>(t1 - t0).count());
+
+    std::vector<double> q(m * b), alpha(m * b * b), beta((m + 1) * b * b);
+    HCHECK(hipMemcpy(q.data(), d_q, sizeof(double) * q.size(), hipMemcpyDeviceToHost));
+    HCHECK(hipMemcpy(alpha.data(), d_alpha, sizeof(double) * alpha.size(), hipMemcpyDeviceToHost));
+    HCHECK(hipMemcpy(beta.data(), d_beta, sizeof(double) * beta.size(), hipMemcpyDeviceToHost));
+    if (vector) {
+        // scalar recurrence: beta[0] = ||b||; T off-diagonal = beta[1..]
+        std::vector<double> bsc(m);
+        for (int j = 0; j < m; ++j) bsc[j] = beta[j];
+        beta.assign(bsc.begin(), bsc.end());
+        beta.push_back(0.0);
+    }
+    std::vector<double> ritz(m * b), sol(b);
+    CHECK(lzh_ritz_values(m, b, alpha.data(), beta.data(), ritz.data()));
+    CHECK(lzh_block_solution(m, b, T_end, alpha.data(), beta.data(), q.data(), sol.data()));
+    std::printf("Ritz values (%d):", m * b);
+    for (double r : ritz) std::printf(" %.15e", r);
+    std::printf("\nSolution for block lanczos\n");
+    for (double s : sol) std::printf("%.15e\n", s);
+
+    if (fdtd_steps > 0) {
+        std::printf(" start fdtd \n");
+        double *d_out;
+        HCHECK(hipMalloc(&d_out, sizeof(double) * b));
+        CHECK(lz_fdtd_block(h, n, A.nnz, d_rp, d_col, d_val, LZ_F64, b, d_B, fdtd_steps, T_end, lc,
+                            d_q0, d_q1, d_out));
+        std::vector<double> fd(b);
+        HCHECK(hipMemcpy(fd.data(), d_out, sizeof(double) * b, hipMemcpyDeviceToHost));
+        std::printf("Solution from fdtd\n");
+        double num = 0, den = 0;
+        for (int c = 0; c < b; ++c) {
+            std::printf("%.15e\n", fd[c]);
+            num += (sol[c] - fd[c]) * (sol[c] - fd[c]);
+            den += fd[c] * fd[c];
+        }
+        std::printf("Relative error for block lanczos is %.6e\n", std::sqrt(num / den));
+        HCHECK(hipFree(d_out));
+    }
+    lz_finalize(h);
+    return 0;
+}

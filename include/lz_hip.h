@@ -1,0 +1,177 @@
+/* include/lz_hip.h -- C ABI of liblz_hip.so, the MI355X (gfx950) Lanczos hot path.
+ *
+ * Drop-in boundary for the reference's header-only operator API
+ * (ibrohimmn1994/GPU-implementation-of-signle-and-block-Lanczos, paths relative
+ * to source/).  Each entry point names the reference interface it replaces.
+ *
+ * Conventions (all entry points):
+ *   - return 0 on success, a negative LZ_E* code on failure; lz_last_error()
+ *     gives a message (thread-local).  No exceptions cross the ABI.
+ *   - every array argument is a DEVICE pointer owned by the caller unless the
+ *     comment says "host"; sizes are element counts.
+ *   - work is enqueued on the handle's stream (lz_set_stream; default: the
+ *     legacy null stream) and is asynchronous unless stated otherwise.
+ *   - sparse operator: CSR, int64 row_ptr[n_rows+1], int32 col[nnz], values in
+ *     `dtype`.  Dense blocks ("tall-skinny", n x b) are ROW-MAJOR with leading
+ *     dimension ld >= b (element (r,c) at r*ld + c) unless a layout argument says
+ *     LZ_COL_MAJOR (the reference's Dense_matrix layout, element at r + c*ld).
+ *   - b x b matrices (alpha, beta, S) are row-major b*b; every one the Lanczos
+ *     iteration produces is symmetric, so they equal the reference's
+ *     column-major storage element for element.
+ */
+#ifndef LZ_HIP_H
+#define LZ_HIP_H
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+typedef enum { LZ_F64 = 0, LZ_F32 = 1 } lz_dtype;
+typedef enum { LZ_ROW_MAJOR = 0, LZ_COL_MAJOR = 1 } lz_layout;
+
+enum {
+    LZ_OK = 0,
+    LZ_E_ARG = -1,      /* invalid argument (shape, null pointer, unsupported b/dtype) */
+    LZ_E_HIP = -2,      /* HIP runtime error (includes "no device") */
+    LZ_E_COMM = -3,     /* RCCL error */
+    LZ_E_STATE = -4     /* handle not initialised / wrong call order */
+};
+
+typedef struct lz_handle lz_handle;  /* opaque */
+
+/* ---------------------------------------------------------------- runtime */
+/* Replaces the implicit CUDA context + cublasCreate/initiate_cusolver of the
+ * driver (test_lanczos.cu:224-236, utils/lib_utils.hpp:777-805).  Allocates the
+ * handle's small device workspace (partial sums, b x b scratch). */
+int lz_init(int device, lz_handle **h);
+int lz_finalize(lz_handle *h);
+int lz_set_stream(lz_handle *h, void *hip_stream);
+const char *lz_last_error(void);
+const char *lz_version(void);
+/* 1 when a gfx950 device is visible and the code object loads on it. */
+int lz_device_ok(int device);
+
+/* Per-kernel-class timing with hipEvents recorded on the handle's stream
+ * around every launch of the class (no host synchronisation; read after the
+ * work).  Classes: 0 fused SpMM pass, 1 fused update pass, 2 one-workgroup
+ * finish/sqrtm kernels, 3 Gram slabs, 4 tall x small products, 5 plain SpMM.
+ * lz_prof_enable resets the record (capacity 4096 launches). */
+int lz_prof_enable(lz_handle *h, int on);
+int lz_prof_read(lz_handle *h, int kernel_class, double *ms_total, int *count);
+
+/* ----------------------------------------------------------- sparse kernels */
+/* Y = A*X with b columns.  Replaces spmm(Ell_matrix<T>&, Dense_matrix<T>&,
+ * Dense_matrix<T>&) (kernels/spmv_spmm.hpp:262-333, kernel :137-199) and,
+ * at b == 1, spmv(Ell_matrix<T>&, Vector<T>&, Vector<T>&) (:209-260, kernel
+ * :105-135).  Row-major X/Y: b in {1,2,4,8,16,32,64}; column-major: any b<=64.
+ * X has n_cols rows, Y has n_rows rows. */
+int lz_csr_spmm(lz_handle *h, int64_t n_rows, int64_t n_cols, int64_t nnz,
+                const int64_t *row_ptr, const int32_t *col, const void *val, lz_dtype dtype,
+                int b, const void *X, int64_t ldx, lz_layout layout, void *Y, int64_t ldy);
+
+/* y = A*x  (spmv, kernels/spmv_spmm.hpp:209-260) */
+int lz_csr_spmv(lz_handle *h, int64_t n_rows, int64_t n_cols, int64_t nnz,
+                const int64_t *row_ptr, const int32_t *col, const void *val, lz_dtype dtype,
+                const void *x, void *y);
+
+/* ------------------------------------------------ tall-skinny dense kernels */
+/* R = W^T W  (b x b, written to device R).  Replaces mm_tt_cublas
+ * (utils/lib_utils.hpp:102-123) / tt::mm_tt (kernels/mm_tt.hpp:5-179).
+ * Deterministic (fixed-order two-stage reduction, no float atomics). */
+int lz_gram(lz_handle *h, int64_t n, int b, lz_dtype dtype, const void *W, int64_t ld, void *R);
+
+/* R = 0.5 (W^T Q + Q^T W).  Replaces mm_tt2_cublas (lib_utils.hpp:164-202) /
+ * tt2::mm_tt2 (kernels/mm_tt2.hpp:14-210). */
+int lz_sym_cross_gram(lz_handle *h, int64_t n, int b, lz_dtype dtype, const void *W,
+                      const void *Q, int64_t ld, void *R);
+
+/* W = beta*W + alpha*Q*S  (S b x b device).  Replaces mm_cublas(beta, alpha, Q,
+ * S, W) (lib_utils.hpp:28-51) / ts::mm_ts1, mm_ts2 (kernels/mm_ts.hpp:5-273).
+ * beta == 0 never reads W (W may alias nothing; Q must not alias W). */
+int lz_tsmm(lz_handle *h, int64_t n, int b, lz_dtype dtype, double beta, double alpha,
+            const void *Q, const void *S, void *W, int64_t ld);
+
+/* beta <- V sqrt|L| V^T, beta_inv <- V |L|^-1/2 V^T for the symmetric b x b G
+ * (lower triangle read).  Replaces sqrtm_cusolver = cusolverDn{D,S}syevjBatched
+ * + custom_mult2 (lib_utils.hpp:649-745) and sqrtm::My_sqrtm_cusolver
+ * (kernels/my_sqrtm_cusolver.hpp:174-376).  One workgroup, parallel Jacobi.
+ * G may alias beta.  b <= 32.  eigval (device, may be NULL) receives the
+ * ascending eigenvalues of G. */
+int lz_sqrtm_pair(lz_handle *h, int b, lz_dtype dtype, const void *G, void *beta,
+                  void *beta_inv, void *eigval);
+
+/* q[start + c] = Q(lc, c), c < b.  Replaces copy_row_to_vector
+ * (methods/copy_functions.hpp:10-57). */
+int lz_copy_row(lz_handle *h, int b, lz_dtype dtype, const void *Q, int64_t ld, lz_layout layout,
+                int64_t lc, void *q, int64_t start);
+
+/* ------------------------------------------------------------------ methods */
+/* m steps of block Lanczos with symmetric-sqrtm normalisation, no
+ * re-orthogonalisation.  Replaces block_lanczos_blas<T>(A, B, m, lc, q, alpha,
+ * beta, Q0, Q1, W, args, eigen_val, cublasH, n_blocks, n_loads)
+ * (methods/block_lanczos.hpp:88-167); same outputs:
+ *   q[m*b]          row lc of Q_0..Q_{m-1}
+ *   alpha[m*b*b]    alpha_j
+ *   beta[(m+1)*b*b] beta_0 = sqrtm(B^T B), beta_j (j=1..m-1), beta_m = last inverse sqrt
+ * B, Q0, Q1, W: n x b row-major (ld = b), device.  B is read only; Q0/Q1/W are
+ * workspace (the reference passes them pre-set to B; their input content is
+ * ignored here).  Fused device-resident iteration: no host synchronisation
+ * inside; every output stays on the device. */
+int lz_block_lanczos(lz_handle *h, int64_t n, int64_t nnz, const int64_t *row_ptr,
+                     const int32_t *col, const void *val, lz_dtype dtype, int b, int m,
+                     int64_t lc, const void *B, void *q, void *alpha, void *beta, void *Q0,
+                     void *Q1, void *W);
+
+/* Same iteration, reference op order with separate (unfused) kernels: the
+ * structure of block_lanczos_blas one call per line.  For A/B measurement and
+ * as a second GPU path for parity. */
+int lz_block_lanczos_unfused(lz_handle *h, int64_t n, int64_t nnz, const int64_t *row_ptr,
+                             const int32_t *col, const void *val, lz_dtype dtype, int b, int m,
+                             int64_t lc, const void *B, void *q, void *alpha, void *beta,
+                             void *Q0, void *Q1, void *W);
+
+/* Single-vector Lanczos.  Replaces vector_lanczos<T>(A, b, m, lc, q, alpha,
+ * beta, q0, q1, w) (methods/vector_lanczos.hpp:8-67; the correct variant -- the
+ * BLAS variant's axpy at :116 is a reference bug not reproduced).  alpha[m],
+ * beta[m] are DEVICE arrays here (the reference keeps host arrays; copy them
+ * back with one hipMemcpy after the call).  beta[0] = ||b||. */
+int lz_vector_lanczos(lz_handle *h, int64_t n, int64_t nnz, const int64_t *row_ptr,
+                      const int32_t *col, const void *val, lz_dtype dtype, int m, int64_t lc,
+                      const void *bvec, void *q, void *alpha, void *beta, void *q0, void *q1,
+                      void *w);
+
+/* Forward-Euler validation run U += dt*A*U, Nsteps times, then out[c] = U(lc,c).
+ * Replaces ftdt_block (methods/fdtd.hpp:33-56).  U0 n x b row-major; U, D are
+ * n x b workspaces. */
+int lz_fdtd_block(lz_handle *h, int64_t n, int64_t nnz, const int64_t *row_ptr,
+                  const int32_t *col, const void *val, lz_dtype dtype, int b, const void *U0,
+                  int64_t steps, double T_end, int64_t lc, void *U, void *D, void *out);
+
+/* ------------------------------------------------------------ multi-GPU (RCCL)
+ * Row-partitioned block Lanczos: rank g owns rows [row0, row0 + n_local) of A
+ * and of every Krylov block.  New in this build (the reference is single-GPU).
+ * lz_comm_unique_id fills 128 bytes on rank 0; the caller broadcasts them (any
+ * transport) and every rank calls lz_comm_init. */
+int lz_comm_unique_id(unsigned char out[128]);
+int lz_comm_init(lz_handle *h, int nranks, int rank, const unsigned char id[128]);
+int lz_comm_destroy(lz_handle *h);
+
+/* Distributed block Lanczos.  A_local: the rank's n_local rows in CSR with
+ * GLOBAL column indices; X_full: n_global x b row-major workspace that receives
+ * the all-gathered Krylov block every iteration (ncclAllGather over xGMI);
+ * row_counts[nranks] (host) = rows per rank (the all-gather needs equal counts:
+ * every rank passes max(row_counts) as n_pad and pads its slab).  B_local,
+ * Q0,Q1,W: n_local x b.  lc_rank: the rank owning row lc (q written there only;
+ * other ranks' q untouched).  Outputs alpha/beta identical on every rank. */
+int lz_block_lanczos_dist(lz_handle *h, int64_t n_local, int64_t n_pad, int64_t n_global,
+                          int64_t nnz_local, const int64_t *row_ptr, const int32_t *col,
+                          const void *val, lz_dtype dtype, int b, int m, int64_t lc_local,
+                          int lc_rank, const void *B_local, void *q, void *alpha, void *beta,
+                          void *Q0, void *Q1, void *W, void *X_full);
+
+#ifdef __cplusplus
+}
+#endif
+#endif

@@ -1,0 +1,211 @@
+"""GPU parity of the individual hot-path kernels (liblz_hip.so through the C ABI)
+against the CPU oracle / exact numpy references.
+
+Tolerances: fp64 results of a sum of k products are compared with
+|gpu - ref| <= 64 * eps * sum|terms| (reordered summation, FMA), fp32 likewise
+with the fp32 eps.  Integer/index work (row probe) is bit-exact.
+"""
+import numpy as np
+import pytest
+
+from conftest import golden_csr
+
+pytestmark = pytest.mark.gpu
+
+EPS = {np.float64: np.finfo(np.float64).eps, np.float32: np.finfo(np.float32).eps}
+
+
+def spmm_bound(A, X):
+    absA = A.__class__(A.n, A.row_ptr, A.col, np.abs(A.val))
+    return absA, np.abs(X)
+
+
+def dense_of(A):
+    import scipy.sparse as sp
+    return sp.csr_matrix((A.val.astype(np.float64), A.col, A.row_ptr), shape=(A.n, A.n))
+
+
+def check_spmm(lz, orc, h, torch, A, b, dtype, layout="row"):
+    rng = np.random.default_rng(b * 7 + A.n)
+    X = rng.uniform(-1, 1, (A.n, b)).astype(dtype)
+    Ad = lz.CsrDevice.from_host(lz.CsrHost(A.n, A.row_ptr, A.col, A.val.astype(dtype)))
+    M = dense_of(A)
+    ref = M @ X.astype(np.float64)
+    bound = abs(M) @ np.abs(X.astype(np.float64))
+    if layout == "row":
+        Xd = torch.from_numpy(X).cuda()
+        Yd = torch.full((A.n, b), np.nan, dtype=Xd.dtype, device="cuda")
+        h.spmm(Ad, Xd, Yd)
+        Y = Yd.cpu().numpy()
+    else:  # column-major (the reference's Dense_matrix layout): tensors (b, n)
+        Xd = torch.from_numpy(np.ascontiguousarray(X.T)).cuda()
+        Yd = torch.full((b, A.n), np.nan, dtype=Xd.dtype, device="cuda")
+        h.spmm(Ad, Xd, Yd, layout=lz.LZ_COL_MAJOR)
+        Y = Yd.cpu().numpy().T
+    tol = 64 * EPS[dtype] * bound + 1e-300
+    assert np.all(np.abs(Y - ref) <= tol), f"b={b} {dtype} max err {np.max(np.abs(Y - ref))}"
+    if dtype == np.float64 and layout == "row":
+        Yo = orc.csr_spmm(A, X)
+        assert np.all(np.abs(Y - Yo) <= tol)
+
+
+@pytest.mark.parametrize("b", [1, 2, 4, 8, 16, 32])
+def test_spmm_rowmajor_f64(lz, orc, handle, torch_cuda, b):
+    A = lz.gen_banded(20011, 10.0, 500, seed=3)
+    check_spmm(lz, orc, handle, torch_cuda, A, b, np.float64)
+
+
+@pytest.mark.parametrize("b", [4, 8, 16, 32])
+def test_spmm_rowmajor_f32(lz, orc, handle, torch_cuda, b):
+    A = lz.gen_banded(9001, 12.0, 300, seed=5)
+    check_spmm(lz, orc, handle, torch_cuda, A, b, np.float32)
+
+
+@pytest.mark.parametrize("b", [1, 4, 5])
+def test_spmm_colmajor(lz, orc, handle, torch_cuda, b):
+    A = lz.gen_banded(3001, 8.0, 100, seed=9)
+    check_spmm(lz, orc, handle, torch_cuda, A, b, np.float64, layout="col")
+
+
+def test_spmm_matrix_a_and_bug_compat(lz, orc, handle, torch_cuda, golden):
+    for bug in (False, True):
+        A = golden_csr(lz, golden, 10, bug)
+        check_spmm(lz, orc, handle, torch_cuda, A, 4, np.float64)
+        check_spmm(lz, orc, handle, torch_cuda, A, 16, np.float64)
+
+
+def test_spmm_edge_cases(lz, orc, handle, torch_cuda):
+    # empty rows, a dense row, n = 1, nnz = 0
+    rng = np.random.default_rng(1)
+    n = 777
+    rows = []
+    for r in range(n):
+        k = 0 if r % 5 == 0 else (n if r == 3 else rng.integers(1, 20))
+        rows.append(np.sort(rng.choice(n, size=min(k, n), replace=False)))
+    rp = np.zeros(n + 1, np.int64)
+    rp[1:] = np.cumsum([len(c) for c in rows])
+    col = np.concatenate(rows).astype(np.int32)
+    val = rng.uniform(-1, 1, col.size)
+    A = lz.CsrHost(n, rp, col, val)
+    for b in (1, 4, 16, 32):
+        check_spmm(lz, orc, handle, torch_cuda, A, b, np.float64)
+    one = lz.CsrHost(1, np.array([0, 1], np.int64), np.array([0], np.int32), np.array([2.5]))
+    check_spmm(lz, orc, handle, torch_cuda, one, 16, np.float64)
+    empty = lz.CsrHost(5, np.zeros(6, np.int64), np.zeros(0, np.int32), np.zeros(0))
+    check_spmm(lz, orc, handle, torch_cuda, empty, 16, np.float64)
+
+
+def test_spmv(lz, orc, handle, torch_cuda):
+    torch = torch_cuda
+    for npr in (3.0, 10.0, 40.0, 100.0):
+        A = lz.gen_banded(10007, npr, 2000, seed=int(npr))
+        x = np.random.default_rng(2).uniform(-1, 1, A.n)
+        Ad = lz.CsrDevice.from_host(A)
+        y = torch.empty(A.n, dtype=torch.float64, device="cuda")
+        handle.spmv(Ad, torch.from_numpy(x).cuda(), y)
+        ref = orc.csr_spmm(A, x)[:, 0]
+        bound = abs(dense_of(A)) @ np.abs(x)
+        assert np.all(np.abs(y.cpu().numpy() - ref) <= 64 * EPS[np.float64] * bound)
+
+
+@pytest.mark.parametrize("b,n", [(16, 100003), (16, 13), (4, 5003), (8, 777), (32, 4099), (1, 1000)])
+def test_gram_and_cross_gram(lz, handle, torch_cuda, b, n):
+    torch = torch_cuda
+    rng = np.random.default_rng(b + n)
+    W = rng.uniform(-1, 1, (n, b))
+    Q = rng.uniform(-1, 1, (n, b))
+    Wd, Qd = torch.from_numpy(W).cuda(), torch.from_numpy(Q).cuda()
+    R = torch.empty(b, b, dtype=torch.float64, device="cuda")
+    handle.mm_tt(Wd, R)
+    bound = np.abs(W).T @ np.abs(W)
+    assert np.all(np.abs(R.cpu().numpy() - W.T @ W) <= 64 * EPS[np.float64] * bound)
+    handle.mm_tt2(Wd, Qd, R)
+    ref = 0.5 * (W.T @ Q + Q.T @ W)
+    bound = np.abs(W).T @ np.abs(Q) + np.abs(Q).T @ np.abs(W)
+    assert np.all(np.abs(R.cpu().numpy() - ref) <= 64 * EPS[np.float64] * bound)
+
+
+def test_gram_deterministic(lz, handle, torch_cuda):
+    torch = torch_cuda
+    W = torch.from_numpy(np.random.default_rng(5).uniform(-1, 1, (1 << 20, 16))).cuda()
+    R1 = torch.empty(16, 16, dtype=torch.float64, device="cuda")
+    R2 = torch.empty_like(R1)
+    handle.mm_tt(W, R1)
+    handle.mm_tt(W, R2)
+    assert torch.equal(R1, R2)
+
+
+@pytest.mark.parametrize("b,n", [(16, 100003), (16, 7), (4, 999), (32, 3001), (8, 64)])
+@pytest.mark.parametrize("sw", [0.0, 1.0])
+def test_tsmm(lz, handle, torch_cuda, b, n, sw):
+    torch = torch_cuda
+    rng = np.random.default_rng(b * n)
+    Q = rng.uniform(-1, 1, (n, b))
+    S = rng.uniform(-1, 1, (b, b))
+    W0 = rng.uniform(-1, 1, (n, b))
+    Wd = torch.from_numpy(W0.copy()).cuda()
+    handle.mm_ts(sw, -1.0, torch.from_numpy(Q).cuda(), torch.from_numpy(S).cuda(), Wd)
+    ref = sw * W0 - Q @ S
+    bound = np.abs(sw * W0) + np.abs(Q) @ np.abs(S)
+    assert np.all(np.abs(Wd.cpu().numpy() - ref) <= 64 * EPS[np.float64] * bound)
+
+
+def test_tsmm_f32(lz, handle, torch_cuda):
+    torch = torch_cuda
+    rng = np.random.default_rng(3)
+    Q = rng.uniform(-1, 1, (5000, 32)).astype(np.float32)
+    S = rng.uniform(-1, 1, (32, 32)).astype(np.float32)
+    W = torch.zeros(5000, 32, dtype=torch.float32, device="cuda")
+    handle.mm_ts(0.0, 1.0, torch.from_numpy(Q).cuda(), torch.from_numpy(S).cuda(), W)
+    ref = Q.astype(np.float64) @ S.astype(np.float64)
+    bound = np.abs(Q).astype(np.float64) @ np.abs(S).astype(np.float64)
+    assert np.all(np.abs(W.cpu().numpy() - ref) <= 64 * EPS[np.float32] * bound)
+
+
+@pytest.mark.parametrize("b", [1, 2, 3, 4, 7, 16, 32])
+def test_sqrtm_pair(lz, orc, handle, torch_cuda, b):
+    torch = torch_cuda
+    rng = np.random.default_rng(b)
+    X = rng.uniform(-1, 1, (4 * b + 3, b))
+    G = X.T @ X + 1e-3 * np.eye(b)
+    beta = torch.empty(b, b, dtype=torch.float64, device="cuda")
+    binv = torch.empty_like(beta)
+    ev = torch.empty(b, dtype=torch.float64, device="cuda")
+    handle.sqrtm(torch.from_numpy(G).cuda(), beta, binv, ev)
+    s, si = orc.sqrtm_pair(G)
+    scale = np.linalg.norm(G, 2)
+    assert np.max(np.abs(beta.cpu().numpy() - s)) <= 1e-12 * np.sqrt(scale) * b
+    assert np.max(np.abs(binv.cpu().numpy() @ beta.cpu().numpy() - np.eye(b))) <= 1e-10 * np.linalg.cond(G) ** 0.5
+    assert np.allclose(ev.cpu().numpy(), np.linalg.eigvalsh(G), rtol=1e-12, atol=1e-13 * scale)
+
+
+def test_sqrtm_known_answer(lz, handle, torch_cuda, golden):
+    """The 4x4 matrix of kernels/my_sqrtm_solver.cpp:385 (indefinite: |lambda| is used)."""
+    torch = torch_cuda
+    K = golden["ka4_matrix"]
+    beta = torch.empty(4, 4, dtype=torch.float64, device="cuda")
+    binv = torch.empty_like(beta)
+    ev = torch.empty(4, dtype=torch.float64, device="cuda")
+    handle.sqrtm(torch.from_numpy(K).cuda(), beta, binv, ev)
+    assert np.allclose(ev.cpu().numpy(), golden["ka4_eigvals"], rtol=0, atol=1e-13)
+    assert np.allclose(beta.cpu().numpy(), golden["ka4_sqrtm"], rtol=0, atol=1e-13)
+    assert np.allclose(binv.cpu().numpy(), golden["ka4_inv_sqrtm"], rtol=0, atol=1e-12)
+
+
+def test_copy_row_exact(lz, handle, torch_cuda):
+    torch = torch_cuda
+    Q = torch.arange(1000 * 16, dtype=torch.float64, device="cuda").reshape(1000, 16)
+    q = torch.zeros(64, dtype=torch.float64, device="cuda")
+    handle.copy_row_to_vector(84, 16, Q, q)
+    assert torch.equal(q[16:32], Q[84]) and torch.count_nonzero(q[:16]) == 0
+
+
+def test_errors_are_loud(lz, handle, torch_cuda):
+    torch = torch_cuda
+    W = torch.zeros(10, 3, dtype=torch.float64, device="cuda")
+    with pytest.raises(lz.LanczosError):
+        handle.sqrtm(torch.zeros(40, 40, dtype=torch.float64, device="cuda"), W, W)
+    A = lz.CsrDevice.from_host(lz.gen_banded(100, 5.0, 10))
+    with pytest.raises(lz.LanczosError):
+        handle.spmm(A, torch.zeros(100, 3, dtype=torch.float64, device="cuda"),
+                    torch.zeros(100, 3, dtype=torch.float64, device="cuda"))
