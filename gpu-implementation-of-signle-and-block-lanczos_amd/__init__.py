@@ -142,7 +142,16 @@ def hip_lib():
     if _hip is None:
         if not os.path.exists(HIP_LIB):
             raise LanczosError(f"{HIP_LIB} missing: run make in {PKG_DIR}")
-        _hip = _bind(ctypes.CDLL(HIP_LIB, mode=ctypes.RTLD_GLOBAL), HIP_SYMBOLS)
+        # PyTorch bundles its own HIP runtime / RCCL under the same SONAMEs
+        # (libamdhip64.so.7, librccl.so.1).  Import it first so the dynamic
+        # loader resolves liblz_hip.so's dependencies to the copies already in
+        # the process: one HIP runtime per process, shared with torch's
+        # allocator and streams.
+        try:
+            import torch  # noqa: F401
+        except ImportError:
+            pass
+        _hip = _bind(ctypes.CDLL(HIP_LIB), HIP_SYMBOLS)
     return _hip
 
 
@@ -346,6 +355,13 @@ def _torch():
     return torch
 
 
+def _ld(t) -> int:
+    """Leading dimension of a 2-D tensor (stride of a size-1 dim is arbitrary)."""
+    if t.shape[1] > 1 and t.stride(1) != 1:
+        raise LanczosError("inner dimension must be contiguous")
+    return t.stride(0) if t.shape[0] > 1 else t.shape[1]
+
+
 def _ptr(t) -> Optional[int]:
     return None if t is None else t.data_ptr()
 
@@ -423,10 +439,8 @@ class Handle:
     def spmm(self, A: CsrDevice, X, Y, layout: int = LZ_ROW_MAJOR):
         """Y = A*X (kernels/spmv_spmm.hpp:262-333). X/Y (rows, b) row-major tensors, or
         column-major (b, rows) tensors viewed transposed when layout=LZ_COL_MAJOR."""
-        if layout == LZ_ROW_MAJOR:
-            b, ldx, ldy = X.shape[1], X.stride(0), Y.stride(0)
-        else:
-            b, ldx, ldy = X.shape[0], X.stride(0), Y.stride(0)
+        b = X.shape[1] if layout == LZ_ROW_MAJOR else X.shape[0]
+        ldx, ldy = _ld(X), _ld(Y)
         _check(self.L.lz_csr_spmm(self.ptr, A.n, A.n_cols, A.nnz, _ptr(A.row_ptr), _ptr(A.col),
                                   _ptr(A.val), A.dtype, b, _ptr(X), ldx, layout, _ptr(Y), ldy), "lz_csr_spmm")
         return Y
