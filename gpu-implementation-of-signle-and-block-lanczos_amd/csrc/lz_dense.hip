@@ -99,19 +99,56 @@ __global__ __launch_bounds__(256) void k_gram_gen(int64_t n, int b, const T *__r
     }
 }
 
-template <typename T>
-__global__ __launch_bounds__(256) void k_gram_finish(int b, const double *__restrict__ part, int P,
-                                                     int mode, T *__restrict__ R)
+// Fixed-order reduction of P slabs of bb doubles by a 1024-thread workgroup:
+// for bb <= 1024 each entry gets G = 1024/bb threads, thread g summing slabs
+// g, g+G, ... with four independent accumulators (loads in flight), then the
+// G partial sums are added in order g = 0..G-1.  Deterministic for a given
+// (P, bb).  Result in out[bb] (LDS); all threads must call it.
+constexpr int kRedThreads = 1024;
+__device__ void reduce_slabs(const double *__restrict__ part, int P, int bb, double *out,
+                             double *scratch)
 {
-    __shared__ double g[kMaxB * kMaxB];
-    const int bb = b * b;
-    for (int e = threadIdx.x; e < bb; e += 256) {
-        double s = 0.0;
-        for (int p = 0; p < P; ++p) s += part[(int64_t)p * bb + e];
-        g[e] = s;
+    const int t = threadIdx.x;
+    if (bb <= kRedThreads) {
+        const int G = kRedThreads / bb;
+        const int e = t % bb, g = t / bb;
+        double s0 = 0.0, s1 = 0.0, s2 = 0.0, s3 = 0.0;
+        if (g < G) {
+            int p = g;
+            for (; p + 3 * G < P; p += 4 * G) {
+                s0 += part[(int64_t)p * bb + e];
+                s1 += part[(int64_t)(p + G) * bb + e];
+                s2 += part[(int64_t)(p + 2 * G) * bb + e];
+                s3 += part[(int64_t)(p + 3 * G) * bb + e];
+            }
+            for (; p < P; p += G) s0 += part[(int64_t)p * bb + e];
+        }
+        scratch[t] = (s0 + s1) + (s2 + s3);
+        __syncthreads();
+        if (t < bb) {
+            double s = 0.0;
+            for (int gg = 0; gg < G; ++gg) s += scratch[gg * bb + t];
+            out[t] = s;
+        }
+    } else {
+        for (int e = t; e < bb; e += kRedThreads) {
+            double s = 0.0;
+            for (int p = 0; p < P; ++p) s += part[(int64_t)p * bb + e];
+            out[e] = s;
+        }
     }
     __syncthreads();
-    for (int e = threadIdx.x; e < bb; e += 256) {
+}
+
+template <typename T>
+__global__ __launch_bounds__(kRedThreads) void k_gram_finish(int b, const double *__restrict__ part,
+                                                             int P, int mode, T *__restrict__ R)
+{
+    __shared__ double g[kMaxB * kMaxB];
+    __shared__ double scratch[kRedThreads];
+    const int bb = b * b;
+    reduce_slabs(part, P, bb, g, scratch);
+    for (int e = threadIdx.x; e < bb; e += kRedThreads) {
         const int i = e / b, j = e % b;
         const double v = mode ? 0.5 * (g[i * b + j] + g[j * b + i]) : g[e];
         R[e] = (T)v;
@@ -163,7 +200,7 @@ int gram_finish(lz_handle *h, int b, int nparts, int mode, T *R, const double *s
 {
     {
     const int ev_ = prof_begin(h, PROF_SMALL);
-    hipLaunchKernelGGL((k_gram_finish<T>), dim3(1), dim3(256), 0, h->stream, b,
+    hipLaunchKernelGGL((k_gram_finish<T>), dim3(1), dim3(kRedThreads), 0, h->stream, b,
                        slabs ? slabs : h->partials, nparts, mode, R);
     prof_end(h, ev_);
     }
@@ -172,38 +209,36 @@ int gram_finish(lz_handle *h, int b, int nparts, int mode, T *R, const double *s
 }
 
 // ============================================================ sqrtm (Jacobi)
-// One workgroup.  Parallel (round-robin ordered) cyclic Jacobi on the b x b
-// symmetric matrix in LDS: each round applies b/2 disjoint rotations at once,
-// every element of A' = J^T A J and V' = V J computed by one thread from the
-// previous buffers (ping-pong, two barriers per round).  Then
+// One workgroup.  All 1024 threads reduce the Gram slabs; then waves 1..15 exit
+// and wave 0 alone runs a parallel (round-robin ordered) cyclic Jacobi on the
+// b x b symmetric matrix in LDS: each round applies b/2 disjoint rotations at
+// once, every element of A' = J^T A J and V' = V J computed from the previous
+// buffers (ping-pong; a one-wave barrier is nearly free).  Then
 // beta = V sqrt|L| V^T and beta_inv = V |L|^-1/2 V^T as custom_mult2
 // (utils/lib_utils.hpp:649-694), which takes |lambda| exactly like this.
 template <typename T>
-__global__ __launch_bounds__(256) void k_sqrtm(int b, const T *__restrict__ Gin,
-                                               const double *__restrict__ part, int P,
-                                               T *__restrict__ beta, T *__restrict__ binv,
-                                               T *__restrict__ eig)
+__global__ __launch_bounds__(kRedThreads) void k_sqrtm(int b, const T *__restrict__ Gin,
+                                                       const double *__restrict__ part, int P,
+                                                       T *__restrict__ beta, T *__restrict__ binv,
+                                                       T *__restrict__ eig)
 {
     constexpr int MB = 32;
     __shared__ double Abuf[2][MB * MB], Vbuf[2][MB * MB];
     __shared__ double cc[MB], ss[MB];
     __shared__ int partner[MB];
-    __shared__ double red[2][256];
+    __shared__ double scratch[kRedThreads];
     const int tid = threadIdx.x, bb = b * b;
     double *A = Abuf[0], *An = Abuf[1], *V = Vbuf[0], *Vn = Vbuf[1];
-    for (int e = tid; e < bb; e += 256) {
-        double g;
-        if (P > 0) {
-            g = 0.0;
-            for (int p = 0; p < P; ++p) g += part[(int64_t)p * bb + e];
-        } else {
-            g = (double)Gin[e];
-        }
-        An[e] = g;
+    if (P > 0) {
+        reduce_slabs(part, P, bb, An, scratch);
+    } else {
+        for (int e = tid; e < bb; e += kRedThreads) An[e] = (double)Gin[e];
+        __syncthreads();
     }
-    __syncthreads();
+    if (tid >= 64) return;  // the rest is one wave: s_barrier waits only for it
+    constexpr int NT = 64;
     // symmetrise from the lower triangle (syevj with CUBLAS_FILL_MODE_LOWER)
-    for (int e = tid; e < bb; e += 256) {
+    for (int e = tid; e < bb; e += NT) {
         const int i = e / b, j = e % b;
         A[e] = (i < j) ? An[j * b + i] : An[e];
         V[e] = (i == j) ? 1.0 : 0.0;
@@ -212,24 +247,17 @@ __global__ __launch_bounds__(256) void k_sqrtm(int b, const T *__restrict__ Gin,
     const int bo = b + (b & 1);  // even player count (index b = bye when b odd)
     for (int sweep = 0; sweep < 40; ++sweep) {
         double off = 0.0, tot = 0.0;
-        for (int e = tid; e < bb; e += 256) {
+        for (int e = tid; e < bb; e += NT) {
             const double a2 = A[e] * A[e];
             tot += a2;
             if (e / b != e % b) off += a2;
         }
-        red[0][tid] = off;
-        red[1][tid] = tot;
-        __syncthreads();
-        for (int st = 128; st > 0; st >>= 1) {
-            if (tid < st) {
-                red[0][tid] += red[0][tid + st];
-                red[1][tid] += red[1][tid + st];
-            }
-            __syncthreads();
+#pragma unroll
+        for (int o = 32; o > 0; o >>= 1) {
+            off += __shfl_xor(off, o, 64);
+            tot += __shfl_xor(tot, o, 64);
         }
-        const double offn = red[0][0], totn = red[1][0];
-        __syncthreads();
-        if (!(offn > 1e-300 + 1e-32 * totn)) break;  // block-uniform
+        if (!(off > 1e-300 + 1e-32 * tot)) break;  // wave-uniform
         for (int rnd = 0; rnd < bo - 1; ++rnd) {
             if (tid < bo / 2) {
                 // circle method: position 0 fixed, others rotate
@@ -253,7 +281,7 @@ __global__ __launch_bounds__(256) void k_sqrtm(int b, const T *__restrict__ Gin,
                 }
             }
             __syncthreads();
-            for (int e = tid; e < bb; e += 256) {
+            for (int e = tid; e < bb; e += NT) {
                 const int i = e / b, j = e % b;
                 const int ip = partner[i], jp = partner[j];
                 const double ai = cc[i], bi = (ip == i) ? 0.0 : ss[i];
@@ -274,7 +302,7 @@ __global__ __launch_bounds__(256) void k_sqrtm(int b, const T *__restrict__ Gin,
         }
     }
     // beta = V f(L) V^T
-    for (int e = tid; e < bb; e += 256) {
+    for (int e = tid; e < bb; e += NT) {
         const int i = e / b, j = e % b;
         double s1 = 0.0, s2 = 0.0;
         for (int k = 0; k < b; ++k) {
@@ -305,7 +333,7 @@ int sqrtm_pair(lz_handle *h, int b, const T *G, int nparts, T *beta, T *beta_inv
     LZ_ARG_CHECK(b >= 1 && b <= 32, "sqrtm supports b <= 32");
     {
     const int ev_ = prof_begin(h, PROF_SMALL);
-    hipLaunchKernelGGL((k_sqrtm<T>), dim3(1), dim3(256), 0, h->stream, b, G,
+    hipLaunchKernelGGL((k_sqrtm<T>), dim3(1), dim3(kRedThreads), 0, h->stream, b, G,
                        slabs ? slabs : h->partials, nparts, beta, beta_inv, eig);
     prof_end(h, ev_);
     }

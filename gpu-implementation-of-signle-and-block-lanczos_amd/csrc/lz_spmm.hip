@@ -39,40 +39,67 @@ __global__ __launch_bounds__(256) void k_spmm_rm(int64_t n, const int64_t *__res
     const int gi = tid / LPR, p = tid % LPR;
     const int gbase = (tid & 63) / LPR * LPR;
     XcdSched sch(ceil_div(n, RB));
-    for (int64_t u = sch.begin; u < sch.end; u += sch.step) {
-        const int64_t row = u * RB + gi;
-        const bool valid = row < n;
-        const int64_t k0 = valid ? rp[row] : 0, k1 = valid ? rp[row + 1] : 0;
-        T acc[VEC];
+    // Each group walks its rows (u = begin, begin+step, ...) as one stream of
+    // LPR-nnz batches, software-pipelined: the (col,val) pair of the NEXT batch
+    // and the row_ptr pair of the NEXT row are loaded while the current
+    // batch's X rows are gathered, so the only latency on the critical path is
+    // the (mostly L2-resident) X gather.  Control flow is group-uniform.
+    int64_t u = sch.begin;
+    if (u >= sch.end) return;
+    int64_t r = u * RB + gi, k = 0, k1 = 0;
+    if (r < n) { k = rp[r]; k1 = rp[r + 1]; }
+    int64_t un = u + sch.step, rn = un * RB + gi, kn0 = 0, kn1 = 0;
+    if (un < sch.end && rn < n) { kn0 = rp[rn]; kn1 = rp[rn + 1]; }
+    int cN = 0;
+    T vN = T(0);
+    if (k + p < k1) { cN = col[k + p]; vN = val[k + p]; }
+    T acc[VEC];
 #pragma unroll
-        for (int i = 0; i < VEC; ++i) acc[i] = T(0);
-        for (int64_t kb = k0; kb < k1; kb += LPR) {
-            const int64_t k = kb + p;
-            const bool in = k < k1;
-            const int c = in ? col[k] : 0;
-            const T v = in ? val[k] : T(0);
-            const int cnt = (int)((k1 - kb) < LPR ? (k1 - kb) : LPR);
-            Vec<T, VEC> xs[LPR];
-            T vs[LPR];
+    for (int i = 0; i < VEC; ++i) acc[i] = T(0);
+    for (;;) {
+        const int c = cN;
+        const T v = vN;
+        const int64_t rem = k1 - k;
+        const int cnt = rem < LPR ? (int)rem : LPR;
+        const bool last = rem <= LPR;
+        const int64_t rcur = r;
+        if (!last) {
+            k += LPR;
+        } else {  // the next row becomes current; fetch row_ptr of the one after
+            u = un; r = rn; k = kn0; k1 = kn1;
+            un = u + sch.step;
+            rn = un * RB + gi;
+            kn0 = kn1 = 0;
+            if (un < sch.end && rn < n) { kn0 = rp[rn]; kn1 = rp[rn + 1]; }
+        }
+        cN = 0;
+        vN = T(0);
+        if (u < sch.end && k + p < k1) { cN = col[k + p]; vN = val[k + p]; }
+        Vec<T, VEC> xs[LPR];
+        T vs[LPR];
 #pragma unroll
-            for (int t = 0; t < LPR; ++t) {
-                const int ct = (LPR == 1) ? c : __shfl(c, gbase + t, 64);
-                vs[t] = (LPR == 1) ? v : __shfl(v, gbase + t, 64);
-                xs[t] = ldv<T, VEC>(X + (int64_t)ct * ldx + p * VEC);
-            }
+        for (int t = 0; t < LPR; ++t) {
+            const int ct = (LPR == 1) ? c : __shfl(c, gbase + t, 64);
+            vs[t] = (LPR == 1) ? v : __shfl(v, gbase + t, 64);
+            xs[t] = ldv<T, VEC>(X + (int64_t)ct * ldx + p * VEC);
+        }
 #pragma unroll
-            for (int t = 0; t < LPR; ++t) {
-                if (t < cnt) {
+        for (int t = 0; t < LPR; ++t) {
+            if (t < cnt) {
 #pragma unroll
-                    for (int i = 0; i < VEC; ++i) acc[i] = fma(vs[t], xs[t].v[i], acc[i]);
-                }
+                for (int i = 0; i < VEC; ++i) acc[i] = fma(vs[t], xs[t].v[i], acc[i]);
             }
         }
-        if (valid) {
-            Vec<T, VEC> o;
+        if (last) {
+            if (rcur < n) {
+                Vec<T, VEC> o;
 #pragma unroll
-            for (int i = 0; i < VEC; ++i) o.v[i] = acc[i];
-            stv<T, VEC>(Y + row * ldy + p * VEC, o);
+                for (int i = 0; i < VEC; ++i) o.v[i] = acc[i];
+                stv<T, VEC>(Y + rcur * ldy + p * VEC, o);
+            }
+#pragma unroll
+            for (int i = 0; i < VEC; ++i) acc[i] = T(0);
+            if (u >= sch.end) break;
         }
     }
 }
