@@ -24,6 +24,17 @@ int prof_begin(lz_handle *h, int cls)
     return idx;
 }
 
+int ensure_partials(lz_handle *h, size_t doubles)
+{
+    if (doubles <= h->partials_cap) return LZ_OK;
+    LZ_HIP_TRY(hipStreamSynchronize(h->stream));
+    LZ_HIP_TRY(hipFree(h->partials));
+    h->partials = nullptr;
+    LZ_HIP_TRY(hipMalloc(&h->partials, doubles * sizeof(double)));
+    h->partials_cap = doubles;
+    return LZ_OK;
+}
+
 void prof_end(lz_handle *h, int idx)
 {
     if (idx >= 0) (void)hipEventRecord(h->ev_pool[idx + 1], h->stream);
@@ -115,7 +126,7 @@ static int block_lanczos_fused16(lz_handle *h, int64_t n, const int64_t *rp, con
         double *res_out = bufs[j & 1];
         LZ_TRY(fused_spmm16(h, n, rp, col, val, res_in, res_in, Q0, res_out, binv,
                             j ? beta + j * bb : nullptr, lc, q + j * 16, &P));
-        LZ_TRY(gram_finish<double>(h, 16, P, 1, alpha + j * bb));
+        LZ_TRY(gram_finish<double>(h, 16, P, 1, alpha + j * bb, h->partials2));
         LZ_TRY(fused_update16(h, n, res_out, Q0, alpha + j * bb, &P));
         if (j + 1 < m)
             LZ_TRY(sqrtm_pair<double>(h, 16, nullptr, P, beta + (j + 1) * bb, binv, nullptr));
@@ -174,7 +185,7 @@ static int block_lanczos_dist16(lz_handle *h, int64_t n_local, int64_t n_pad, co
     for (int j = 0; j < m; ++j) {
         LZ_TRY(fused_spmm16(h, n_local, rp, col, val, X, own, Q0, W, binv,
                             j ? beta + j * bb : nullptr, lc_local, q + j * 16, &P));
-        LZ_TRY(gram_finish<double>(h, 16, P, 0, slab));
+        LZ_TRY(gram_finish<double>(h, 16, P, 0, slab, h->partials2));
         LZ_NCCL_TRY(ncclAllReduce(slab, slab, bb, ncclDouble, ncclSum, comm, h->stream));
         LZ_TRY(gram_finish<double>(h, 16, 1, 1, alpha + j * bb, slab));
         LZ_TRY(fused_update16(h, n_local, W, Q0, alpha + j * bb, &P));
@@ -234,7 +245,9 @@ int lz_init(int device, lz_handle **out)
         return LZ_E_HIP;
     }
     h->n_cu = prop.multiProcessorCount;
-    LZ_HIP_TRY(hipMalloc(&h->partials, sizeof(double) * (size_t)kMaxPartials * kMaxB * kMaxB));
+    h->partials_cap = (size_t)kMaxPartials * kMaxB * kMaxB;
+    LZ_HIP_TRY(hipMalloc(&h->partials, sizeof(double) * h->partials_cap));
+    LZ_HIP_TRY(hipMalloc(&h->partials2, sizeof(double) * 256 * kMaxB * kMaxB));
     LZ_HIP_TRY(hipMalloc(&h->scratch, sizeof(double) * 8 * kMaxB * kMaxB));
     *out = h;
     return LZ_OK;
@@ -250,6 +263,7 @@ int lz_finalize(lz_handle *h)
         delete[] h->ev_pool;
     }
     (void)hipFree(h->partials);
+    (void)hipFree(h->partials2);
     (void)hipFree(h->scratch);
     delete h;
     return LZ_OK;

@@ -62,7 +62,9 @@ struct lz_handle {
     int n_cu = 256;
     // device workspace: per-workgroup partial b x b sums (double), b x b
     // scratch matrices and a few scalars.
-    double *partials = nullptr;   // kMaxPartials * kMaxB * kMaxB doubles
+    double *partials = nullptr;   // per-workgroup / per-tile slabs (grown on demand)
+    size_t partials_cap = 0;      // doubles
+    double *partials2 = nullptr;  // first-level folded slabs: 256 * kMaxB * kMaxB doubles
     double *scratch = nullptr;    // 8 * kMaxB * kMaxB doubles
     void *comm = nullptr;         // ncclComm_t when lz_comm_init was called
     int nranks = 1, rank = 0;
@@ -80,5 +82,7 @@ enum ProfClass { PROF_SPMM_PASS = 0, PROF_UPDATE_PASS = 1, PROF_SMALL = 2, PROF_
                  PROF_TSMM = 4, PROF_SPMM = 5, PROF_NCLASS = 6 };
 // bracket one launch: returns the event index of the start (-1 when off)
 int prof_begin(lz_handle *h, int cls);
+// grow h->partials to hold at least `doubles` (outside any timed/captured loop)
+int ensure_partials(lz_handle *h, size_t doubles);
 void prof_end(lz_handle *h, int idx);
 }  // namespace lz

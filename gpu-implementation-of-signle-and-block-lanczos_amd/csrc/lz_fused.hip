@@ -59,6 +59,15 @@ __device__ __forceinline__ void wg_slab(double (*red)[256], d4_t acc, int lane, 
     }
 }
 
+// One 128-row tile per block (8 waves x 16 rows), XCD remap (xcd_remap), so
+// the tiles in flight on an XCD stay a narrow window of rows and the banded X
+// gather hits that XCD's L2.  The tile's (col, val) range is staged through LDS
+// with coalesced loads; each group of 8 lanes (16 B each = one 128-B X row)
+// owns rows 16w+g and 16w+g+8 and issues 8 independent X gathers per step.
+// The per-block 16x16 slab of Q_j^T W' goes to part[tile]; lz_fused.hip's
+// k_slab_reduce1 folds the slabs in fixed order.
+constexpr int kFusedRows = 128, kFusedCap = 2048;
+
 __global__ __launch_bounds__(512) void k_fused_spmm16(
     int64_t n, const int64_t *__restrict__ rp, const int32_t *__restrict__ col,
     const double *__restrict__ val, const double *__restrict__ Wg,
@@ -68,6 +77,8 @@ __global__ __launch_bounds__(512) void k_fused_spmm16(
 {
     __shared__ double tile[8][16 * 17];
     __shared__ double red[8][256];
+    __shared__ int32_t cs[kFusedCap];
+    __shared__ double vs[kFusedCap];
     const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
     const int g = lane >> 3, p = lane & 7;
     double *T = tile[w];
@@ -79,45 +90,57 @@ __global__ __launch_bounds__(512) void k_fused_spmm16(
         bi_op[kc] = binv[idx];
         nb_op[kc] = has_prev ? -beta[idx] : 0.0;
     }
-    d4_t macc = {0.0, 0.0, 0.0, 0.0};
-    const int64_t ntile = ceil_div(n, 16);
-    XcdSched s(ceil_div(ntile, 8));
-    for (int64_t u = s.begin; u < s.end; u += s.step) {
-        const int64_t r0 = (u * 8 + w) * 16;
-        if (r0 >= n) continue;  // wave-uniform
-        // ---- sparse gather: group g (8 lanes, 16 B each) owns rows r0+g, r0+g+8
-        double y[2][2];
+    const int64_t u = xcd_remap(blockIdx.x, gridDim.x);
+    const int64_t rb = u * kFusedRows;
+    const int64_t rend = (rb + kFusedRows < n) ? rb + kFusedRows : n;
+    const int64_t kA = rp[rb], kB = rp[rend];
+    const int64_t r0 = rb + 16 * w;  // this wave's 16-row tile
+    int64_t k0[2], k1[2];
+#pragma unroll
+    for (int rr = 0; rr < 2; ++rr) {
+        const int64_t row = r0 + g + 8 * rr;
+        k0[rr] = row < n ? rp[row] : kB;
+        k1[rr] = row < n ? rp[row + 1] : kB;
+    }
+    const double *Xp = Wg + 2 * p;
+    double y[2][2] = {{0.0, 0.0}, {0.0, 0.0}};
+    for (int64_t c0 = kA; c0 < kB; c0 += kFusedCap) {  // block-uniform
+        const int64_t c1 = (c0 + kFusedCap < kB) ? c0 + kFusedCap : kB;
+        if (c0 != kA) __syncthreads();
+        for (int64_t k = c0 + threadIdx.x; k < c1; k += 512) {
+            cs[k - c0] = col[k];
+            vs[k - c0] = val[k];
+        }
+        __syncthreads();
 #pragma unroll
         for (int rr = 0; rr < 2; ++rr) {
-            const int64_t row = r0 + g + 8 * rr;
-            const bool valid = row < n;
-            const int64_t k0 = valid ? rp[row] : 0, k1 = valid ? rp[row + 1] : 0;
-            double a0 = 0.0, a1 = 0.0;
-            for (int64_t kb = k0; kb < k1; kb += 8) {
-                const int64_t k = kb + p;
-                const bool in = k < k1;
-                const int c = in ? col[k] : 0;
-                const double v = in ? val[k] : 0.0;
-                const int cnt = (int)((k1 - kb) < 8 ? (k1 - kb) : 8);
+            const int64_t a = k0[rr] > c0 ? k0[rr] : c0, e = k1[rr] < c1 ? k1[rr] : c1;
+            double a0 = y[rr][0], a1 = y[rr][1];
+            for (int64_t kb = a; kb < e; kb += 8) {
+                const int cnt = (int)((e - kb) < 8 ? (e - kb) : 8);
+                const int base = (int)(kb - c0);
                 double2 xs[8];
-                double vs[8];
+                double vv[8];
 #pragma unroll
                 for (int t = 0; t < 8; ++t) {
-                    const int ct = __shfl(c, (g << 3) + t, 64);
-                    vs[t] = __shfl(v, (g << 3) + t, 64);
-                    xs[t] = *reinterpret_cast<const double2 *>(Wg + (int64_t)ct * 16 + 2 * p);
+                    const int li = base + (t < cnt ? t : 0);
+                    vv[t] = vs[li];
+                    xs[t] = *reinterpret_cast<const double2 *>(Xp + (int64_t)cs[li] * 16);
                 }
 #pragma unroll
                 for (int t = 0; t < 8; ++t) {
                     if (t < cnt) {
-                        a0 = fma(vs[t], xs[t].x, a0);
-                        a1 = fma(vs[t], xs[t].y, a1);
+                        a0 = fma(vv[t], xs[t].x, a0);
+                        a1 = fma(vv[t], xs[t].y, a1);
                     }
                 }
             }
             y[rr][0] = a0;
             y[rr][1] = a1;
         }
+    }
+    d4_t macc = {0.0, 0.0, 0.0, 0.0};
+    if (r0 < n) {  // wave-uniform
         // ---- Y tile -> A operands
 #pragma unroll
         for (int rr = 0; rr < 2; ++rr) {
@@ -153,7 +176,37 @@ __global__ __launch_bounds__(512) void k_fused_spmm16(
 #pragma unroll
         for (int r = 0; r < 4; ++r) macc = mfma16(q1[r], wn[r], macc);
     }
-    wg_slab(red, macc, lane, w, part);
+    // slab of this tile, indexed by tile (row order): fixed-order reduction later
+#pragma unroll
+    for (int r = 0; r < 4; ++r) red[w][((lane >> 4) + 4 * r) * 16 + (lane & 15)] = macc[r];
+    __syncthreads();
+    if (threadIdx.x < 256) {
+        double sum = 0.0;
+#pragma unroll
+        for (int ww = 0; ww < 8; ++ww) sum += red[ww][threadIdx.x];
+        part[u * 256 + threadIdx.x] = sum;
+    }
+}
+
+// First-level fixed-order fold of P slabs (bb doubles each) into gridDim.x
+// slabs: block q sums slabs [q*P/G, (q+1)*P/G) in order.
+__global__ __launch_bounds__(256) void k_slab_reduce1(const double *__restrict__ part, int64_t P,
+                                                      int bb, double *__restrict__ out)
+{
+    const int64_t G = gridDim.x, q = blockIdx.x;
+    const int64_t s0 = q * P / G, s1 = (q + 1) * P / G;
+    for (int e = threadIdx.x; e < bb; e += 256) {
+        double a0 = 0.0, a1 = 0.0, a2 = 0.0, a3 = 0.0;
+        int64_t s = s0;
+        for (; s + 3 < s1; s += 4) {
+            a0 += part[s * bb + e];
+            a1 += part[(s + 1) * bb + e];
+            a2 += part[(s + 2) * bb + e];
+            a3 += part[(s + 3) * bb + e];
+        }
+        for (; s < s1; ++s) a0 += part[s * bb + e];
+        out[q * bb + e] = (a0 + a1) + (a2 + a3);
+    }
 }
 
 __global__ __launch_bounds__(512) void k_fused_update16(int64_t n, double *__restrict__ Wn,
@@ -199,14 +252,22 @@ int fused_spmm16(lz_handle *h, int64_t n, const int64_t *rp, const int32_t *col,
                  const double *Wg, const double *Wown, double *Qbuf, double *Wn, const double *binv,
                  const double *beta, int64_t lc, double *qrow, int *nparts)
 {
-    const int64_t units = ceil_div(ceil_div(n, 16), 8);
-    const int grid = (int)std::max<int64_t>(1, std::min<int64_t>(units, h->n_cu * 2));
+    const int64_t tiles = ceil_div(n, kFusedRows);
+    LZ_ARG_CHECK(tiles >= 1 && tiles < (1LL << 31), "tile count");
+    LZ_TRY(ensure_partials(h, tiles * 256));
     const int ev = prof_begin(h, PROF_SPMM_PASS);
-    hipLaunchKernelGGL(k_fused_spmm16, dim3(grid), dim3(512), 0, h->stream, n, rp, col, val, Wg,
-                       Wown, Qbuf, Wn, binv, beta, lc, qrow, h->partials);
+    hipLaunchKernelGGL(k_fused_spmm16, dim3((unsigned)tiles), dim3(512), 0, h->stream, n, rp, col,
+                       val, Wg, Wown, Qbuf, Wn, binv, beta, lc, qrow, h->partials);
     prof_end(h, ev);
     LZ_LAUNCH_CHECK();
-    *nparts = grid;
+    // fold the per-tile slabs to <= 256 (fixed order) in the second slab buffer
+    const int g1 = (int)std::min<int64_t>(tiles, 256);
+    const int ev2 = prof_begin(h, PROF_SMALL);
+    hipLaunchKernelGGL(k_slab_reduce1, dim3(g1), dim3(256), 0, h->stream, h->partials, tiles, 256,
+                       h->partials2);
+    prof_end(h, ev2);
+    LZ_LAUNCH_CHECK();
+    *nparts = g1;
     return LZ_OK;
 }
 

@@ -31,6 +31,18 @@ struct XcdSched {
     }
 };
 
+// Bijective XCD-aware block -> tile remap (cdna_hip_programming.md T1): blocks
+// are dealt round-robin over the 8 XCDs (speed only), so XCD x runs blocks
+// x, x+8, ...; map them to the contiguous tile range of XCD x.  With one tile
+// per block and in-order dispatch, the tiles in flight on one XCD form a
+// narrow sliding window, which keeps a banded operator's X gather in its L2.
+__device__ __forceinline__ int64_t xcd_remap(int64_t b, int64_t nb)
+{
+    if (nb < 8) return b;
+    const int64_t q = nb >> 3, r = nb & 7, x = b & 7, k = b >> 3;
+    return (x < r) ? x * (q + 1) + k : r * (q + 1) + (x - r) * q + k;
+}
+
 // wave-private LDS hand-off: make this wave's LDS writes visible to its own
 // later LDS reads (DS ops of one wave complete in order once lgkmcnt drains).
 __device__ __forceinline__ void wave_lds_sync()

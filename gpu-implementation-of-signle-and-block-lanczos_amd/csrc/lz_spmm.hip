@@ -104,6 +104,73 @@ __global__ __launch_bounds__(256) void k_spmm_rm(int64_t n, const int64_t *__res
     }
 }
 
+// Tile-per-block SpMM (the default row-major kernel).  A block owns RB
+// consecutive rows (one group of LPR lanes per row): it stages the tile's
+// (col, val) range into LDS with coalesced loads, then every group gathers its
+// row's X rows 8 nnz at a time (8 independent 16-byte loads per lane in
+// flight), reading (col, val) from LDS.  One tile per block with the XCD remap
+// keeps each XCD's in-flight tiles contiguous (L2-resident X window).  Tiles
+// with more than CAP nnz are staged in CAP-sized chunks.
+template <typename T, int B, int CAP>
+__global__ __launch_bounds__(256) void k_spmm_lds(int64_t n, const int64_t *__restrict__ rp,
+                                                  const int32_t *__restrict__ col,
+                                                  const T *__restrict__ val,
+                                                  const T *__restrict__ X, int64_t ldx,
+                                                  T *__restrict__ Y, int64_t ldy)
+{
+    using S = SpmmShape<T, B>;
+    constexpr int VEC = S::VEC, LPR = S::LPR, RB = S::RB, UNR = 8;
+    __shared__ int32_t cs[CAP];
+    __shared__ T vs[CAP];
+    const int tid = threadIdx.x;
+    const int gi = tid / LPR, p = tid % LPR;
+    const int64_t r0 = xcd_remap(blockIdx.x, gridDim.x) * RB;
+    const int64_t rend = (r0 + RB < n) ? r0 + RB : n;
+    const int64_t kA = rp[r0], kB = rp[rend];
+    const int64_t row = r0 + gi;
+    const bool valid = row < n;
+    const int64_t k0 = valid ? rp[row] : kB, k1 = valid ? rp[row + 1] : kB;
+    const T *Xp = X + p * VEC;
+    T acc[VEC];
+#pragma unroll
+    for (int i = 0; i < VEC; ++i) acc[i] = T(0);
+    for (int64_t c0 = kA; c0 < kB; c0 += CAP) {  // block-uniform
+        const int64_t c1 = (c0 + CAP < kB) ? c0 + CAP : kB;
+        if (c0 != kA) __syncthreads();
+        for (int64_t k = c0 + tid; k < c1; k += 256) {
+            cs[k - c0] = col[k];
+            vs[k - c0] = val[k];
+        }
+        __syncthreads();
+        const int64_t a = k0 > c0 ? k0 : c0, e = k1 < c1 ? k1 : c1;
+        for (int64_t kb = a; kb < e; kb += UNR) {  // group-uniform
+            const int cnt = (int)((e - kb) < UNR ? (e - kb) : UNR);
+            const int base = (int)(kb - c0);
+            Vec<T, VEC> xs[UNR];
+            T vv[UNR];
+#pragma unroll
+            for (int t = 0; t < UNR; ++t) {
+                const int li = base + (t < cnt ? t : 0);
+                vv[t] = vs[li];
+                xs[t] = ldv<T, VEC>(Xp + (int64_t)cs[li] * ldx);
+            }
+#pragma unroll
+            for (int t = 0; t < UNR; ++t) {
+                if (t < cnt) {
+#pragma unroll
+                    for (int i = 0; i < VEC; ++i) acc[i] = fma(vv[t], xs[t].v[i], acc[i]);
+                }
+            }
+        }
+    }
+    if (valid) {
+        Vec<T, VEC> o;
+#pragma unroll
+        for (int i = 0; i < VEC; ++i) o.v[i] = acc[i];
+        stv<T, VEC>(Y + row * ldy + p * VEC, o);
+    }
+}
+
 // Column-major compatibility path (the reference's Dense_matrix layout,
 // element (r,c) at r + c*ld).  One thread per row; any b.
 template <typename T>
@@ -158,12 +225,20 @@ static int launch_spmm_rm(lz_handle *h, int64_t n, const int64_t *rp, const int3
                           const T *val, const T *X, int64_t ldx, T *Y, int64_t ldy)
 {
     using S = SpmmShape<T, B>;
+    constexpr int CAP = S::RB * 32 < 1024 ? 1024 : (S::RB * 32 > 4096 ? 4096 : S::RB * 32);
     const int64_t units = ceil_div(n, S::RB);
-    const int grid = (int)std::min<int64_t>(units, (int64_t)h->n_cu * 8);
-    if (grid <= 0) return LZ_OK;
+    if (units <= 0) return LZ_OK;
+    static const char *variant = getenv("LZ_SPMM_KERNEL");  // "stream": A/B only
     const int ev = prof_begin(h, PROF_SPMM);
-    hipLaunchKernelGGL((k_spmm_rm<T, B>), dim3(grid), dim3(256), 0, h->stream, n, rp, col, val,
-                       X, ldx, Y, ldy);
+    if (variant && variant[0] == 's') {
+        const int grid = (int)std::min<int64_t>(units, (int64_t)h->n_cu * 8);
+        hipLaunchKernelGGL((k_spmm_rm<T, B>), dim3(grid), dim3(256), 0, h->stream, n, rp, col,
+                           val, X, ldx, Y, ldy);
+    } else {
+        LZ_ARG_CHECK(units < (1LL << 31), "too many row tiles");
+        hipLaunchKernelGGL((k_spmm_lds<T, B, CAP>), dim3((unsigned)units), dim3(256), 0, h->stream,
+                           n, rp, col, val, X, ldx, Y, ldy);
+    }
     prof_end(h, ev);
     LZ_LAUNCH_CHECK();
     return LZ_OK;
