@@ -247,7 +247,10 @@ int lz_init(int device, lz_handle **out)
     h->n_cu = prop.multiProcessorCount;
     h->partials_cap = (size_t)kMaxPartials * kMaxB * kMaxB;
     LZ_HIP_TRY(hipMalloc(&h->partials, sizeof(double) * h->partials_cap));
-    LZ_HIP_TRY(hipMalloc(&h->partials2, sizeof(double) * 256 * kMaxB * kMaxB));
+    LZ_HIP_TRY(hipMalloc(&h->partials2, sizeof(double) * (256 * kMaxB * kMaxB + 4096 * 256)));
+    LZ_HIP_TRY(hipMalloc(&h->qctr, 64 * sizeof(unsigned)));
+    LZ_HIP_TRY(hipMemset(h->qctr, 0, 64 * sizeof(unsigned)));
+    if (const char *e = getenv("LZ_SPMM_BLOCKS_PER_CU")) h->spmm_blocks_per_cu = atoi(e);
     LZ_HIP_TRY(hipMalloc(&h->scratch, sizeof(double) * 8 * kMaxB * kMaxB));
     *out = h;
     return LZ_OK;
@@ -264,6 +267,7 @@ int lz_finalize(lz_handle *h)
     }
     (void)hipFree(h->partials);
     (void)hipFree(h->partials2);
+    (void)hipFree(h->qctr);
     (void)hipFree(h->scratch);
     delete h;
     return LZ_OK;

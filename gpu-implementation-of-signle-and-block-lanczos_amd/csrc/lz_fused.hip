@@ -44,6 +44,30 @@ __device__ __forceinline__ void tile_to_aop(double *T, const double *__restrict_
     wave_lds_sync();
 }
 
+// the same in two halves: global -> registers (issue early), registers -> LDS
+// -> A operands (later)
+__device__ __forceinline__ void tile_load(const double *__restrict__ src, int64_t r0, int64_t n,
+                                          int lane, double v[4])
+{
+    const int64_t row = r0 + (lane >> 2);
+    v[0] = v[1] = v[2] = v[3] = 0.0;
+    if (row < n) {
+        const double2 *s2 = reinterpret_cast<const double2 *>(src + row * 16 + 4 * (lane & 3));
+        const double2 x = s2[0], y = s2[1];
+        v[0] = x.x; v[1] = x.y; v[2] = y.x; v[3] = y.y;
+    }
+}
+
+__device__ __forceinline__ void tile_regs_to_aop(double *T, const double v[4], int lane, double a[4])
+{
+#pragma unroll
+    for (int i = 0; i < 4; ++i) T[(lane >> 2) * 17 + 4 * (lane & 3) + i] = v[i];
+    wave_lds_sync();
+#pragma unroll
+    for (int kc = 0; kc < 4; ++kc) a[kc] = T[(lane & 15) * 17 + 4 * kc + (lane >> 4)];
+    wave_lds_sync();
+}
+
 // sum the 8 waves' 16x16 accumulators of the workgroup into its slab
 __device__ __forceinline__ void wg_slab(double (*red)[256], d4_t acc, int lane, int w,
                                         double *__restrict__ part)
@@ -103,6 +127,11 @@ __global__ __launch_bounds__(512) void k_fused_spmm16(
         k1[rr] = row < n ? rp[row + 1] : kB;
     }
     const double *Xp = Wg + 2 * p;
+    // the epilogue's own-row tiles (W rows and Q_{j-1} rows) are fetched now so
+    // their HBM latency overlaps the gather
+    double wv[4], qv[4] = {0.0, 0.0, 0.0, 0.0};
+    tile_load(Wown, r0, n, lane, wv);
+    if (has_prev) tile_load(Qbuf, r0, n, lane, qv);
     double y[2][2] = {{0.0, 0.0}, {0.0, 0.0}};
     for (int64_t c0 = kA; c0 < kB; c0 += kFusedCap) {  // block-uniform
         const int64_t c1 = (c0 + kFusedCap < kB) ? c0 + kFusedCap : kB;
@@ -125,7 +154,8 @@ __global__ __launch_bounds__(512) void k_fused_spmm16(
                 for (int t = 0; t < 8; ++t) {
                     const int li = base + (t < cnt ? t : 0);
                     vv[t] = vs[li];
-                    xs[t] = *reinterpret_cast<const double2 *>(Xp + (int64_t)cs[li] * 16);
+                    if (t < cnt)  // exec-masked: no L1/TA work past the row's end
+                        xs[t] = *reinterpret_cast<const double2 *>(Xp + (int64_t)cs[li] * 16);
                 }
 #pragma unroll
                 for (int t = 0; t < 8; ++t) {
@@ -152,8 +182,8 @@ __global__ __launch_bounds__(512) void k_fused_spmm16(
 #pragma unroll
         for (int kc = 0; kc < 4; ++kc) ya[kc] = T[(lane & 15) * 17 + 4 * kc + (lane >> 4)];
         wave_lds_sync();
-        tile_to_aop(T, Wown, r0, n, lane, wa);
-        if (has_prev) tile_to_aop(T, Qbuf, r0, n, lane, qa);
+        tile_regs_to_aop(T, wv, lane, wa);
+        if (has_prev) tile_regs_to_aop(T, qv, lane, qa);
         // ---- epilogue products on the matrix cores
         d4_t q1 = {0.0, 0.0, 0.0, 0.0}, wn = {0.0, 0.0, 0.0, 0.0};
 #pragma unroll
@@ -196,17 +226,40 @@ __global__ __launch_bounds__(256) void k_slab_reduce1(const double *__restrict__
     const int64_t G = gridDim.x, q = blockIdx.x;
     const int64_t s0 = q * P / G, s1 = (q + 1) * P / G;
     for (int e = threadIdx.x; e < bb; e += 256) {
-        double a0 = 0.0, a1 = 0.0, a2 = 0.0, a3 = 0.0;
+        double a[8] = {0.0, 0.0, 0.0, 0.0, 0.0, 0.0, 0.0, 0.0};
         int64_t s = s0;
-        for (; s + 3 < s1; s += 4) {
-            a0 += part[s * bb + e];
-            a1 += part[(s + 1) * bb + e];
-            a2 += part[(s + 2) * bb + e];
-            a3 += part[(s + 3) * bb + e];
+        for (; s + 7 < s1; s += 8) {
+#pragma unroll
+            for (int i = 0; i < 8; ++i) a[i] += part[(s + i) * bb + e];
         }
-        for (; s < s1; ++s) a0 += part[s * bb + e];
-        out[q * bb + e] = (a0 + a1) + (a2 + a3);
+        for (; s < s1; ++s) a[0] += part[s * bb + e];
+        out[q * bb + e] = ((a[0] + a[1]) + (a[2] + a[3])) + ((a[4] + a[5]) + (a[6] + a[7]));
     }
+}
+
+// Fold P slabs of bb (<= 256) doubles to <= 256 slabs at h->partials2 in one
+// or two fixed-order levels (the first level writes <= 4096 slabs past the
+// first 256*256 doubles of partials2).  Returns the folded count.
+static int fold_slabs(lz_handle *h, const double *part, int64_t P, int bb, int *nout)
+{
+    double *final_ = h->partials2;
+    double *lvl1 = h->partials2 + 256 * 256;
+    const int ev = prof_begin(h, PROF_SMALL);
+    if (P <= 256) {
+        hipLaunchKernelGGL(k_slab_reduce1, dim3((unsigned)P), dim3(256), 0, h->stream, part, P, bb,
+                           final_);
+        *nout = (int)P;
+    } else {
+        const int g1 = (int)std::min<int64_t>(P, 4096);
+        hipLaunchKernelGGL(k_slab_reduce1, dim3(g1), dim3(256), 0, h->stream, part, P, bb, lvl1);
+        const int g2 = std::min(g1, 256);
+        hipLaunchKernelGGL(k_slab_reduce1, dim3(g2), dim3(256), 0, h->stream, lvl1, (int64_t)g1,
+                           bb, final_);
+        *nout = g2;
+    }
+    prof_end(h, ev);
+    LZ_LAUNCH_CHECK();
+    return LZ_OK;
 }
 
 __global__ __launch_bounds__(512) void k_fused_update16(int64_t n, double *__restrict__ Wn,
@@ -260,15 +313,8 @@ int fused_spmm16(lz_handle *h, int64_t n, const int64_t *rp, const int32_t *col,
                        val, Wg, Wown, Qbuf, Wn, binv, beta, lc, qrow, h->partials);
     prof_end(h, ev);
     LZ_LAUNCH_CHECK();
-    // fold the per-tile slabs to <= 256 (fixed order) in the second slab buffer
-    const int g1 = (int)std::min<int64_t>(tiles, 256);
-    const int ev2 = prof_begin(h, PROF_SMALL);
-    hipLaunchKernelGGL(k_slab_reduce1, dim3(g1), dim3(256), 0, h->stream, h->partials, tiles, 256,
-                       h->partials2);
-    prof_end(h, ev2);
-    LZ_LAUNCH_CHECK();
-    *nparts = g1;
-    return LZ_OK;
+    // fold the per-tile slabs to <= 256 (fixed order) at h->partials2
+    return fold_slabs(h, h->partials, tiles, 256, nparts);
 }
 
 int fused_update16(lz_handle *h, int64_t n, double *Wn, const double *Q, const double *alpha,
