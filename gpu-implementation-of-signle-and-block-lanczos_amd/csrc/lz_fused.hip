@@ -92,7 +92,7 @@ __device__ __forceinline__ void wg_slab(double (*red)[256], d4_t acc, int lane, 
 // k_slab_reduce1 folds the slabs in fixed order.
 constexpr int kFusedRows = 128, kFusedCap = 2048;
 
-__global__ __launch_bounds__(512) void k_fused_spmm16(
+__global__ __launch_bounds__(512, 4) void k_fused_spmm16(
     int64_t n, const int64_t *__restrict__ rp, const int32_t *__restrict__ col,
     const double *__restrict__ val, const double *__restrict__ Wg,
     const double *__restrict__ Wown, double *__restrict__ Qbuf,
