@@ -326,6 +326,183 @@ __global__ __launch_bounds__(kRedThreads) void k_sqrtm(int b, const T *__restric
     }
 }
 
+// Compile-time-B variant (B = 8, 16, 32).  After the slab reduction one wave
+// runs the same round-robin (circle method) parallel Jacobi, restructured so
+// that a round is short straight-line code: A and U = V^T are kept in
+// "position space" -- the entry of index x lives at its round-robin position,
+// so the pairs of every round are the fixed positions (p, B-1-p), and after
+// each round the rows and columns are written back moved one position along
+// the circle (position 0 fixed, pos -> pos-1, 1 -> B-1).  Every LDS address a
+// lane touches is then the same in every round; after B-1 rounds (one sweep)
+// positions coincide with indices again, so the convergence test and the
+// result see the matrix in index order.  Lane t owns the position-space
+// entries (t / B + (64/B) k, t % B).  Per round: lanes p < B/2 compute and
+// publish the rotation of (p, B-1-p) (one sqrt, one division, a refined rsq),
+// then every lane forms A' = R A R^T and U' = R U from four A and two U reads
+// and writes them to the other buffer at the moved positions.  The products
+// are ordered so that A' stays bit-symmetric (contraction off).  Rotations
+// below the relative threshold a_pq^2 <= eps^2 |a_pp a_qq| are skipped and the
+// sweeps stop once no pair exceeds it (high relative accuracy for the small
+// eigenvalues of a nearly rank-deficient W'^T W').
+#ifdef LZ_SQRTM_PROBE
+__device__ long long lz_sqrtm_probe[2];  // sweeps, Jacobi clock cycles (scripts/probe)
+#endif
+
+// Jacobi rotation for the pair (p, q): c, s with R[p][p] = R[q][q] = c,
+// R[p][q] = -s, R[q][p] = s annihilating a_pq (Numerical Recipes' t with
+// tau = (a_qq - a_pp) / 2 a_pq, rewritten without the tau division).
+__device__ __forceinline__ void jacobi_rot(double app, double aqq, double apq, double &c, double &s)
+{
+#pragma clang fp contract(off)
+    constexpr double kTol2 = 2.220446049250313e-16 * 2.220446049250313e-16;
+    c = 1.0;
+    s = 0.0;
+    if (apq != 0.0 && apq * apq > kTol2 * (fabs(app) * fabs(aqq))) {
+        const double d = aqq - app, a2 = 2.0 * apq;
+        const double t = (d >= 0.0 ? a2 : -a2) / (fabs(d) + sqrt(d * d + a2 * a2));
+        const double x = 1.0 + t * t;
+        double y = __builtin_amdgcn_rsq(x);
+        y = y * (1.5 - 0.5 * x * y * y);
+        c = y;
+        s = t * y;
+    }
+}
+
+template <typename T, int B>
+__global__ __launch_bounds__(kRedThreads) void k_sqrtm_b(const T *__restrict__ Gin,
+                                                         const double *__restrict__ part, int P,
+                                                         T *__restrict__ beta, T *__restrict__ binv,
+                                                         T *__restrict__ eig)
+{
+#pragma clang fp contract(off)
+    static_assert(B == 8 || B == 16 || B == 32, "B in {8, 16, 32}");
+    constexpr int BB = B * B, LD = B + 1, NE = BB / 64, RS = 64 / B;
+    constexpr int UN = B >= 32 ? 2 : NE;
+    constexpr double kTol2 = 2.220446049250313e-16 * 2.220446049250313e-16;
+    __shared__ double g[BB];
+    __shared__ double scratch[kRedThreads];
+    __shared__ double Abuf[2][B * LD], Ubuf[2][B * LD];
+    __shared__ double cc[B], ss[B];
+    const int tid = threadIdx.x;
+    if (P > 0) {
+        reduce_slabs(part, P, BB, g, scratch);
+    } else {
+        for (int e = tid; e < BB; e += kRedThreads) g[e] = (double)Gin[e];
+        __syncthreads();
+    }
+    if (tid >= 64) return;  // one wave from here on
+    const int j = tid % B, r0 = tid / B;  // column, first row of this lane
+    const int jq = B - 1 - j;                      // partner position of j
+    const int jn = j == 0 ? 0 : (j == 1 ? B - 1 : j - 1);  // moved position of j
+    double *Am = Abuf[0], *An = Abuf[1], *Um = Ubuf[0], *Un = Ubuf[1];
+#pragma unroll UN
+    for (int k = 0; k < NE; ++k) {
+        const int i = r0 + RS * k;
+        // symmetrise from the lower triangle (syevj with CUBLAS_FILL_MODE_LOWER)
+        Am[i * LD + j] = (i < j) ? g[j * B + i] : g[i * B + j];
+        Um[i * LD + j] = (i == j) ? 1.0 : 0.0;
+    }
+    wave_lds_sync();
+#ifdef LZ_SQRTM_PROBE
+    const long long t0 = clock64();
+    int nsw = 0;
+#endif
+    for (int sweep = 0; sweep < 60; ++sweep) {
+#ifdef LZ_SQRTM_PROBE
+        nsw = sweep;
+#endif
+        // converged when no off-diagonal entry exceeds the rotation threshold
+        bool need = false;
+        const double djj = fabs(Am[j * LD + j]);
+#pragma unroll UN
+        for (int k = 0; k < NE; ++k) {
+            const int i = r0 + RS * k;
+            const double aij = Am[i * LD + j];
+            if (i != j && aij != 0.0 && aij * aij > kTol2 * (fabs(Am[i * LD + i]) * djj)) need = true;
+        }
+        if (__ballot(need) == 0) break;  // wave-uniform
+#pragma unroll 1
+        for (int rnd = 0; rnd < B - 1; ++rnd) {
+            if (tid < B / 2) {
+                const int p = tid, q = B - 1 - tid;
+                double c, s;
+                jacobi_rot(Am[p * LD + p], Am[q * LD + q], Am[p * LD + q], c, s);
+                cc[p] = c;
+                cc[q] = c;
+                ss[p] = -s;  // R[p][q]
+                ss[q] = s;   // R[q][p]
+            }
+            wave_lds_sync();
+            const double cj = cc[j], sj = ss[j];
+            for (int k0 = 0; k0 < NE; k0 += UN) {
+                double v[UN][6], ci[UN], si[UN];
+#pragma unroll
+                for (int kk = 0; kk < UN; ++kk) {  // all reads of the chunk first
+                    const int i = r0 + RS * (k0 + kk), iq = B - 1 - i;
+                    ci[kk] = cc[i];
+                    si[kk] = ss[i];
+                    v[kk][0] = Am[i * LD + j];
+                    v[kk][1] = Am[i * LD + jq];
+                    v[kk][2] = Am[iq * LD + j];
+                    v[kk][3] = Am[iq * LD + jq];
+                    v[kk][4] = Um[i * LD + j];
+                    v[kk][5] = Um[iq * LD + j];
+                }
+#pragma unroll
+                for (int kk = 0; kk < UN; ++kk) {
+                    const int i = r0 + RS * (k0 + kk);
+                    const int in = i == 0 ? 0 : (i == 1 ? B - 1 : i - 1);
+                    const double x1 = v[kk][0] * (ci[kk] * cj), x2 = v[kk][1] * (ci[kk] * sj);
+                    const double x3 = v[kk][2] * (si[kk] * cj), x4 = v[kk][3] * (si[kk] * sj);
+                    const bool ann = (i == jq) && si[kk] != 0.0;  // the annihilated pair
+                    An[in * LD + jn] = ann ? 0.0 : (x1 + x4) + (x2 + x3);
+                    Un[in * LD + j] = v[kk][4] * ci[kk] + v[kk][5] * si[kk];
+                }
+            }
+            {
+                double *t = Am; Am = An; An = t;
+                t = Um; Um = Un; Un = t;
+            }
+            wave_lds_sync();
+        }
+    }
+#ifdef LZ_SQRTM_PROBE
+    if (tid == 0) {
+        lz_sqrtm_probe[0] = nsw;
+        lz_sqrtm_probe[1] = clock64() - t0;
+    }
+#endif
+    // beta = V f(L) V^T with V[i][k] = U[k][i]; f(L) tabulated once
+    if (tid < B) {
+        const double sq = sqrt(fabs(Am[tid * LD + tid]));
+        cc[tid] = sq;
+        ss[tid] = 1.0 / sq;
+    }
+    wave_lds_sync();
+#pragma unroll 1
+    for (int k = 0; k < NE; ++k) {
+        const int i = r0 + RS * k;
+        double s1 = 0.0, s2 = 0.0;
+#pragma unroll 4
+        for (int kk = 0; kk < B; ++kk) {
+            const double vv = Um[kk * LD + i] * Um[kk * LD + j];
+            s1 += vv * cc[kk];
+            s2 += vv * ss[kk];
+        }
+        if (beta) beta[i * B + j] = (T)s1;
+        if (binv) binv[i * B + j] = (T)s2;
+    }
+    if (eig && tid < B) {
+        const double lk = Am[tid * LD + tid];
+        int rank = 0;
+        for (int k = 0; k < B; ++k) {
+            const double lm = Am[k * LD + k];
+            rank += (lm < lk) || (lm == lk && k < tid);
+        }
+        eig[rank] = (T)lk;
+    }
+}
+
 template <typename T>
 int sqrtm_pair(lz_handle *h, int b, const T *G, int nparts, T *beta, T *beta_inv, T *eig,
                const double *slabs)
@@ -333,8 +510,19 @@ int sqrtm_pair(lz_handle *h, int b, const T *G, int nparts, T *beta, T *beta_inv
     LZ_ARG_CHECK(b >= 1 && b <= 32, "sqrtm supports b <= 32");
     {
     const int ev_ = prof_begin(h, PROF_SMALL);
-    hipLaunchKernelGGL((k_sqrtm<T>), dim3(1), dim3(kRedThreads), 0, h->stream, b, G,
-                       slabs ? slabs : h->partials, nparts, beta, beta_inv, eig);
+    const double *sl = slabs ? slabs : h->partials;
+#define LZ_SQRTM_B(BV)                                                                        \
+    case BV:                                                                                  \
+        hipLaunchKernelGGL((k_sqrtm_b<T, BV>), dim3(1), dim3(kRedThreads), 0, h->stream, G, sl, \
+                           nparts, beta, beta_inv, eig);                                      \
+        break;
+    switch (b) {
+        LZ_SQRTM_B(8) LZ_SQRTM_B(16) LZ_SQRTM_B(32)
+    default:
+        hipLaunchKernelGGL((k_sqrtm<T>), dim3(1), dim3(kRedThreads), 0, h->stream, b, G, sl,
+                           nparts, beta, beta_inv, eig);
+    }
+#undef LZ_SQRTM_B
     prof_end(h, ev_);
     }
     LZ_LAUNCH_CHECK();
