@@ -145,7 +145,7 @@ def main():
         h.prof_enable(False)
         t_avg = ms / cnt * 1e-3
         gbs = spmm_bytes(n, A.nnz, b) / t_avg / 1e9
-        plain = {"kernel": "k_spmm_rm<double,16>", "avg_ms": round(ms / cnt, 4),
+        plain = {"kernel": "k_spmm_buf<double,16,2048,2>", "avg_ms": round(ms / cnt, 4),
                  "bytes_per_launch": spmm_bytes(n, A.nnz, b), "achieved_GBs": round(gbs, 1),
                  "frac_of_hbm_peak": round(gbs / HBM_PEAK_GBS, 4)}
 

@@ -124,7 +124,7 @@ static int block_lanczos_fused16(lz_handle *h, int64_t n, const int64_t *rp, con
     double *bufs[2] = {W, Q1};  // the residual alternates; Q_j lives in Q0
     for (int j = 0; j < m; ++j) {
         double *res_out = bufs[j & 1];
-        LZ_TRY(fused_spmm16(h, n, rp, col, val, res_in, res_in, Q0, res_out, binv,
+        LZ_TRY(fused_spmm16(h, n, rp, col, val, res_in, n, res_in, Q0, res_out, binv,
                             j ? beta + j * bb : nullptr, lc, q + j * 16, &P));
         LZ_TRY(gram_finish<double>(h, 16, P, 1, alpha + j * bb, h->partials2));
         LZ_TRY(fused_update16(h, n, res_out, Q0, alpha + j * bb, &P));
@@ -183,7 +183,7 @@ static int block_lanczos_dist16(lz_handle *h, int64_t n_local, int64_t n_pad, co
     LZ_TRY(sqrtm_pair<double>(h, 16, nullptr, 1, beta, binv, nullptr, slab));
     LZ_NCCL_TRY(ncclAllGather(B, X, n_pad * 16, ncclDouble, comm, h->stream));
     for (int j = 0; j < m; ++j) {
-        LZ_TRY(fused_spmm16(h, n_local, rp, col, val, X, own, Q0, W, binv,
+        LZ_TRY(fused_spmm16(h, n_local, rp, col, val, X, n_pad * h->nranks, own, Q0, W, binv,
                             j ? beta + j * bb : nullptr, lc_local, q + j * 16, &P));
         LZ_TRY(gram_finish<double>(h, 16, P, 0, slab, h->partials2));
         LZ_NCCL_TRY(ncclAllReduce(slab, slab, bb, ncclDouble, ncclSum, comm, h->stream));
@@ -248,9 +248,6 @@ int lz_init(int device, lz_handle **out)
     h->partials_cap = (size_t)kMaxPartials * kMaxB * kMaxB;
     LZ_HIP_TRY(hipMalloc(&h->partials, sizeof(double) * h->partials_cap));
     LZ_HIP_TRY(hipMalloc(&h->partials2, sizeof(double) * (256 * kMaxB * kMaxB + 4096 * 256)));
-    LZ_HIP_TRY(hipMalloc(&h->qctr, 64 * sizeof(unsigned)));
-    LZ_HIP_TRY(hipMemset(h->qctr, 0, 64 * sizeof(unsigned)));
-    if (const char *e = getenv("LZ_SPMM_BLOCKS_PER_CU")) h->spmm_blocks_per_cu = atoi(e);
     LZ_HIP_TRY(hipMalloc(&h->scratch, sizeof(double) * 8 * kMaxB * kMaxB));
     *out = h;
     return LZ_OK;
@@ -267,7 +264,6 @@ int lz_finalize(lz_handle *h)
     }
     (void)hipFree(h->partials);
     (void)hipFree(h->partials2);
-    (void)hipFree(h->qctr);
     (void)hipFree(h->scratch);
     delete h;
     return LZ_OK;

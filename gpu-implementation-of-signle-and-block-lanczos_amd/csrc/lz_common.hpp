@@ -66,8 +66,6 @@ struct lz_handle {
     size_t partials_cap = 0;      // doubles
     double *partials2 = nullptr;  // first-level folded slabs: 256 * kMaxB * kMaxB doubles
     double *scratch = nullptr;    // 8 * kMaxB * kMaxB doubles
-    unsigned *qctr = nullptr;     // 64 tile-queue counters (persistent kernels)
-    int spmm_blocks_per_cu = 4;   // resident 256-thread blocks of k_spmm_q
     void *comm = nullptr;         // ncclComm_t when lz_comm_init was called
     int nranks = 1, rank = 0;
     // optional per-kernel-class timing with hipEvents on the handle's stream

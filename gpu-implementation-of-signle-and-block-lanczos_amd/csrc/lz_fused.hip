@@ -91,18 +91,27 @@ __device__ __forceinline__ void wg_slab(double (*red)[256], d4_t acc, int lane, 
 // The per-block 16x16 slab of Q_j^T W' goes to part[tile]; lz_fused.hip's
 // k_slab_reduce1 folds the slabs in fixed order.
 constexpr int kFusedRows = 128, kFusedCap = 2048;
+#ifdef LZ_FUSED_PROBE
+// per-block phase records of k_fused_spmm16 (scripts/probe/fused_probe.hip):
+// staging, gather, epilogue cycles, start and end realtime stamps, XCC id
+__device__ long long *lz_fused_probe;
+#define LZ_PROBE_T(v) const long long v = clock64()
+#else
+#define LZ_PROBE_T(v)
+#endif
 
+template <bool BUF>
 __global__ __launch_bounds__(512, 4) void k_fused_spmm16(
     int64_t n, const int64_t *__restrict__ rp, const int32_t *__restrict__ col,
-    const double *__restrict__ val, const double *__restrict__ Wg,
+    const double *__restrict__ val, const double *__restrict__ Wg, int64_t nx,
     const double *__restrict__ Wown, double *__restrict__ Qbuf,
     double *__restrict__ Wn, const double *__restrict__ binv, const double *__restrict__ beta,
     int64_t lc, double *__restrict__ qrow, double *__restrict__ part)
 {
     __shared__ double tile[8][16 * 17];
     __shared__ double red[8][256];
-    __shared__ int32_t cs[kFusedCap];
-    __shared__ double vs[kFusedCap];
+    __shared__ int32_t cs[kFusedCap + 8];
+    __shared__ double vs[kFusedCap + 8];
     const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
     const int g = lane >> 3, p = lane & 7;
     double *T = tile[w];
@@ -114,6 +123,11 @@ __global__ __launch_bounds__(512, 4) void k_fused_spmm16(
         bi_op[kc] = binv[idx];
         nb_op[kc] = has_prev ? -beta[idx] : 0.0;
     }
+    LZ_PROBE_T(t_start);
+#ifdef LZ_FUSED_PROBE
+    const long long w_start = wall_clock64();
+    long long t_staged = 0;
+#endif
     const int64_t u = xcd_remap(blockIdx.x, gridDim.x);
     const int64_t rb = u * kFusedRows;
     const int64_t rend = (rb + kFusedRows < n) ? rb + kFusedRows : n;
@@ -127,6 +141,13 @@ __global__ __launch_bounds__(512, 4) void k_fused_spmm16(
         k1[rr] = row < n ? rp[row + 1] : kB;
     }
     const double *Xp = Wg + 2 * p;
+    // X through a buffer resource (BUF: X < 2 GiB, columns < 2^24): 32-bit
+    // offsets, out-of-range offset = masked load (returns 0, no traffic)
+    __amdgpu_buffer_rsrc_t xr;
+    if constexpr (BUF)
+        xr = __builtin_amdgcn_make_buffer_rsrc(const_cast<double *>(Wg), (short)0,
+                                               (int)(nx * 128), 0x00020000);
+    const uint32_t lane_off = 16u * (uint32_t)p;
     // the epilogue's own-row tiles (W rows and Q_{j-1} rows) are fetched now so
     // their HBM latency overlaps the gather
     double wv[4], qv[4] = {0.0, 0.0, 0.0, 0.0};
@@ -136,32 +157,70 @@ __global__ __launch_bounds__(512, 4) void k_fused_spmm16(
     for (int64_t c0 = kA; c0 < kB; c0 += kFusedCap) {  // block-uniform
         const int64_t c1 = (c0 + kFusedCap < kB) ? c0 + kFusedCap : kB;
         if (c0 != kA) __syncthreads();
-        for (int64_t k = c0 + threadIdx.x; k < c1; k += 512) {
-            cs[k - c0] = col[k];
-            vs[k - c0] = val[k];
+        {  // the chunk's run in one batch of loads, then LDS (+ 8 finite slack slots)
+            constexpr int SPT = kFusedCap / 512;
+            int32_t ct[SPT];
+            double vt[SPT];
+#pragma unroll
+            for (int q = 0; q < SPT; ++q) {
+                const int64_t k = c0 + threadIdx.x + 512 * q;
+                ct[q] = k < c1 ? col[k] : 0;
+                vt[q] = k < c1 ? val[k] : 0.0;
+            }
+#pragma unroll
+            for (int q = 0; q < SPT; ++q) {
+                if (c0 + threadIdx.x + 512 * q < c1) {
+                    cs[threadIdx.x + 512 * q] = ct[q];
+                    vs[threadIdx.x + 512 * q] = vt[q];
+                }
+            }
+            if (threadIdx.x < 8) {
+                cs[c1 - c0 + threadIdx.x] = 0;
+                vs[c1 - c0 + threadIdx.x] = 0.0;
+            }
         }
         __syncthreads();
+#ifdef LZ_FUSED_PROBE
+        if (c0 == kA) t_staged = clock64();
+#endif
 #pragma unroll
         for (int rr = 0; rr < 2; ++rr) {
-            const int64_t a = k0[rr] > c0 ? k0[rr] : c0, e = k1[rr] < c1 ? k1[rr] : c1;
+            const int a = (int)((k0[rr] > c0 ? k0[rr] : c0) - c0);
+            const int e = (int)((k1[rr] < c1 ? k1[rr] : c1) - c0);
             double a0 = y[rr][0], a1 = y[rr][1];
-            for (int64_t kb = a; kb < e; kb += 8) {
-                const int cnt = (int)((e - kb) < 8 ? (e - kb) : 8);
-                const int base = (int)(kb - c0);
-                double2 xs[8];
+            for (int kb = a; kb < e; kb += 8) {  // group-uniform
+                const int cnt = e - kb;
+                int32_t cc[8];
                 double vv[8];
 #pragma unroll
                 for (int t = 0; t < 8; ++t) {
-                    const int li = base + (t < cnt ? t : 0);
-                    vv[t] = vs[li];
-                    if (t < cnt)  // exec-masked: no L1/TA work past the row's end
-                        xs[t] = *reinterpret_cast<const double2 *>(Xp + (int64_t)cs[li] * 16);
+                    cc[t] = cs[kb + t];
+                    vv[t] = vs[kb + t];
                 }
+                double2 xs[8];
+                if constexpr (BUF) {
 #pragma unroll
-                for (int t = 0; t < 8; ++t) {
-                    if (t < cnt) {
+                    for (int t = 0; t < 8; ++t) {
+                        const uint32_t off =
+                            t < cnt ? __umul24((unsigned)cc[t], 128u) + lane_off : 0x80000000u;
+                        const auto u4 = __builtin_amdgcn_raw_buffer_load_b128(xr, off, 0, 0);
+                        __builtin_memcpy(&xs[t], &u4, 16);
+                    }
+#pragma unroll
+                    for (int t = 0; t < 8; ++t) {  // masked entries: x == 0, v finite
                         a0 = fma(vv[t], xs[t].x, a0);
                         a1 = fma(vv[t], xs[t].y, a1);
+                    }
+                } else {
+#pragma unroll
+                    for (int t = 0; t < 8; ++t)
+                        if (t < cnt) xs[t] = *reinterpret_cast<const double2 *>(Xp + (int64_t)cc[t] * 16);
+#pragma unroll
+                    for (int t = 0; t < 8; ++t) {
+                        if (t < cnt) {
+                            a0 = fma(vv[t], xs[t].x, a0);
+                            a1 = fma(vv[t], xs[t].y, a1);
+                        }
                     }
                 }
             }
@@ -169,6 +228,7 @@ __global__ __launch_bounds__(512, 4) void k_fused_spmm16(
             y[rr][1] = a1;
         }
     }
+    LZ_PROBE_T(t_gathered);
     d4_t macc = {0.0, 0.0, 0.0, 0.0};
     if (r0 < n) {  // wave-uniform
         // ---- Y tile -> A operands
@@ -216,6 +276,18 @@ __global__ __launch_bounds__(512, 4) void k_fused_spmm16(
         for (int ww = 0; ww < 8; ++ww) sum += red[ww][threadIdx.x];
         part[u * 256 + threadIdx.x] = sum;
     }
+#ifdef LZ_FUSED_PROBE
+    if (threadIdx.x == 0) {
+        const long long t_end = clock64();
+        long long *rec = lz_fused_probe + 8 * (int64_t)blockIdx.x;
+        rec[0] = t_staged - t_start;
+        rec[1] = t_gathered - t_staged;
+        rec[2] = t_end - t_gathered;
+        rec[3] = w_start;
+        rec[4] = wall_clock64();
+        rec[5] = __builtin_amdgcn_s_getreg((20 << 0) | (0 << 6) | (3 << 11));  // HW_ID2-ish (unused)
+    }
+#endif
 }
 
 // First-level fixed-order fold of P slabs (bb doubles each) into gridDim.x
@@ -302,15 +374,20 @@ __global__ __launch_bounds__(512) void k_fused_update16(int64_t n, double *__res
 }
 
 int fused_spmm16(lz_handle *h, int64_t n, const int64_t *rp, const int32_t *col, const double *val,
-                 const double *Wg, const double *Wown, double *Qbuf, double *Wn, const double *binv,
+                 const double *Wg, int64_t nx, const double *Wown, double *Qbuf, double *Wn, const double *binv,
                  const double *beta, int64_t lc, double *qrow, int *nparts)
 {
     const int64_t tiles = ceil_div(n, kFusedRows);
     LZ_ARG_CHECK(tiles >= 1 && tiles < (1LL << 31), "tile count");
     LZ_TRY(ensure_partials(h, tiles * 256));
+    const bool buf = nx * 128 < (1LL << 31) && nx < (1 << 24);
     const int ev = prof_begin(h, PROF_SPMM_PASS);
-    hipLaunchKernelGGL(k_fused_spmm16, dim3((unsigned)tiles), dim3(512), 0, h->stream, n, rp, col,
-                       val, Wg, Wown, Qbuf, Wn, binv, beta, lc, qrow, h->partials);
+    if (buf)
+        hipLaunchKernelGGL(k_fused_spmm16<true>, dim3((unsigned)tiles), dim3(512), 0, h->stream, n,
+                           rp, col, val, Wg, nx, Wown, Qbuf, Wn, binv, beta, lc, qrow, h->partials);
+    else
+        hipLaunchKernelGGL(k_fused_spmm16<false>, dim3((unsigned)tiles), dim3(512), 0, h->stream, n,
+                           rp, col, val, Wg, nx, Wown, Qbuf, Wn, binv, beta, lc, qrow, h->partials);
     prof_end(h, ev);
     LZ_LAUNCH_CHECK();
     // fold the per-tile slabs to <= 256 (fixed order) at h->partials2

@@ -37,10 +37,10 @@ int copy_row(lz_handle *h, int b, const T *Q, int64_t ld, int col_major, int64_t
 // ---- fused block-Lanczos passes, b = 16 fp64 (lz_fused.hip)
 // Pass 1: Y = A*Wg; Qbuf[r] <- Wg[r]*binv (after reading Qbuf[r] when beta
 // != nullptr); Wn[r] = Y[r]*binv - Qprev[r]*beta; slabs of Qbuf^T Wn; row probe.
-// Wown: the rows r of Wg this rank owns (== Wg single-GPU; a slice of the
+// nx: rows of Wg.  Wown: the rows r of Wg this rank owns (== Wg single-GPU; a slice of the
 // all-gathered block multi-GPU).
 int fused_spmm16(lz_handle *h, int64_t n, const int64_t *rp, const int32_t *col,
-                 const double *val, const double *Wg, const double *Wown, double *Qbuf, double *Wn,
+                 const double *val, const double *Wg, int64_t nx, const double *Wown, double *Qbuf, double *Wn,
                  const double *binv, const double *beta, int64_t lc, double *qrow, int *nparts);
 // Pass 2: Wn <- Wn - Q*alpha; slabs of Wn^T Wn.
 int fused_update16(lz_handle *h, int64_t n, double *Wn, const double *Q, const double *alpha,
