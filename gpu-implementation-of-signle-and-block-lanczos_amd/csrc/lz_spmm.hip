@@ -141,29 +141,29 @@ __device__ __forceinline__ Vec<T, VEC> ldbuf(__amdgpu_buffer_rsrc_t r, uint32_t 
     return v;
 }
 
-template <typename T, int B, int CAP, int RPG>
-__global__ __launch_bounds__(256) void k_spmm_buf(int64_t n, const int64_t *__restrict__ rp,
+template <typename T, int B, int CAP, int RPG, int UNR = 8, int MINW = 1>
+__global__ __launch_bounds__(256, MINW) void k_spmm_buf(int64_t n, const int64_t *__restrict__ rp,
                                                   const int32_t *__restrict__ col,
                                                   const T *__restrict__ val,
                                                   const T *__restrict__ X, int64_t ldx,
                                                   T *__restrict__ Y, int64_t ldy)
 {
     using S = SpmmShape<T, B>;
-    constexpr int VEC = S::VEC, LPR = S::LPR, RB = S::RB, UNR = 8, TR = RB * RPG;
+    constexpr int VEC = S::VEC, LPR = S::LPR, RB = S::RB, TR = RB * RPG;
+    constexpr int EPV = 16 / (int)sizeof(T);                // values per 16-B load
+    constexpr int SPTC = ((CAP + 4) / 4 + 255) / 256;         // 16-B col loads per thread
+    constexpr int SPTV = ((CAP + EPV) / EPV + 255) / 256;     // 16-B val loads per thread
     __shared__ int32_t cs[CAP + UNR];
     __shared__ T vs[CAP + UNR];
+    __shared__ int64_t rps[TR + 1];
     const int tid = threadIdx.x;
     const int gi = tid / LPR, p = tid % LPR;
     const int64_t r0 = xcd_remap(blockIdx.x, gridDim.x) * TR;
     const int64_t rend = (r0 + TR < n) ? r0 + TR : n;
     const int64_t kA = rp[r0], kB = rp[rend];
-    int64_t k0[RPG], k1[RPG];
-#pragma unroll
-    for (int j = 0; j < RPG; ++j) {
-        const int64_t row = r0 + gi + RB * j;
-        k0[j] = row < n ? rp[row] : kB;
-        k1[j] = row < n ? rp[row + 1] : kB;
-    }
+    const int64_t nnz = rp[n];
+    // the tile's row pointers: one load per thread, shared through LDS
+    for (int t = tid; t <= TR; t += 256) rps[t] = rp[(r0 + t < rend) ? r0 + t : rend];
     const __amdgpu_buffer_rsrc_t xr = lz_rsrc(X, (uint32_t)(n * ldx * (int64_t)sizeof(T)));
     const uint32_t rowb = (uint32_t)(ldx * sizeof(T)), lane_off = p * VEC * sizeof(T);
     T acc[RPG][VEC];
@@ -171,26 +171,58 @@ __global__ __launch_bounds__(256) void k_spmm_buf(int64_t n, const int64_t *__re
     for (int j = 0; j < RPG; ++j)
 #pragma unroll
         for (int i = 0; i < VEC; ++i) acc[j][i] = T(0);
+    int64_t k0[RPG], k1[RPG];
     for (int64_t c0 = kA; c0 < kB; c0 += CAP) {  // block-uniform
         const int64_t c1 = (c0 + CAP < kB) ? c0 + CAP : kB;
         if (c0 != kA) __syncthreads();
-        {  // the whole chunk in one batch of loads (one HBM round trip), then LDS
-            constexpr int SPT = CAP / 256;
-            int32_t ct[SPT];
-            T vt[SPT];
+        {   // the chunk in one batch of 16-B loads (aligned down), scattered into LDS;
+            // buffer bases at the chunk so offsets stay 32-bit for any nnz; a 16-B
+            // piece reaching past nnz (last tile only) is read element-wise
+            const int64_t bc = c0 & ~(int64_t)3, bv = c0 & ~(int64_t)(EPV - 1);
+            const __amdgpu_buffer_rsrc_t cr = lz_rsrc(col + bc, 0x7fffffffu);
+            const __amdgpu_buffer_rsrc_t vr = lz_rsrc(val + bv, 0x7fffffffu);
+            int4 ct[SPTC];
+            int4 vt[SPTV];
 #pragma unroll
-            for (int q = 0; q < SPT; ++q) {
-                const int64_t k = c0 + tid + 256 * q;
-                const bool ok = k < c1;
-                ct[q] = ok ? col[k] : 0;
-                vt[q] = ok ? val[k] : T(0);
+            for (int q = 0; q < SPTC; ++q) {
+                const int64_t k = bc + 4 * (int64_t)(tid + 256 * q);
+                ct[q] = int4{0, 0, 0, 0};
+                if (k + 4 <= nnz && k < c1)
+                    ct[q] = __builtin_bit_cast(int4, __builtin_amdgcn_raw_buffer_load_b128(cr, (uint32_t)((k - bc) * 4), 0, 0));
+                else if (k < c1) {
+                    ct[q].x = col[k];
+                    if (k + 1 < nnz) ct[q].y = col[k + 1];
+                    if (k + 2 < nnz) ct[q].z = col[k + 2];
+                }
             }
 #pragma unroll
-            for (int q = 0; q < SPT; ++q) {
-                if (c0 + tid + 256 * q < c1) {
-                    cs[tid + 256 * q] = ct[q];
-                    vs[tid + 256 * q] = vt[q];
+            for (int q = 0; q < SPTV; ++q) {
+                const int64_t k = bv + EPV * (int64_t)(tid + 256 * q);
+                vt[q] = int4{0, 0, 0, 0};
+                if (k + EPV <= nnz && k < c1) {
+                    vt[q] = __builtin_bit_cast(int4, __builtin_amdgcn_raw_buffer_load_b128(vr, (uint32_t)((k - bv) * sizeof(T)), 0, 0));
+                } else if (k < c1) {
+                    T tv[EPV] = {};
+                    for (int e = 0; e < EPV && k + e < nnz; ++e) tv[e] = val[k + e];
+                    __builtin_memcpy(&vt[q], tv, 16);
                 }
+            }
+#pragma unroll
+            for (int q = 0; q < SPTC; ++q) {
+                const int64_t k = bc + 4 * (int64_t)(tid + 256 * q);
+                const int32_t cv[4] = {ct[q].x, ct[q].y, ct[q].z, ct[q].w};
+#pragma unroll
+                for (int e = 0; e < 4; ++e)
+                    if (k + e >= c0 && k + e < c1) cs[k + e - c0] = cv[e];
+            }
+#pragma unroll
+            for (int q = 0; q < SPTV; ++q) {
+                const int64_t k = bv + EPV * (int64_t)(tid + 256 * q);
+                T tv[EPV];
+                __builtin_memcpy(tv, &vt[q], 16);
+#pragma unroll
+                for (int e = 0; e < EPV; ++e)
+                    if (k + e >= c0 && k + e < c1) vs[k + e - c0] = tv[e];
             }
         }
         if (tid < UNR) {  // finite slack past the chunk
@@ -198,6 +230,14 @@ __global__ __launch_bounds__(256) void k_spmm_buf(int64_t n, const int64_t *__re
             vs[c1 - c0 + tid] = T(0);
         }
         __syncthreads();
+        if (c0 == kA) {
+#pragma unroll
+            for (int j = 0; j < RPG; ++j) {
+                const int r = gi + RB * j;
+                k0[j] = rps[r < TR ? r : TR];
+                k1[j] = rps[r + 1 < TR ? r + 1 : TR];
+            }
+        }
 #pragma unroll
         for (int j = 0; j < RPG; ++j) {
             const int a = (int)((k0[j] > c0 ? k0[j] : c0) - c0), e = (int)((k1[j] < c1 ? k1[j] : c1) - c0);
@@ -234,6 +274,161 @@ __global__ __launch_bounds__(256) void k_spmm_buf(int64_t n, const int64_t *__re
             for (int i = 0; i < VEC; ++i) o.v[i] = acc[j][i];
             stv<T, VEC>(Y + row * ldy + p * VEC, o);
         }
+    }
+}
+
+// Merge-based (nnz-split) tile SpMM.  Row-wise gathering wastes the load slots
+// past each row's end: with 8 loads per step and ~10 nnz per row only 61 % of
+// the issued 16-B gathers carry an entry on the C3 operator, and the gather
+// pipe (TA: ~34 TB/s of 128-B L2-resident rows chip-wide, measured) is what
+// the kernel waits on.  Here the tile's run of N entries is split evenly over
+// the G groups (E = N/G rounded up to 8 per group, 91 % slot use at 128 rows),
+// each group walks its range 8 entries per step and emits a row's partial sum
+// whenever the row id changes: rows wholly inside a group are stored
+// directly, a group's first and last rows go to LDS slots (HEAD, TAIL) and are
+// finished after a barrier by summing the slots of the groups that cover
+// them, in group order -- deterministic for a given tile size.  Tiles whose
+// run exceeds CAP are processed row-wise from global memory.
+template <typename T, int B, int TR, int CAP>
+__global__ __launch_bounds__(256) void k_spmm_merge(int64_t n, const int64_t *__restrict__ rp,
+                                                    const int32_t *__restrict__ col,
+                                                    const T *__restrict__ val,
+                                                    const T *__restrict__ X, int64_t ldx,
+                                                    T *__restrict__ Y, int64_t ldy)
+{
+    using S = SpmmShape<T, B>;
+    constexpr int VEC = S::VEC, LPR = S::LPR, G = 256 / LPR, UNR = 8, SPT = CAP / 256;
+    static_assert(TR <= 255, "row ids are bytes");
+    __shared__ int32_t rel[TR + 1];
+    __shared__ int32_t cs[CAP + UNR];
+    __shared__ T vs[CAP + UNR];
+    __shared__ uint8_t rid[CAP + UNR];
+    __shared__ Vec<T, VEC> part[G][2][LPR];  // HEAD / TAIL partial rows per group
+    const int tid = threadIdx.x;
+    const int gi = tid / LPR, p = tid % LPR;
+    const int64_t r0 = xcd_remap(blockIdx.x, gridDim.x) * TR;
+    const int nrows = (int)((n - r0) < TR ? (n - r0) : TR);
+    const int64_t kA = rp[r0];
+    if (tid <= nrows) rel[tid] = (int)(rp[r0 + tid] - kA);
+    const int64_t N64 = rp[r0 + nrows] - kA;
+    const __amdgpu_buffer_rsrc_t xr = lz_rsrc(X, (uint32_t)(n * ldx * (int64_t)sizeof(T)));
+    const uint32_t rowb = (uint32_t)(ldx * sizeof(T)), lane_off = p * VEC * sizeof(T);
+    auto store_row = [&](int r, const Vec<T, VEC> &o) { stv<T, VEC>(Y + (r0 + r) * ldy + p * VEC, o); };
+    if (N64 > CAP) {  // block-uniform: long rows -- row-wise straight from global
+        for (int r = gi; r < nrows; r += G) {
+            const int64_t a = rp[r0 + r], e = rp[r0 + r + 1];
+            Vec<T, VEC> acc;
+#pragma unroll
+            for (int i = 0; i < VEC; ++i) acc.v[i] = T(0);
+            for (int64_t k = a; k < e; k += UNR) {
+                Vec<T, VEC> xs[UNR];
+                T vv[UNR];
+#pragma unroll
+                for (int t = 0; t < UNR; ++t) {
+                    const bool ok = k + t < e;
+                    vv[t] = ok ? val[k + t] : T(0);
+                    const uint32_t off = ok ? __umul24((unsigned)col[k + t], rowb) + lane_off : 0x80000000u;
+                    xs[t] = ldbuf<T, VEC>(xr, off);
+                }
+#pragma unroll
+                for (int t = 0; t < UNR; ++t)
+#pragma unroll
+                    for (int i = 0; i < VEC; ++i) acc.v[i] = fma(vv[t], xs[t].v[i], acc.v[i]);
+            }
+            store_row(r, acc);
+        }
+        return;
+    }
+    const int N = (int)N64;
+    {  // stage the run (one batch of loads) and the row id of every entry
+        int32_t ct[SPT];
+        T vt[SPT];
+#pragma unroll
+        for (int q = 0; q < SPT; ++q) {
+            const int k = tid + 256 * q;
+            ct[q] = k < N ? col[kA + k] : 0;
+            vt[q] = k < N ? val[kA + k] : T(0);
+        }
+        __syncthreads();  // rel
+        if (tid < nrows)
+            for (int k = rel[tid]; k < rel[tid + 1]; ++k) rid[k] = (uint8_t)tid;
+#pragma unroll
+        for (int q = 0; q < SPT; ++q) {
+            if (tid + 256 * q < N) {
+                cs[tid + 256 * q] = ct[q];
+                vs[tid + 256 * q] = vt[q];
+            }
+        }
+        if (tid < UNR) {
+            cs[N + tid] = 0;
+            vs[N + tid] = T(0);
+            rid[N + tid] = 255;
+        }
+        __syncthreads();
+    }
+    const int E = ((N + G - 1) / G + UNR - 1) / UNR * UNR;
+    const int start = gi * E, end = (start + E < N) ? start + E : N;
+    if (start < end) {  // group-uniform
+        const int first = rid[start];
+        int cur = first;
+        Vec<T, VEC> acc;
+#pragma unroll
+        for (int i = 0; i < VEC; ++i) acc.v[i] = T(0);
+        for (int s0 = start; s0 < end; s0 += UNR) {
+            int32_t cc[UNR];
+            T vv[UNR];
+            int rr[UNR];
+#pragma unroll
+            for (int t = 0; t < UNR; ++t) {
+                cc[t] = cs[s0 + t];
+                vv[t] = vs[s0 + t];
+                rr[t] = rid[s0 + t];
+            }
+            Vec<T, VEC> xs[UNR];
+#pragma unroll
+            for (int t = 0; t < UNR; ++t) {
+                const uint32_t off =
+                    s0 + t < end ? __umul24((unsigned)cc[t], rowb) + lane_off : 0x80000000u;
+                xs[t] = ldbuf<T, VEC>(xr, off);
+            }
+#pragma unroll
+            for (int t = 0; t < UNR; ++t) {
+                const int r = s0 + t < end ? rr[t] : cur;
+                if (r != cur) {  // the segment of row cur ends: emit it
+                    if (cur == first) part[gi][0][p] = acc;
+                    else store_row(cur, acc);
+#pragma unroll
+                    for (int i = 0; i < VEC; ++i) acc.v[i] = T(0);
+                    cur = r;
+                }
+#pragma unroll
+                for (int i = 0; i < VEC; ++i) acc.v[i] = fma(vv[t], xs[t].v[i], acc.v[i]);
+            }
+        }
+        part[gi][cur == first ? 0 : 1][p] = acc;
+    }
+    __syncthreads();
+    // finish the rows that are some group's first or last row, and empty rows
+    for (int r = gi; r < nrows; r += G) {
+        const int a = rel[r], e = rel[r + 1];
+        Vec<T, VEC> sum;
+#pragma unroll
+        for (int i = 0; i < VEC; ++i) sum.v[i] = T(0);
+        if (a == e) {
+            store_row(r, sum);
+            continue;
+        }
+        const int g1 = a / E, g2 = (e - 1) / E;
+        const bool head1 = a <= g1 * E;                            // first row of g1
+        const int end2 = (g2 + 1) * E < N ? (g2 + 1) * E : N;
+        const bool tail2 = e >= end2;                              // last row of g2
+        if (g1 == g2 && !head1 && !tail2) continue;                // stored by its group
+        for (int g = g1; g <= g2; ++g) {
+            const Vec<T, VEC> &q = part[g][(g == g1 && !head1) ? 1 : 0][p];
+#pragma unroll
+            for (int i = 0; i < VEC; ++i) sum.v[i] += q.v[i];
+        }
+        store_row(r, sum);
     }
 }
 
@@ -303,12 +498,31 @@ static int launch_spmm_rm(lz_handle *h, int64_t n, const int64_t *rp, const int3
     const bool buf_ok = n * ldx * (int64_t)sizeof(T) < (1LL << 31) && n < (1 << 24);
     constexpr int CAP2 = CAP * 2 < 4096 ? CAP * 2 : 4096;
     const int ev = prof_begin(h, PROF_SPMM);
-    if (buf_ok && !(variant && variant[0] == 't')) {
+    if (buf_ok && variant && variant[0] == 'm') {
+        const int64_t mt = ceil_div(n, (int64_t)128);
+        LZ_ARG_CHECK(mt < (1LL << 31), "too many row tiles");
+        hipLaunchKernelGGL((k_spmm_merge<T, B, 128, 2048>), dim3((unsigned)mt), dim3(256), 0,
+                           h->stream, n, rp, col, val, X, ldx, Y, ldy);
+    } else if (buf_ok && variant && variant[0] == 'x') {  // occupancy experiments: x<unr><waves/SIMD>
+        const int unr = variant[1] - '0', occ = variant[2] - '0';
+        if (unr == 4 && occ == 8)
+            hipLaunchKernelGGL((k_spmm_buf<T, B, 1024, 2, 4, 8>), dim3((unsigned)tiles), dim3(256), 0,
+                               h->stream, n, rp, col, val, X, ldx, Y, ldy);
+        else if (unr == 4 && occ == 6)
+            hipLaunchKernelGGL((k_spmm_buf<T, B, 1024, 2, 4, 6>), dim3((unsigned)tiles), dim3(256), 0,
+                               h->stream, n, rp, col, val, X, ldx, Y, ldy);
+        else if (unr == 8 && occ == 6)
+            hipLaunchKernelGGL((k_spmm_buf<T, B, 1024, 2, 8, 6>), dim3((unsigned)tiles), dim3(256), 0,
+                               h->stream, n, rp, col, val, X, ldx, Y, ldy);
+        else
+            hipLaunchKernelGGL((k_spmm_buf<T, B, 1024, 2, 8, 8>), dim3((unsigned)tiles), dim3(256), 0,
+                               h->stream, n, rp, col, val, X, ldx, Y, ldy);
+    } else if (buf_ok && !(variant && variant[0] == 't')) {
         if (rpg == 1)
             hipLaunchKernelGGL((k_spmm_buf<T, B, CAP, 1>), dim3((unsigned)tiles), dim3(256), 0,
                                h->stream, n, rp, col, val, X, ldx, Y, ldy);
         else if (rpg == 2)
-            hipLaunchKernelGGL((k_spmm_buf<T, B, CAP2, 2>), dim3((unsigned)tiles), dim3(256), 0,
+            hipLaunchKernelGGL((k_spmm_buf<T, B, 1024, 2>), dim3((unsigned)tiles), dim3(256), 0,
                                h->stream, n, rp, col, val, X, ldx, Y, ldy);
         else
             hipLaunchKernelGGL((k_spmm_buf<T, B, 4096, 4>), dim3((unsigned)tiles), dim3(256), 0,
