@@ -43,6 +43,23 @@ def fused_pass_bytes(n, nnz, b, sv=8):
     return nnz * (sv + 4) + (n + 1) * 8 + 4 * n * b * sv
 
 
+def pmc_traffic(kernel, n, nnz, hw):
+    """HBM bytes per launch of `kernel` from the committed rocprofv3 PMC summary
+    (profiles/*_pmc_<kernel>.json, written by scripts/pmc_traffic.py from separate
+    FETCH_SIZE / WRITE_SIZE passes of this bench command; FETCH_SIZE doubled per
+    MI355X_MICROARCH.md's gfx950 note).  None unless it was taken on this workload."""
+    import glob
+    for f in sorted(glob.glob(os.path.join(ROOT, "profiles", f"*_pmc_{kernel}.json")), reverse=True):
+        try:
+            d = json.load(open(f))
+        except (OSError, ValueError):
+            continue
+        w = d.get("workload", {})
+        if w.get("n") == n and w.get("nnz") == nnz and w.get("halfwidth") == hw:
+            return d.get("hbm_bytes_per_launch"), os.path.relpath(f, ROOT)
+    return None, None
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -145,7 +162,7 @@ def main():
         h.prof_enable(False)
         t_avg = ms / cnt * 1e-3
         gbs = spmm_bytes(n, A.nnz, b) / t_avg / 1e9
-        plain = {"kernel": "k_spmm_buf<double,16,2048,2>", "avg_ms": round(ms / cnt, 4),
+        plain = {"kernel": "k_spmm_buf<double,16,1024,2>", "avg_ms": round(ms / cnt, 4),
                  "bytes_per_launch": spmm_bytes(n, A.nnz, b), "achieved_GBs": round(gbs, 1),
                  "frac_of_hbm_peak": round(gbs / HBM_PEAK_GBS, 4)}
 
@@ -167,9 +184,11 @@ def main():
         t_pass = spmm_ms / max(spmm_cnt, 1) * 1e-3 if spmm_cnt else None
         if fused and t_pass:
             ach = fused_pass_bytes(n, A.nnz, b) / t_pass / 1e9
+            traffic, tsrc = pmc_traffic("k_fused_spmm16", n, A.nnz, args.halfwidth)
             roof = {"bound": "hbm", "kernel": "k_fused_spmm16", "achieved": round(ach, 1),
                     "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": round(ach / HBM_PEAK_GBS, 4),
-                    "traffic": None, "avg_ms": round(t_pass * 1e3, 4),
+                    "traffic": traffic, "traffic_unit": "bytes/launch", "traffic_source": tsrc,
+                    "avg_ms": round(t_pass * 1e3, 4),
                     "bytes_per_launch": fused_pass_bytes(n, A.nnz, b)}
         elif plain:
             roof = {"bound": "hbm", "kernel": plain["kernel"], "achieved": plain["achieved_GBs"],
