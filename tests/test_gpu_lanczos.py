@@ -156,3 +156,16 @@ def test_block_large_properties(lz, orc, handle, torch_cuda):
     gu = gpu_block(lz, handle, torch_cuda, A, B, m, lc, fused=False)
     assert_close_run(lz, m, 16, g1, gu)
     assert_close_run(lz, m, 16, g1, orc.block_lanczos(A, B, m, lc))
+
+
+def test_block_b16_long_runs(lz, orc, handle, torch_cuda):
+    """Fused pass with 128-row tiles whose CSR run exceeds the LDS staging
+    buffer (power-law rows up to 5000 nnz): chunked staging path, fp64."""
+    A = lz.gen_powerlaw(30011, 12.0, 1.8, 5000, seed=13, dtype=np.float64)
+    rp = np.asarray(A.row_ptr)
+    tile_runs = rp[np.minimum(np.arange(0, A.n + 128, 128), A.n)]
+    assert np.diff(tile_runs).max() > 2048, "test operator must overflow the staging buffer"
+    B = lz.uniform_B(A.n, 16, seed=14)
+    m, lc = 6, 4321
+    got = gpu_block(lz, handle, torch_cuda, A, B, m, lc)
+    assert_close_run(lz, m, 16, got, orc.block_lanczos(A, B, m, lc))
