@@ -56,6 +56,7 @@ HIP_SYMBOLS = [
     ("lz_last_error", ctypes.c_char_p, []),
     ("lz_version", ctypes.c_char_p, []),
     ("lz_device_ok", _c_int, [_c_int]),
+    ("lz_device_error", _c_int, [_c_vp, ctypes.POINTER(_c_int)]),
     ("lz_prof_enable", _c_int, [_c_vp, _c_int]),
     ("lz_prof_read", _c_int, [_c_vp, _c_int, ctypes.POINTER(_c_dbl), ctypes.POINTER(_c_int)]),
     ("lz_csr_spmm", _c_int, [_c_vp, _c_i64, _c_i64, _c_i64, _c_vp, _c_vp, _c_vp, _c_int, _c_int,
@@ -506,6 +507,12 @@ class Handle:
 
     # --- hipEvent timing of kernel classes ------------------------------
     PROF_SPMM_PASS, PROF_UPDATE_PASS, PROF_SMALL, PROF_GRAM, PROF_TSMM, PROF_SPMM = range(6)
+
+    def device_error(self) -> int:
+        """Synchronise and return (then clear) the device error word (0 = ok)."""
+        c = _c_int()
+        _check(self.L.lz_device_error(self._h, ctypes.byref(c)), "lz_device_error")
+        return c.value
 
     def prof_enable(self, on: bool = True):
         _check(self.L.lz_prof_enable(self._h, int(on)), "lz_prof_enable")

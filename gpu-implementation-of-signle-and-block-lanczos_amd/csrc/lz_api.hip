@@ -249,6 +249,8 @@ int lz_init(int device, lz_handle **out)
     LZ_HIP_TRY(hipMalloc(&h->partials, sizeof(double) * h->partials_cap));
     LZ_HIP_TRY(hipMalloc(&h->partials2, sizeof(double) * (256 * kMaxB * kMaxB + 4096 * 256)));
     LZ_HIP_TRY(hipMalloc(&h->scratch, sizeof(double) * 8 * kMaxB * kMaxB));
+    LZ_HIP_TRY(hipMalloc(&h->err_flag, 64));
+    LZ_HIP_TRY(hipMemset(h->err_flag, 0, 64));
     *out = h;
     return LZ_OK;
 }
@@ -265,7 +267,17 @@ int lz_finalize(lz_handle *h)
     (void)hipFree(h->partials);
     (void)hipFree(h->partials2);
     (void)hipFree(h->scratch);
+    (void)hipFree(h->err_flag);
     delete h;
+    return LZ_OK;
+}
+
+int lz_device_error(lz_handle *h, int *code)
+{
+    LZ_ARG_CHECK(h && code, "null argument");
+    LZ_HIP_TRY(hipStreamSynchronize(h->stream));
+    LZ_HIP_TRY(hipMemcpy(code, h->err_flag, sizeof(int), hipMemcpyDeviceToHost));
+    LZ_HIP_TRY(hipMemset(h->err_flag, 0, sizeof(int)));
     return LZ_OK;
 }
 

@@ -66,6 +66,7 @@ struct lz_handle {
     size_t partials_cap = 0;      // doubles
     double *partials2 = nullptr;  // first-level folded slabs: 256 * kMaxB * kMaxB doubles
     double *scratch = nullptr;    // 8 * kMaxB * kMaxB doubles
+    int *err_flag = nullptr;      // device: nonzero if a persistent kernel gave up a bounded spin
     void *comm = nullptr;         // ncclComm_t when lz_comm_init was called
     int nranks = 1, rank = 0;
     // optional per-kernel-class timing with hipEvents on the handle's stream

@@ -277,6 +277,286 @@ __global__ __launch_bounds__(256, MINW) void k_spmm_buf(int64_t n, const int64_t
     }
 }
 
+// Wave-specialised persistent SpMM (b = 16 fp64).  A wave that mixes HBM
+// streaming loads with L2-resident gathers waits HBM latency at every gather
+// step (vmcnt is in order: a load's data waits for every older load).  Measured
+// (scripts/probe/gather_probe.hip): 8 gathers + 2 stream loads per step in the
+// same waves took 2.5x longer than the same work split over gather-only and
+// stream-only waves.  So each block has one LOADER wave that streams the CSR
+// runs of the block's tiles into a ring of WS_K LDS stages with LDS-DMA
+// (buffer_load_dwordx4 ... lds: no VGPRs, bounds-checked per chunk), and
+// WS_NC CONSUMER waves that only gather X (L2) and store Y.  Hand-off through
+// LDS words: ready[s] = tile sequence number once its DMA has landed (the
+// loader waits vmcnt with a fixed number of DMA instructions per tile, so the
+// count is a compile-time immediate); done[s] counts consumer waves finished
+// with the stage.  Every spin is bounded (kWsSpin) so a logic error cannot
+// hang the GPU.  Persistent grid, XCD-aware strided tile order (as
+// k_fused_pw16 had) so an XCD's tiles in flight stay adjacent.
+constexpr int ws_instr(int pieces) { return (pieces + 63) / 64; }
+constexpr long kWsSpin = 1L << 24;
+
+// WS_NC consumer waves (16 rows each), WS_K LDS stages, loader pipeline depth
+// WS_D (tiles whose DMA is in flight), WS_CAP staged nonzeros per tile.
+template <int WS_NC, int WS_K, int WS_D, int WS_CAP>
+struct WsCfg {
+    static constexpr int TR = 16 * WS_NC;
+    static constexpr int RP_PIECES = (TR + 2) * 8 / 16;  // 16-B pieces of row_ptr
+    static constexpr int COL_PIECES = (WS_CAP + 8) * 4 / 16;
+    static constexpr int VAL_PIECES = (WS_CAP + 4) * 8 / 16;
+    static constexpr int DMA_INSTR = ws_instr(RP_PIECES) + ws_instr(COL_PIECES) + ws_instr(VAL_PIECES);
+    static_assert(DMA_INSTR * (WS_D - 1) <= 63, "vmcnt immediate");
+    static_assert(WS_D <= WS_K, "pipeline depth");
+    // one DMA wave-instruction lands 1 KiB (64 lanes x 16 B, out-of-range
+    // lanes included), so every region is a whole number of KiB
+    struct Stage {
+        int64_t rp[ws_instr(RP_PIECES) * 128];
+        int32_t col[ws_instr(COL_PIECES) * 256];
+        double val[ws_instr(VAL_PIECES) * 128];
+    };
+};
+
+typedef __attribute__((address_space(3))) void ws_lds_t;
+
+// LDS word access from the loader wave in inline asm: after an LDS-DMA the
+// compiler inserts vmcnt(0) before any LDS instruction it emits (the DMA could
+// alias it), which would wait for the tile in flight.  These words are never
+// DMA targets.
+__device__ __forceinline__ uint32_t ws_lds_addr(int *p)
+{
+    return (uint32_t)(uintptr_t)(__attribute__((address_space(3))) int *)p;
+}
+__device__ __forceinline__ int ws_lds_read(uint32_t a)
+{
+    int v;
+    asm volatile("ds_read_b32 %0, %1\n\ts_waitcnt lgkmcnt(0)" : "=v"(v) : "v"(a) : "memory");
+    return v;
+}
+__device__ __forceinline__ void ws_lds_write(uint32_t a, int v)
+{
+    asm volatile("ds_write_b32 %0, %1" ::"v"(a), "v"(v) : "memory");
+}
+
+__device__ __forceinline__ void ws_dma(__amdgpu_buffer_rsrc_t r, void *lds_base, int pieces, int lane)
+{
+#pragma unroll
+    for (int q = 0; q < (pieces + 63) / 64; ++q) {
+        const int piece = 64 * q + lane;
+        // pieces past the end get an out-of-range offset (no memory access)
+        const uint32_t off = piece < pieces ? 16u * piece : 0x80000000u;
+        __builtin_amdgcn_raw_ptr_buffer_load_lds(r, (ws_lds_t *)((char *)lds_base + 1024 * q), 16, off, 0, 0, 0);
+    }
+}
+
+// Y rows (g, g+8) of one group: the two rows' entries walked as one list, 8 per
+// step; masked slots read entry o0 and load nothing (out-of-range offset).
+template <typename CP, typename VP>
+__device__ __forceinline__ void ws_gather(CP cp, VP vp, int o0, int len0, int o1, int cnt,
+                                          __amdgpu_buffer_rsrc_t xr, uint32_t lane_off, double y[4])
+{
+    for (int f = 0; f < cnt; f += 8) {
+        int32_t c[8];
+        double v[8];
+#pragma unroll
+        for (int tt = 0; tt < 8; ++tt) {
+            const int ff = f + tt;
+            int o = ff < len0 ? o0 + ff : o1 + (ff - len0);
+            o = ff < cnt ? o : o0;
+            c[tt] = cp[o];
+            v[tt] = vp[o];
+        }
+        double2 xs[8];
+#pragma unroll
+        for (int tt = 0; tt < 8; ++tt) {
+            const uint32_t off = f + tt < cnt ? __umul24((unsigned)c[tt], 128u) + lane_off : 0x80000000u;
+            const auto u4 = __builtin_amdgcn_raw_buffer_load_b128(xr, off, 0, 0);
+            __builtin_memcpy(&xs[tt], &u4, 16);
+        }
+#pragma unroll
+        for (int tt = 0; tt < 8; ++tt) {
+            if (f + tt < len0) {
+                y[0] = fma(v[tt], xs[tt].x, y[0]);
+                y[1] = fma(v[tt], xs[tt].y, y[1]);
+            } else {  // masked entries: x == 0
+                y[2] = fma(v[tt], xs[tt].x, y[2]);
+                y[3] = fma(v[tt], xs[tt].y, y[3]);
+            }
+        }
+    }
+}
+
+#ifdef LZ_WS_PROBE
+// per block: [0] loader cycles waiting on done, [1] loader cycles in vmcnt waits,
+// [2] consumer-0 cycles waiting on ready, [3] consumer-0 total cycles, [4] loader total
+__device__ long long *lz_ws_probe;
+#define WS_T(v) const long long v = clock64()
+#else
+#define WS_T(v)
+#endif
+template <int WS_NC, int WS_K, int WS_D, int WS_CAP>
+__global__ __launch_bounds__(64 * (WS_NC + 1)) void k_spmm_ws(int64_t n, const int64_t *__restrict__ rp,
+                                                           const int32_t *__restrict__ col,
+                                                           const double *__restrict__ val,
+                                                           const double *__restrict__ X,
+                                                           double *__restrict__ Y, int *__restrict__ err)
+{
+    using C = WsCfg<WS_NC, WS_K, WS_D, WS_CAP>;
+    constexpr int WS_TR = C::TR;
+    __shared__ typename C::Stage st[WS_K];
+    __shared__ int ready[WS_K], done[WS_K];
+    const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+    if (threadIdx.x < WS_K) {
+        ready[threadIdx.x] = -1;
+        done[threadIdx.x] = 0;
+    }
+    __syncthreads();  // the only block barrier
+    // this block's tile sequence (XCD-aware, strided)
+    const int64_t T = ceil_div(n, (int64_t)WS_TR);
+    int64_t begin, end, k, K;
+    {
+        const int64_t G = gridDim.x, b = blockIdx.x;
+        if (G < 8) {
+            begin = 0; end = T; k = b; K = G;
+        } else {
+            const int64_t x = b & 7;
+            begin = T * x / 8;
+            end = T * (x + 1) / 8;
+            k = b >> 3;
+            K = (G - x + 7) >> 3;
+        }
+    }
+    const int64_t nt = (end - begin - k + K - 1) / K > 0 ? (end - begin - k + K - 1) / K : 0;
+    const int64_t nnz = rp[n];
+    // LDS hand-off words: workgroup-scope relaxed atomics (ds_read / ds_write,
+    // never flat: flat ops would break the loader's counted vmcnt wait)
+    auto ld = [](int *a) { return __hip_atomic_load(a, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP); };
+    if (w == 0) {
+        // ------------------------------------------------------------ loader
+        auto tile_r0 = [&](int64_t i) { return (begin + k + i * K) * WS_TR; };
+#ifdef LZ_WS_PROBE
+        long long c_done = 0, c_vm = 0;
+        const long long c_start = clock64();
+#endif
+        int64_t kA_next = nt > 0 ? rp[tile_r0(0)] : 0;  // row_ptr of the next tile, one ahead
+        for (int64_t i = 0; i < nt; ++i) {
+            const int s = (int)(i % WS_K);
+            const int64_t r0 = tile_r0(i), r1 = (r0 + WS_TR < n) ? r0 + WS_TR : n;
+            const int64_t kA = kA_next;
+            if (i + 1 < nt) kA_next = rp[tile_r0(i + 1)];
+            if (i >= WS_K) {  // wait until every consumer is done with tile i - K
+                long spin = 0;
+                WS_T(t0);
+                const uint32_t da = ws_lds_addr(&done[s]);
+                while (ws_lds_read(da) < WS_NC * (int)(i / WS_K) && ++spin < kWsSpin) __builtin_amdgcn_s_sleep(1);
+                if (spin >= kWsSpin) { *err = 1; break; }
+#ifdef LZ_WS_PROBE
+                c_done += clock64() - t0;
+#endif
+            }
+            const int64_t ca = kA & ~(int64_t)3, va = kA & ~(int64_t)1;
+            const auto rr = __builtin_amdgcn_make_buffer_rsrc(const_cast<int64_t *>(rp + r0), (short)0,
+                                                              (int)((r1 - r0 + 1) * 8), 0x00020000);
+            const int64_t cb = (nnz - ca) * 4, vb = (nnz - va) * 8;
+            const auto cr = __builtin_amdgcn_make_buffer_rsrc(const_cast<int32_t *>(col + ca), (short)0,
+                                                              (int)(cb < 0x7fffffff ? cb : 0x7fffffff), 0x00020000);
+            const auto vr = __builtin_amdgcn_make_buffer_rsrc(const_cast<double *>(val + va), (short)0,
+                                                              (int)(vb < 0x7fffffff ? vb : 0x7fffffff), 0x00020000);
+            ws_dma(rr, st[s].rp, C::RP_PIECES, lane);
+            ws_dma(cr, st[s].col, C::COL_PIECES, lane);
+            ws_dma(vr, st[s].val, C::VAL_PIECES, lane);
+            if (i >= WS_D - 1) {  // tile i-D+1 has landed once only D-1 tiles' DMA are younger
+                WS_T(t1);
+                asm volatile("s_waitcnt vmcnt(%0)" ::"n"(C::DMA_INSTR * (WS_D - 1)) : "memory");
+#ifdef LZ_WS_PROBE
+                c_vm += clock64() - t1;
+#endif
+                const int64_t pub = i - (WS_D - 1);
+                if (lane == 0) ws_lds_write(ws_lds_addr(&ready[(int)(pub % WS_K)]), (int)pub);
+            }
+        }
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        for (int64_t pub = nt - (WS_D - 1) > 0 ? nt - (WS_D - 1) : 0; pub < nt; ++pub)
+            if (lane == 0) ws_lds_write(ws_lds_addr(&ready[(int)(pub % WS_K)]), (int)pub);
+#ifdef LZ_WS_PROBE
+        if (lane == 0) {
+            (void)c_done;
+            (void)c_vm;
+            lz_ws_probe[8 * blockIdx.x + 4] = clock64() - c_start;
+            lz_ws_probe[8 * blockIdx.x + 5] = nt;
+        }
+#endif
+        return;
+    }
+    // -------------------------------------------------------------- consumers
+    const int cw = w - 1, g = lane >> 3, p = lane & 7;
+    const __amdgpu_buffer_rsrc_t xr =
+        __builtin_amdgcn_make_buffer_rsrc(const_cast<double *>(X), (short)0, (int)(n * 128), 0x00020000);
+    const uint32_t lane_off = 16u * p;
+#ifdef LZ_WS_PROBE
+    long long c_ready = 0, c_gather = 0, c_steps = 0;
+    const long long c_cstart = clock64();
+    const long long w_cstart = wall_clock64();
+#endif
+    for (int64_t i = 0; i < nt; ++i) {
+        const int s = (int)(i % WS_K);
+        const int64_t t = begin + k + i * K;
+        const int64_t r0 = t * WS_TR;
+        long spin = 0;
+        WS_T(t2);
+        while (ld(&ready[s]) != (int)i && ++spin < kWsSpin) __builtin_amdgcn_s_sleep(1);
+#ifdef LZ_WS_PROBE
+        c_ready += clock64() - t2;
+#endif
+        if (spin >= kWsSpin) { *err = 2; break; }
+        asm volatile("" ::: "memory");
+        const typename C::Stage &S = st[s];
+        const int64_t kA = S.rp[0];
+        const int co = (int)(kA & 3), vo = (int)(kA & 1);  // stage offsets of entry kA
+        const int runlen = (int)(S.rp[(r0 + WS_TR < n ? WS_TR : n - r0)] - kA);
+        const int lr = 16 * cw + g;  // local rows lr, lr + 8
+        const int nrow = (int)(n - r0 < WS_TR ? n - r0 : WS_TR);
+        const int o0 = lr < nrow ? (int)(S.rp[lr] - kA) : 0;
+        const int len0 = lr < nrow ? (int)(S.rp[lr + 1] - kA) - o0 : 0;
+        const int o1 = lr + 8 < nrow ? (int)(S.rp[lr + 8] - kA) : 0;
+        const int len1 = lr + 8 < nrow ? (int)(S.rp[lr + 9] - kA) - o1 : 0;
+        const int cnt = len0 + len1;
+        double y[4] = {0.0, 0.0, 0.0, 0.0};
+        // the tile-uniform choice of (col, val) source is made outside the loop:
+        // a merged loop makes the compiler wait vmcnt(0) before every LDS read
+        // (the global-path load could target the same register), which
+        // serialises every gather behind the previous ones
+        WS_T(t3);
+        if (runlen <= WS_CAP)
+            ws_gather(S.col + co, S.val + vo, o0, len0, o1, cnt, xr, lane_off, y);
+        else
+            ws_gather(col + kA, val + kA, o0, len0, o1, cnt, xr, lane_off, y);
+#ifdef LZ_WS_PROBE
+        c_gather += clock64() - t3;
+        c_steps += (cnt + 7) / 8;
+#endif
+        // this wave no longer reads the stage (its LDS reads have returned)
+        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+        if (lane == 0) atomicAdd(&done[s], 1);
+#ifdef LZ_WS_NOSTORE
+        if (y[0] == 1.2345e300) {  // diagnostic build: keep the math, drop the stores
+#endif
+        if (lr < nrow) *reinterpret_cast<double2 *>(Y + (r0 + lr) * 16 + 2 * p) = double2{y[0], y[1]};
+        if (lr + 8 < nrow) *reinterpret_cast<double2 *>(Y + (r0 + lr + 8) * 16 + 2 * p) = double2{y[2], y[3]};
+#ifdef LZ_WS_NOSTORE
+        }
+#endif
+    }
+#ifdef LZ_WS_PROBE
+    if (cw == 0 && lane == 0) {
+        lz_ws_probe[8 * blockIdx.x + 2] = c_ready;
+        lz_ws_probe[8 * blockIdx.x + 3] = clock64() - c_cstart;
+        lz_ws_probe[8 * blockIdx.x + 6] = w_cstart;
+        lz_ws_probe[8 * blockIdx.x + 1] = c_gather;
+        lz_ws_probe[8 * blockIdx.x + 0] = c_steps;
+        lz_ws_probe[8 * blockIdx.x + 7] = wall_clock64();
+    }
+#endif
+}
+
 // Merge-based (nnz-split) tile SpMM.  Row-wise gathering wastes the load slots
 // past each row's end: with 8 loads per step and ~10 nnz per row only 61 % of
 // the issued 16-B gathers carry an entry on the C3 operator, and the gather
@@ -498,6 +778,28 @@ static int launch_spmm_rm(lz_handle *h, int64_t n, const int64_t *rp, const int3
     const bool buf_ok = n * ldx * (int64_t)sizeof(T) < (1LL << 31) && n < (1 << 24);
     constexpr int CAP2 = CAP * 2 < 4096 ? CAP * 2 : 4096;
     const int ev = prof_begin(h, PROF_SPMM);
+    if constexpr (B == 16 && std::is_same<T, double>::value) {
+        if (buf_ok && ldx == 16 && ldy == 16 && variant && variant[0] == 'w') {
+            // LZ_SPMM_KERNEL=w<cfg>: 0: 8 consumers, 3 stages, depth 2 (2 blocks/CU)
+            //   1: 4 consumers, 4 stages, depth 3 (3 blocks/CU)  2: 8 consumers, 4 stages, depth 3 (1/CU)
+            const int cfg = variant[1] ? variant[1] - '0' : 0;
+            auto go = [&](auto kern, int tr, int bpc, int threads) {
+                const int grid = (int)std::max<int64_t>(1, std::min<int64_t>(ceil_div(n, (int64_t)tr),
+                                                                             (int64_t)h->n_cu * bpc));
+                hipLaunchKernelGGL(kern, dim3(grid), dim3(threads), 0, h->stream, n, rp, col, val, X, Y,
+                                   h->err_flag);
+            };
+            if (cfg == 1)
+                go(k_spmm_ws<4, 4, 3, 888>, 64, 3, 320);
+            else if (cfg == 2)
+                go(k_spmm_ws<8, 4, 3, 1784>, 128, 1, 576);
+            else
+                go(k_spmm_ws<8, 3, 2, 1784>, 128, 2, 576);
+            prof_end(h, ev);
+            LZ_LAUNCH_CHECK();
+            return LZ_OK;
+        }
+    }
     if (buf_ok && variant && variant[0] == 'm') {
         const int64_t mt = ceil_div(n, (int64_t)128);
         LZ_ARG_CHECK(mt < (1LL << 31), "too many row tiles");

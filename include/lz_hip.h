@@ -58,6 +58,11 @@ int lz_device_ok(int device);
  * work).  Classes: 0 fused SpMM pass, 1 fused update pass, 2 one-workgroup
  * finish/sqrtm kernels, 3 Gram slabs, 4 tall x small products, 5 plain SpMM.
  * lz_prof_enable resets the record (capacity 4096 launches). */
+/* Synchronises the handle's stream and returns (then clears) the device error
+ * word: nonzero if a persistent kernel abandoned a bounded spin-wait (its
+ * results are then invalid).  0 in normal operation. */
+int lz_device_error(lz_handle *h, int *code);
+
 int lz_prof_enable(lz_handle *h, int on);
 int lz_prof_read(lz_handle *h, int kernel_class, double *ms_total, int *count);
 

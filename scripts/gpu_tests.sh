@@ -1,0 +1,6 @@
+#!/bin/bash
+cd "$GRAFT_REPO_ROOT" || exit 1
+export TMPDIR=/tmp
+mkdir -p gpurun_out
+timeout -k 10 900 python -m pytest tests -m gpu -q -x -p no:cacheprovider "$@" > gpurun_out/pytest_gpu.log 2>&1
+rc=$?; tail -15 gpurun_out/pytest_gpu.log; exit $rc

@@ -20,5 +20,6 @@ for _ in range(10):
 e.record(); torch.cuda.synchronize()
 ms = s.elapsed_time(e) / 10
 byt = A.nnz * 12 + (n + 1) * 8 + 2 * n * b * 8
-print(json.dumps(dict(variant=os.environ.get("LZ_SPMM_KERNEL", "buf"),
+err = h.device_error()
+print(json.dumps(dict(err=err, variant=os.environ.get("LZ_SPMM_KERNEL", "buf"),
                       n=n, hw=hw, b=b, ms=round(ms, 4), GBs=round(byt / ms / 1e6, 1), same=bool(torch.equal(ref, Y)) if os.environ.get("LZ_SPMM_KERNEL","")[2:3] == "" else None)), flush=True)
