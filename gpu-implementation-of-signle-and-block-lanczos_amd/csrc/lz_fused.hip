@@ -373,14 +373,289 @@ __global__ __launch_bounds__(512) void k_fused_update16(int64_t n, double *__res
     wg_slab(red, gacc, lane, w, part);
 }
 
+// ---------------------------------------------------------------------------
+// Wave-specialised persistent pass 1 (the k_spmm_ws structure, lz_spmm.hip,
+// plus the fused epilogue).  One block per CU: a LOADER wave streams, per tile
+// of 16*NC rows, the CSR run and the tile's Q_{j-1} rows into a double-buffered
+// LDS stage with LDS-DMA (a fixed number of DMA instructions per tile, so its
+// landing wait is a compile-time vmcnt); NC CONSUMER waves (one 16-row strip
+// each) gather X from L2 (8 loads in flight per lane; gather throughput scales
+// with the number of consumer waves, so NC is as large as LDS and VGPRs allow),
+// load their own W rows (L2-resident: just gathered by neighbouring tiles), run
+// the MFMA epilogue, store Q_j and W', and accumulate Q_j^T W' in registers
+// across their tiles -- one 16x16 slab per consumer wave, no block barrier
+// after the first.  The consumers' memory waits cover only L2 traffic and their
+// own stores, never the HBM streams.  Q strips land in chunk-column-major order
+// (slot c4*16 + r); after reading its Q operand a consumer reuses its strip of
+// the stage as the XOR-swizzled transpose scratch for W and Y.  Rows past n are
+// out of range for the DMA and land as zeros.
+template <int NC, int CAP>
+struct FwCfg {
+    static constexpr int TR = 16 * NC;
+    static constexpr int RP_PIECES = (TR + 2) * 8 / 16;
+    static constexpr int COL_PIECES = (CAP + 8) * 4 / 16;
+    static constexpr int VAL_PIECES = (CAP + 4) * 8 / 16;
+    static constexpr int DMA_INSTR = ws_instr(RP_PIECES) + ws_instr(COL_PIECES) + ws_instr(VAL_PIECES) + 2 * NC;
+    static_assert(DMA_INSTR <= 63, "vmcnt immediate");
+    struct Stage {
+        int64_t rp[ws_instr(RP_PIECES) * 128];
+        int32_t col[ws_instr(COL_PIECES) * 256];
+        double val[ws_instr(VAL_PIECES) * 128];
+        double qt[TR * 16];  // Q_{j-1} rows, per strip in slot order; then scratch
+    };
+};
+
+// DMA NC 16-row strips of a row-major n x 16 block (buffer `r` based at the
+// tile's first row) into dst in slot order: strip j, slot c4*16 + r holds row
+// 16j + r, doubles 2c4, 2c4+1.
+template <int NC>
+__device__ __forceinline__ void fw_strips_dma(__amdgpu_buffer_rsrc_t r, double *dst, int lane)
+{
+#pragma unroll
+    for (int j = 0; j < NC; ++j)
+#pragma unroll
+        for (int h2 = 0; h2 < 2; ++h2) {
+            const int slot = 64 * h2 + lane, c4 = slot >> 4, rr = slot & 15;
+            const uint32_t off = (uint32_t)(((16 * j + rr) * 16 + 2 * c4) * 8);
+            __builtin_amdgcn_raw_ptr_buffer_load_lds(r, (ws_lds_t *)(dst + 256 * j + 128 * h2), 16, off, 0, 0, 0);
+        }
+}
+
+// 16x16 scratch with XOR swizzle: element (r, c) at r*16 + (c ^ r); the MFMA
+// operand read (16 rows, one column per lane group) hits 16 distinct banks.
+__device__ __forceinline__ int fw_sw(int r, int c) { return r * 16 + (c ^ r); }
+
+template <int NC, int CAP, int FW_K>
+__global__ __launch_bounds__(64 * (NC + 1)) void k_fused_ws16(
+    int64_t n, const int64_t *__restrict__ rp, const int32_t *__restrict__ col,
+    const double *__restrict__ val, const double *__restrict__ Wg, int64_t nx,
+    const double *__restrict__ Wown, double *__restrict__ Qbuf, double *__restrict__ Wn,
+    const double *__restrict__ binv, const double *__restrict__ beta, int64_t lc,
+    double *__restrict__ qrow, double *__restrict__ part, int *__restrict__ err)
+{
+    using C = FwCfg<NC, CAP>;
+    constexpr int TR = C::TR;
+    __shared__ typename C::Stage st[FW_K];
+    __shared__ double ops[2][256];  // beta^-1, -beta in MFMA B-operand order
+    __shared__ int ready[FW_K], done[FW_K];
+    const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+    const bool has_prev = beta != nullptr;
+    if (threadIdx.x < FW_K) {
+        ready[threadIdx.x] = -1;
+        done[threadIdx.x] = 0;
+    }
+    for (int e = threadIdx.x; e < 256; e += blockDim.x) {
+        const int kc = e >> 6, l = e & 63;
+        const int idx = (4 * kc + (l >> 4)) * 16 + (l & 15);
+        ops[0][e] = binv[idx];
+        ops[1][e] = has_prev ? -beta[idx] : 0.0;
+    }
+    __syncthreads();  // the only block barrier
+    const int64_t T = ceil_div(n, (int64_t)TR);
+    int64_t begin, end, k, K;
+    {
+        const int64_t G = gridDim.x, b = blockIdx.x;
+        if (G < 8) {
+            begin = 0; end = T; k = b; K = G;
+        } else {
+            const int64_t x = b & 7;
+            begin = T * x / 8;
+            end = T * (x + 1) / 8;
+            k = b >> 3;
+            K = (G - x + 7) >> 3;
+        }
+    }
+    const int64_t nt = (end - begin - k + K - 1) / K > 0 ? (end - begin - k + K - 1) / K : 0;
+    auto tile_r0 = [&](int64_t i) { return (begin + k + i * K) * TR; };
+    if (w == 0) {
+        // ------------------------------------------------------------ loader
+        // highest issue priority: the loader's DMA must not queue behind the
+        // consumers' gathers, or the consumers starve waiting for stages
+        __builtin_amdgcn_s_setprio(3);
+#ifdef LZ_WS_PROBE
+        long long c_done = 0;
+        const long long c_start = clock64();
+#endif
+        const int64_t nnz = rp[n];
+        int64_t kA_next = nt > 0 ? rp[tile_r0(0)] : 0;
+        for (int64_t i = 0; i < nt; ++i) {
+            const int s = (int)(i % FW_K);
+            const int64_t r0 = tile_r0(i), r1 = (r0 + TR < n) ? r0 + TR : n;
+            const int64_t kA = kA_next;
+            if (i + 1 < nt) kA_next = rp[tile_r0(i + 1)];
+            if (i >= FW_K) {
+                long spin = 0;
+                WS_T(t0);
+                const uint32_t da = ws_lds_addr(&done[s]);
+                while (ws_lds_read(da) < NC * (int)(i / FW_K) && ++spin < kWsSpin) __builtin_amdgcn_s_sleep(1);
+                if (spin >= kWsSpin) { *err = 3; break; }
+#ifdef LZ_WS_PROBE
+                c_done += clock64() - t0;
+#endif
+            }
+            const int64_t ca = kA & ~(int64_t)3, va = kA & ~(int64_t)1;
+            const int64_t cb = (nnz - ca) * 4, vb = (nnz - va) * 8;
+            const auto rr = __builtin_amdgcn_make_buffer_rsrc(const_cast<int64_t *>(rp + r0), (short)0,
+                                                              (int)((r1 - r0 + 1) * 8), 0x00020000);
+            const auto cr = __builtin_amdgcn_make_buffer_rsrc(const_cast<int32_t *>(col + ca), (short)0,
+                                                              (int)(cb < 0x7fffffff ? cb : 0x7fffffff), 0x00020000);
+            const auto vr = __builtin_amdgcn_make_buffer_rsrc(const_cast<double *>(val + va), (short)0,
+                                                              (int)(vb < 0x7fffffff ? vb : 0x7fffffff), 0x00020000);
+            const auto qr = __builtin_amdgcn_make_buffer_rsrc(Qbuf + r0 * 16, (short)0,
+                                                              has_prev ? (int)((r1 - r0) * 128) : 0, 0x00020000);
+            ws_dma(rr, st[s].rp, C::RP_PIECES, lane);
+            ws_dma(cr, st[s].col, C::COL_PIECES, lane);
+            ws_dma(vr, st[s].val, C::VAL_PIECES, lane);
+            fw_strips_dma<NC>(qr, st[s].qt, lane);
+            if (i >= 1) {  // tile i-1 has landed once only tile i's DMA is younger
+                asm volatile("s_waitcnt vmcnt(%0)" ::"n"(C::DMA_INSTR) : "memory");
+                if (lane == 0) ws_lds_write(ws_lds_addr(&ready[(int)((i - 1) % FW_K)]), (int)(i - 1));
+            }
+        }
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        if (nt > 0 && lane == 0) ws_lds_write(ws_lds_addr(&ready[(int)((nt - 1) % FW_K)]), (int)(nt - 1));
+#ifdef LZ_WS_PROBE
+        if (lane == 0) {
+            lz_ws_probe[8 * blockIdx.x + 4] = clock64() - c_start;
+            lz_ws_probe[8 * blockIdx.x + 5] = nt;
+            lz_ws_probe[8 * blockIdx.x + 1] = c_done;
+        }
+#endif
+        return;
+    }
+    // -------------------------------------------------------------- consumers
+    const int cw = w - 1, g = lane >> 3, p = lane & 7;
+    const __amdgpu_buffer_rsrc_t xr =
+        __builtin_amdgcn_make_buffer_rsrc(const_cast<double *>(Wg), (short)0, (int)(nx * 128), 0x00020000);
+    const uint32_t lane_off = 16u * p;
+    d4_t macc = {0.0, 0.0, 0.0, 0.0};
+#ifdef LZ_WS_PROBE
+    long long c_ready = 0, c_gather = 0;
+    const long long c_cstart = clock64();
+#endif
+    for (int64_t i = 0; i < nt; ++i) {
+        const int s = (int)(i % FW_K);
+        const int64_t r0 = tile_r0(i);
+        const int64_t s0 = r0 + 16 * cw;  // this wave's strip
+        // own W rows (L2): lane holds row s0 + (lane >> 2), doubles 4(lane&3)..+3
+        double wv[4];
+        tile_load(Wown, s0, n, lane, wv);
+        long spin = 0;
+        WS_T(t2);
+        while (__hip_atomic_load(&ready[s], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP) != (int)i &&
+               ++spin < kWsSpin)
+            __builtin_amdgcn_s_sleep(1);
+        if (spin >= kWsSpin) { *err = 4; break; }
+#ifdef LZ_WS_PROBE
+        c_ready += clock64() - t2;
+#endif
+        asm volatile("" ::: "memory");
+        typename C::Stage &S = st[s];
+        const int64_t kA = S.rp[0];
+        const int co = (int)(kA & 3), vo = (int)(kA & 1);
+        const int nrow = (int)(n - r0 < TR ? n - r0 : TR);
+        const int runlen = (int)(S.rp[nrow] - kA);
+        const int lr = 16 * cw + g;
+        const int o0 = lr < nrow ? (int)(S.rp[lr] - kA) : 0;
+        const int len0 = lr < nrow ? (int)(S.rp[lr + 1] - kA) - o0 : 0;
+        const int o1 = lr + 8 < nrow ? (int)(S.rp[lr + 8] - kA) : 0;
+        const int len1 = lr + 8 < nrow ? (int)(S.rp[lr + 9] - kA) - o1 : 0;
+        double y[4] = {0.0, 0.0, 0.0, 0.0};
+        WS_T(t3);
+        if (runlen <= CAP)  // tile-uniform, outside the loop (see k_spmm_ws)
+            ws_gather(S.col + co, S.val + vo, o0, len0, o1, len0 + len1, xr, lane_off, y);
+        else
+            ws_gather(col + kA, val + kA, o0, len0, o1, len0 + len1, xr, lane_off, y);
+#ifdef LZ_WS_PROBE
+        c_gather += clock64() - t3;
+#endif
+        // ---- epilogue operands (A operand a[kc] = M[l&15][4kc + (l>>4)])
+        double *Sc = S.qt + 256 * cw;  // Q strip, then this wave's scratch
+        double ya[4], wa[4], qa[4];
+        const int ar = lane & 15;
+#pragma unroll
+        for (int kc = 0; kc < 4; ++kc) {
+            const int c = 4 * kc + (lane >> 4);
+            qa[kc] = Sc[((c >> 1) * 16 + ar) * 2 + (c & 1)];
+        }
+        wave_lds_sync();
+        // W rows -> scratch -> operand
+#pragma unroll
+        for (int q = 0; q < 4; ++q) Sc[fw_sw(lane >> 2, 4 * (lane & 3) + q)] = (s0 + (lane >> 2) < n) ? wv[q] : 0.0;
+        wave_lds_sync();
+#pragma unroll
+        for (int kc = 0; kc < 4; ++kc) wa[kc] = Sc[fw_sw(ar, 4 * kc + (lane >> 4))];
+        wave_lds_sync();
+        // Y rows -> scratch -> operand
+        Sc[fw_sw(g, 2 * p)] = y[0];
+        Sc[fw_sw(g, 2 * p + 1)] = y[1];
+        Sc[fw_sw(g + 8, 2 * p)] = y[2];
+        Sc[fw_sw(g + 8, 2 * p + 1)] = y[3];
+        wave_lds_sync();
+#pragma unroll
+        for (int kc = 0; kc < 4; ++kc) ya[kc] = Sc[fw_sw(ar, 4 * kc + (lane >> 4))];
+        // the stage is no longer used by this wave
+        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+        if (lane == 0) atomicAdd(&done[s], 1);
+        d4_t q1 = {0.0, 0.0, 0.0, 0.0}, wn = {0.0, 0.0, 0.0, 0.0};
+#pragma unroll
+        for (int kc = 0; kc < 4; ++kc) q1 = mfma16(wa[kc], ops[0][64 * kc + lane], q1);
+#pragma unroll
+        for (int kc = 0; kc < 4; ++kc) wn = mfma16(ya[kc], ops[0][64 * kc + lane], wn);
+        if (has_prev) {
+#pragma unroll
+            for (int kc = 0; kc < 4; ++kc) wn = mfma16(qa[kc], ops[1][64 * kc + lane], wn);
+        }
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+            const int64_t row = s0 + (lane >> 4) + 4 * r;
+            if (row < n) {
+                Qbuf[s0 * 16 + 64 * r + lane] = q1[r];
+                Wn[s0 * 16 + 64 * r + lane] = wn[r];
+                if (row == lc) qrow[lane & 15] = q1[r];
+            }
+        }
+#pragma unroll
+        for (int r = 0; r < 4; ++r) macc = mfma16(q1[r], wn[r], macc);
+    }
+    double *slab = part + ((int64_t)blockIdx.x * NC + cw) * 256;
+#pragma unroll
+    for (int r = 0; r < 4; ++r) slab[((lane >> 4) + 4 * r) * 16 + (lane & 15)] = macc[r];
+#ifdef LZ_WS_PROBE
+    if (cw == 0 && lane == 0) {
+        lz_ws_probe[8 * blockIdx.x + 2] = c_ready;
+        lz_ws_probe[8 * blockIdx.x + 3] = clock64() - c_cstart;
+        lz_ws_probe[8 * blockIdx.x + 0] = c_gather;
+    }
+#endif
+}
+
 int fused_spmm16(lz_handle *h, int64_t n, const int64_t *rp, const int32_t *col, const double *val,
                  const double *Wg, int64_t nx, const double *Wown, double *Qbuf, double *Wn, const double *binv,
                  const double *beta, int64_t lc, double *qrow, int *nparts)
 {
     const int64_t tiles = ceil_div(n, kFusedRows);
     LZ_ARG_CHECK(tiles >= 1 && tiles < (1LL << 31), "tile count");
-    LZ_TRY(ensure_partials(h, tiles * 256));
     const bool buf = nx * 128 < (1LL << 31) && nx < (1 << 24);
+    static const char *variant = getenv("LZ_FUSED_KERNEL");  // "tile": the tile-per-block kernel
+    if (buf && !(variant && variant[0] == 't')) {
+        // LZ_FUSED_KERNEL=ws<NC digit>: consumer waves per CU (default 15)
+        const int nc = (variant && variant[0] == 'w' && variant[2]) ? (variant[2] == '8' ? 8 : 15) : 15;
+        const int tr = 16 * nc;
+        const int grid = (int)std::max<int64_t>(1, std::min<int64_t>(ceil_div(n, (int64_t)tr), h->n_cu));
+        LZ_TRY(ensure_partials(h, (size_t)grid * nc * 256));
+        const int ev = prof_begin(h, PROF_SPMM_PASS);
+        if (nc == 8)
+            hipLaunchKernelGGL((k_fused_ws16<8, 1784, 3>), dim3(grid), dim3(64 * 9), 0, h->stream, n, rp, col,
+                               val, Wg, nx, Wown, Qbuf, Wn, binv, beta, lc, qrow, h->partials, h->err_flag);
+        else
+            hipLaunchKernelGGL((k_fused_ws16<15, 2536, 2>), dim3(grid), dim3(64 * 16), 0, h->stream, n, rp, col,
+                               val, Wg, nx, Wown, Qbuf, Wn, binv, beta, lc, qrow, h->partials, h->err_flag);
+        prof_end(h, ev);
+        LZ_LAUNCH_CHECK();
+        return fold_slabs(h, h->partials, (int64_t)grid * nc, 256, nparts);
+    }
+    LZ_TRY(ensure_partials(h, tiles * 256));
     const int ev = prof_begin(h, PROF_SPMM_PASS);
     if (buf)
         hipLaunchKernelGGL(k_fused_spmm16<true>, dim3((unsigned)tiles), dim3(512), 0, h->stream, n,

@@ -102,4 +102,85 @@ __device__ __forceinline__ d4_t mfma16(double a, double b, d4_t c)
     return __builtin_amdgcn_mfma_f64_16x16x4f64(a, b, c, 0, 0, 0);
 }
 
+// ---- wave-specialised persistent kernels (loader wave + consumer waves) ----
+// k_spmm_ws (lz_spmm.hip) and k_fused_ws16 (lz_fused.hip).
+constexpr int ws_instr(int pieces) { return (pieces + 63) / 64; }
+#ifdef LZ_WS_PROBE
+// diagnostic builds (scripts/probe/ws_probe*.hip): per-block wait/cycle records
+__device__ long long *lz_ws_probe;
+#define WS_T(v) const long long v = clock64()
+#else
+#define WS_T(v)
+#endif
+constexpr long kWsSpin = 1L << 24;
+
+typedef __attribute__((address_space(3))) void ws_lds_t;
+
+// LDS word access from the loader wave in inline asm: after an LDS-DMA the
+// compiler inserts vmcnt(0) before any LDS instruction it emits (the DMA could
+// alias it), which would wait for the tile in flight.  These words are never
+// DMA targets.
+__device__ __forceinline__ uint32_t ws_lds_addr(int *p)
+{
+    return (uint32_t)(uintptr_t)(__attribute__((address_space(3))) int *)p;
+}
+__device__ __forceinline__ int ws_lds_read(uint32_t a)
+{
+    int v;
+    asm volatile("ds_read_b32 %0, %1\n\ts_waitcnt lgkmcnt(0)" : "=v"(v) : "v"(a) : "memory");
+    return v;
+}
+__device__ __forceinline__ void ws_lds_write(uint32_t a, int v)
+{
+    asm volatile("ds_write_b32 %0, %1" ::"v"(a), "v"(v) : "memory");
+}
+
+__device__ __forceinline__ void ws_dma(__amdgpu_buffer_rsrc_t r, void *lds_base, int pieces, int lane)
+{
+#pragma unroll
+    for (int q = 0; q < (pieces + 63) / 64; ++q) {
+        const int piece = 64 * q + lane;
+        // pieces past the end get an out-of-range offset (no memory access)
+        const uint32_t off = piece < pieces ? 16u * piece : 0x80000000u;
+        __builtin_amdgcn_raw_ptr_buffer_load_lds(r, (ws_lds_t *)((char *)lds_base + 1024 * q), 16, off, 0, 0, 0);
+    }
+}
+
+// Y rows (g, g+8) of one group: the two rows' entries walked as one list, 8 per
+// step; masked slots read entry o0 and load nothing (out-of-range offset).
+template <typename CP, typename VP>
+__device__ __forceinline__ void ws_gather(CP cp, VP vp, int o0, int len0, int o1, int cnt,
+                                          __amdgpu_buffer_rsrc_t xr, uint32_t lane_off, double y[4])
+{
+    for (int f = 0; f < cnt; f += 8) {
+        int32_t c[8];
+        double v[8];
+#pragma unroll
+        for (int tt = 0; tt < 8; ++tt) {
+            const int ff = f + tt;
+            int o = ff < len0 ? o0 + ff : o1 + (ff - len0);
+            o = ff < cnt ? o : o0;
+            c[tt] = cp[o];
+            v[tt] = vp[o];
+        }
+        double2 xs[8];
+#pragma unroll
+        for (int tt = 0; tt < 8; ++tt) {
+            const uint32_t off = f + tt < cnt ? __umul24((unsigned)c[tt], 128u) + lane_off : 0x80000000u;
+            const auto u4 = __builtin_amdgcn_raw_buffer_load_b128(xr, off, 0, 0);
+            __builtin_memcpy(&xs[tt], &u4, 16);
+        }
+#pragma unroll
+        for (int tt = 0; tt < 8; ++tt) {
+            if (f + tt < len0) {
+                y[0] = fma(v[tt], xs[tt].x, y[0]);
+                y[1] = fma(v[tt], xs[tt].y, y[1]);
+            } else {  // masked entries: x == 0
+                y[2] = fma(v[tt], xs[tt].x, y[2]);
+                y[3] = fma(v[tt], xs[tt].y, y[3]);
+            }
+        }
+    }
+}
+
 }  // namespace lz

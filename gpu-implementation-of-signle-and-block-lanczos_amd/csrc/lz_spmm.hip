@@ -292,9 +292,6 @@ __global__ __launch_bounds__(256, MINW) void k_spmm_buf(int64_t n, const int64_t
 // with the stage.  Every spin is bounded (kWsSpin) so a logic error cannot
 // hang the GPU.  Persistent grid, XCD-aware strided tile order (as
 // k_fused_pw16 had) so an XCD's tiles in flight stay adjacent.
-constexpr int ws_instr(int pieces) { return (pieces + 63) / 64; }
-constexpr long kWsSpin = 1L << 24;
-
 // WS_NC consumer waves (16 rows each), WS_K LDS stages, loader pipeline depth
 // WS_D (tiles whose DMA is in flight), WS_CAP staged nonzeros per tile.
 template <int WS_NC, int WS_K, int WS_D, int WS_CAP>
@@ -315,83 +312,6 @@ struct WsCfg {
     };
 };
 
-typedef __attribute__((address_space(3))) void ws_lds_t;
-
-// LDS word access from the loader wave in inline asm: after an LDS-DMA the
-// compiler inserts vmcnt(0) before any LDS instruction it emits (the DMA could
-// alias it), which would wait for the tile in flight.  These words are never
-// DMA targets.
-__device__ __forceinline__ uint32_t ws_lds_addr(int *p)
-{
-    return (uint32_t)(uintptr_t)(__attribute__((address_space(3))) int *)p;
-}
-__device__ __forceinline__ int ws_lds_read(uint32_t a)
-{
-    int v;
-    asm volatile("ds_read_b32 %0, %1\n\ts_waitcnt lgkmcnt(0)" : "=v"(v) : "v"(a) : "memory");
-    return v;
-}
-__device__ __forceinline__ void ws_lds_write(uint32_t a, int v)
-{
-    asm volatile("ds_write_b32 %0, %1" ::"v"(a), "v"(v) : "memory");
-}
-
-__device__ __forceinline__ void ws_dma(__amdgpu_buffer_rsrc_t r, void *lds_base, int pieces, int lane)
-{
-#pragma unroll
-    for (int q = 0; q < (pieces + 63) / 64; ++q) {
-        const int piece = 64 * q + lane;
-        // pieces past the end get an out-of-range offset (no memory access)
-        const uint32_t off = piece < pieces ? 16u * piece : 0x80000000u;
-        __builtin_amdgcn_raw_ptr_buffer_load_lds(r, (ws_lds_t *)((char *)lds_base + 1024 * q), 16, off, 0, 0, 0);
-    }
-}
-
-// Y rows (g, g+8) of one group: the two rows' entries walked as one list, 8 per
-// step; masked slots read entry o0 and load nothing (out-of-range offset).
-template <typename CP, typename VP>
-__device__ __forceinline__ void ws_gather(CP cp, VP vp, int o0, int len0, int o1, int cnt,
-                                          __amdgpu_buffer_rsrc_t xr, uint32_t lane_off, double y[4])
-{
-    for (int f = 0; f < cnt; f += 8) {
-        int32_t c[8];
-        double v[8];
-#pragma unroll
-        for (int tt = 0; tt < 8; ++tt) {
-            const int ff = f + tt;
-            int o = ff < len0 ? o0 + ff : o1 + (ff - len0);
-            o = ff < cnt ? o : o0;
-            c[tt] = cp[o];
-            v[tt] = vp[o];
-        }
-        double2 xs[8];
-#pragma unroll
-        for (int tt = 0; tt < 8; ++tt) {
-            const uint32_t off = f + tt < cnt ? __umul24((unsigned)c[tt], 128u) + lane_off : 0x80000000u;
-            const auto u4 = __builtin_amdgcn_raw_buffer_load_b128(xr, off, 0, 0);
-            __builtin_memcpy(&xs[tt], &u4, 16);
-        }
-#pragma unroll
-        for (int tt = 0; tt < 8; ++tt) {
-            if (f + tt < len0) {
-                y[0] = fma(v[tt], xs[tt].x, y[0]);
-                y[1] = fma(v[tt], xs[tt].y, y[1]);
-            } else {  // masked entries: x == 0
-                y[2] = fma(v[tt], xs[tt].x, y[2]);
-                y[3] = fma(v[tt], xs[tt].y, y[3]);
-            }
-        }
-    }
-}
-
-#ifdef LZ_WS_PROBE
-// per block: [0] loader cycles waiting on done, [1] loader cycles in vmcnt waits,
-// [2] consumer-0 cycles waiting on ready, [3] consumer-0 total cycles, [4] loader total
-__device__ long long *lz_ws_probe;
-#define WS_T(v) const long long v = clock64()
-#else
-#define WS_T(v)
-#endif
 template <int WS_NC, int WS_K, int WS_D, int WS_CAP>
 __global__ __launch_bounds__(64 * (WS_NC + 1)) void k_spmm_ws(int64_t n, const int64_t *__restrict__ rp,
                                                            const int32_t *__restrict__ col,

@@ -19,7 +19,9 @@ __global__ __launch_bounds__(256) void k_gather(const double *__restrict__ X, ui
     // stream: each block walks its own contiguous slice of Z (16 B per lane per load)
     const int64_t per_block = (int64_t)iters * (S > 0 ? S : 1) * 256 * 2;
     const double *zb = Z + (int64_t)blockIdx.x * per_block + threadIdx.x * 2;
-    const bool stream_only = (mode == 1) && (blockIdx.x & 1);
+    // mode 1: odd blocks stream (they land on other XCDs); mode 2: waves 2,3 of
+    // every block stream (same CU as the gathering waves 0,1)
+    const bool stream_only = (mode == 1 && (blockIdx.x & 1)) || (mode == 2 && (threadIdx.x >> 7));
     for (int it = 0; it < iters; ++it) {
         double2 xs[UNR > 0 ? UNR : 1];
         if (!stream_only) {
@@ -60,11 +62,11 @@ static void run(const double *X, uint32_t rows, const double *Z, int blocks_per_
     hipEventRecord(e1);
     hipEventSynchronize(e1);
     float ms; hipEventElapsedTime(&ms, e0, e1);
-    const double gblocks = mode == 1 ? grid / 2.0 : grid, sblocks = mode == 1 ? grid / 2.0 : grid;
+    const double gblocks = mode ? grid / 2.0 : grid, sblocks = mode ? grid / 2.0 : grid;
     const double gbytes = gblocks * 256 / 8 * iters * UNR * 128;
     const double sbytes = S ? sblocks * 256 * 16.0 * iters * S : 0;
     printf("rows=%u UNR=%d S=%d mode=%s blocks/CU=%d : %.3f ms  gather %.2f TB/s  stream %.2f TB/s\n", rows, UNR, S,
-           mode ? "split" : "mixed", blocks_per_cu, ms, gbytes / ms / 1e9, sbytes / ms / 1e9);
+           mode == 2 ? "wave-split(same CU)" : mode ? "block-split(other XCD)" : "mixed", blocks_per_cu, ms, gbytes / ms / 1e9, sbytes / ms / 1e9);
 }
 
 int main()
@@ -84,6 +86,8 @@ int main()
     run<8, 8>(X, 1u << 13, Z, 4, 0, out);
     run<8, 2>(X, 1u << 13, Z, 4, 1, out);
     run<8, 8>(X, 1u << 13, Z, 4, 1, out);
+    run<8, 2>(X, 1u << 13, Z, 4, 2, out);
+    run<8, 8>(X, 1u << 13, Z, 4, 2, out);
     run<0, 8>(X, 1u << 13, Z, 4, 0, out);
     return 0;
 }
