@@ -38,9 +38,22 @@ def spmm_bytes(n, nnz, b, sv=8):
 
 
 def fused_pass_bytes(n, nnz, b, sv=8):
-    """Algorithmic bytes of one k_fused_spmm16 launch: A, the Krylov block read
+    """Algorithmic bytes of one fused pass-1 launch: A, the Krylov block read
     once, Q_{j-1} read, Q_j and W' written (DESIGN.md "Roofline")."""
     return nnz * (sv + 4) + (n + 1) * 8 + 4 * n * b * sv
+
+
+def fused_kernel():
+    """(full name, PMC short name) of the pass-1 kernel lz_fused.hip launches for
+    b = 16 fp64 (LZ_FUSED_KERNEL selects the diagnostic alternatives)."""
+    v = os.environ.get("LZ_FUSED_KERNEL", "")
+    if v.startswith("t"):
+        return "k_fused_spmm16<true>", "k_fused_spmm16"
+    if v.startswith("p"):
+        return f"k_fused_pf16<{8 if v[1:2] == '8' else 4}>", "k_fused_pf16"
+    if v.startswith("ws8"):
+        return "k_fused_ws16<8,1784,3>", "k_fused_ws16"
+    return "k_fused_ws16<15,2536,2>", "k_fused_ws16"
 
 
 def pmc_traffic(kernel, n, nnz, hw):
@@ -184,8 +197,9 @@ def main():
         t_pass = spmm_ms / max(spmm_cnt, 1) * 1e-3 if spmm_cnt else None
         if fused and t_pass:
             ach = fused_pass_bytes(n, A.nnz, b) / t_pass / 1e9
-            traffic, tsrc = pmc_traffic("k_fused_spmm16", n, A.nnz, args.halfwidth)
-            roof = {"bound": "hbm", "kernel": "k_fused_spmm16", "achieved": round(ach, 1),
+            kname, kshort = fused_kernel()
+            traffic, tsrc = pmc_traffic(kshort, n, A.nnz, args.halfwidth)
+            roof = {"bound": "hbm", "kernel": kname, "achieved": round(ach, 1),
                     "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": round(ach / HBM_PEAK_GBS, 4),
                     "traffic": traffic, "traffic_unit": "bytes/launch", "traffic_source": tsrc,
                     "avg_ms": round(t_pass * 1e3, 4),

@@ -630,6 +630,316 @@ __global__ __launch_bounds__(64 * (NC + 1)) void k_fused_ws16(
 #endif
 }
 
+// ---------------------------------------------------------------------------
+// Per-wave software-pipelined persistent pass 1.  Every wave is independent
+// (no loader, no block barrier after the first): it walks its own strips of 16
+// rows (XCD-contiguous strip ranges, adjacent strips on adjacent waves) and
+// keeps ONE strip of HBM streams in flight in registers -- the next strip's CSR
+// run (16-B loads), its W rows and its Q_{j-1} rows, and the row pointers of
+// the strip after that.  vmcnt retires in order, so the prefetch is issued
+// right AFTER the first gather step of the current strip: that step's wait
+// (usually the only long one -- a 16-row strip of a 10-nnz/row operator is 160
+// entries, 20 per lane group, 3 steps) does not cover the HBM latency, and the
+// prefetched registers have the rest of the strip to land.  At the top of the
+// next strip the registers are committed to the wave's LDS: the run (gather
+// indices), and W/Q rows in XOR-swizzled 16x16 layout for the MFMA epilogue.
+// The prefetch is straight-line code (out-of-range buffer offsets instead of
+// branches): the waitcnt pass merges control-flow paths conservatively, and a
+// path without the prefetch would make every later wait cover it.  Runs longer
+// than kPfCap - 3 entries gather straight from global memory.
+constexpr int kPfCap = 256;
+struct PfWave {
+    int32_t col[kPfCap + 16];  // + slack: slots past the run end read stale entries
+    double val[kPfCap + 16];
+    double wq[2][256];  // W rows, Q_{j-1} rows (then the Y transpose scratch)
+};
+
+struct PfRegs {
+    uint4 c;        // 4 column indices from ca + 4 lane
+    double2 v[2];   // values from va + 2 lane, va + 128 + 2 lane
+    double2 wr[2];  // W row s0 + (lane >> 2), doubles 4 (lane & 3) .. + 3
+    double2 qr[2];  // Q_{j-1}, same layout
+};
+
+__device__ __forceinline__ uint4 pf_ld16(__amdgpu_buffer_rsrc_t r, uint32_t off)
+{
+    const auto u = __builtin_amdgcn_raw_buffer_load_b128(r, off, 0, 0);
+    uint4 o;
+    __builtin_memcpy(&o, &u, 16);
+    return o;
+}
+__device__ __forceinline__ double2 pf_ld16d(__amdgpu_buffer_rsrc_t r, uint32_t off)
+{
+    const auto u = __builtin_amdgcn_raw_buffer_load_b128(r, off, 0, 0);
+    double2 o;
+    __builtin_memcpy(&o, &u, 16);
+    return o;
+}
+
+// lane l <= 16 loads rp[s0 + l] (rows past n are fixed up by pf_rp_fix)
+__device__ __forceinline__ int64_t pf_rp_load(const int64_t *__restrict__ rp, int64_t s0, int64_t n,
+                                              bool live, int lane)
+{
+    const int64_t avail = n + 1 - s0;
+    const int bytes = live ? (int)((avail < 17 ? avail : 17) * 8) : 0;
+    const auto r = __builtin_amdgcn_make_buffer_rsrc(const_cast<int64_t *>(rp + s0), (short)0, bytes, 0x00020000);
+    const auto u = __builtin_amdgcn_raw_buffer_load_b64(r, lane <= 16 ? 8u * lane : 0x80000000u, 0, 0);
+    int64_t v;
+    __builtin_memcpy(&v, &u, 8);
+    return v;
+}
+__device__ __forceinline__ int64_t pf_rp_fix(int64_t v, int64_t s0, int64_t n, int64_t nnz, int lane)
+{
+    return s0 + lane <= n ? v : nnz;
+}
+
+// a wave-uniform int64 from lane `l`
+__device__ __forceinline__ int64_t pf_lane(int64_t v, int l)
+{
+    const int lo = __builtin_amdgcn_readlane((int)(uint64_t)v, l);
+    const int hi = __builtin_amdgcn_readlane((int)((uint64_t)v >> 32), l);
+    return (int64_t)(((uint64_t)(uint32_t)hi << 32) | (uint32_t)lo);
+}
+
+__device__ __forceinline__ int64_t pf_shfl(int64_t v, int src)
+{
+    const int lo = __builtin_amdgcn_ds_bpermute(src << 2, (int)(uint64_t)v);
+    const int hi = __builtin_amdgcn_ds_bpermute(src << 2, (int)((uint64_t)v >> 32));
+    return (int64_t)(((uint64_t)(uint32_t)hi << 32) | (uint32_t)lo);
+}
+
+template <int UNR>
+__global__ __launch_bounds__(512, 4) void k_fused_pf16(
+    int64_t n, const int64_t *__restrict__ rp, const int32_t *__restrict__ col,
+    const double *__restrict__ val, const double *__restrict__ Wg, int64_t nx,
+    const double *__restrict__ Wown, double *__restrict__ Qbuf, double *__restrict__ Wn,
+    const double *__restrict__ binv, const double *__restrict__ beta, int64_t lc,
+    double *__restrict__ qrow, double *__restrict__ part, int dbg)
+{
+    // dbg (diagnostic timing only, results invalid): bit 0 masks the X gathers,
+    // bit 1 masks the HBM streams (run, W, Q), bit 2 drops the stores
+    __shared__ PfWave wl[8];
+    __shared__ double ops[2][256];  // beta^-1, -beta in MFMA B-operand order
+    const int lane_ = threadIdx.x & 63, w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    const bool has_prev = beta != nullptr;
+    for (int e = threadIdx.x; e < 256; e += 512) {
+        const int kc = e >> 6, l = e & 63;
+        const int idx = (4 * kc + (l >> 4)) * 16 + (l & 15);
+        ops[0][e] = binv[idx];
+        ops[1][e] = has_prev ? -beta[idx] : 0.0;
+    }
+    __syncthreads();  // the only block barrier
+    PfWave &L = wl[w];
+    // strips of XCD x: [S x / 8, S (x + 1) / 8); wave kk of the XCD takes
+    // begin + kk, begin + kk + KK, ...
+    const int64_t S = ceil_div(n, (int64_t)16);
+    int64_t begin, end, kk, KK;
+    {
+        const int64_t G = gridDim.x, b = blockIdx.x;
+        if (G < 8) {
+            begin = 0; end = S; kk = b * 8 + w; KK = G * 8;
+        } else {
+            const int64_t x = b & 7;
+            begin = S * x / 8;
+            end = S * (x + 1) / 8;
+            kk = (b >> 3) * 8 + w;
+            KK = ((G - x + 7) >> 3) * 8;
+        }
+    }
+    const int64_t nt = (end - begin - kk + KK - 1) / KK > 0 ? (end - begin - kk + KK - 1) / KK : 0;
+    // strip i's first row (clamped so a dead prefetch still forms a valid base)
+    auto strip0 = [&](int64_t i) {
+        const int64_t s = begin + kk + i * KK;
+        return (s < S ? s : S - 1) * 16;
+    };
+    const int64_t nnz = rp[n];
+    const __amdgpu_buffer_rsrc_t xr =
+        __builtin_amdgcn_make_buffer_rsrc(const_cast<double *>(Wg), (short)0, (int)(nx * 128), 0x00020000);
+
+    // issue the HBM streams of the strip at s0 (row pointers R, fixed up); all
+    // loads are issued, dead ones with out-of-range offsets
+    auto issue = [&](int64_t s0, int64_t R, bool live, PfRegs &P, int lane) {
+        const int64_t kA = pf_lane(R, 0), kB = pf_lane(R, 16);
+        const int64_t ca = kA & ~(int64_t)3, va = kA & ~(int64_t)1;
+        const int cend = (int)(kA - ca + (kB - kA)), vend = (int)(kA - va + (kB - kA));
+        const bool stage = live && cend <= kPfCap && !(dbg & 2);
+        const int64_t cb = (nnz - ca) * 4, vb = (nnz - va) * 8;
+        const auto cr = __builtin_amdgcn_make_buffer_rsrc(const_cast<int32_t *>(col + ca), (short)0,
+                                                          stage ? (int)(cb < 0x7fffffff ? cb : 0x7fffffff) : 0,
+                                                          0x00020000);
+        const auto vr = __builtin_amdgcn_make_buffer_rsrc(const_cast<double *>(val + va), (short)0,
+                                                          stage ? (int)(vb < 0x7fffffff ? vb : 0x7fffffff) : 0,
+                                                          0x00020000);
+        P.c = pf_ld16(cr, 4 * lane < cend ? 16u * lane : 0x80000000u);
+        P.v[0] = pf_ld16d(vr, 2 * lane < vend ? 16u * lane : 0x80000000u);
+        P.v[1] = pf_ld16d(vr, 128 + 2 * lane < vend ? 16u * (64 + lane) : 0x80000000u);
+        const int64_t rows = n - s0 < 16 ? n - s0 : 16;
+        const int wb = live && !(dbg & 2) ? (int)(rows * 128) : 0;
+        const auto wr = __builtin_amdgcn_make_buffer_rsrc(const_cast<double *>(Wown + s0 * 16), (short)0, wb,
+                                                          0x00020000);
+        const auto qr = __builtin_amdgcn_make_buffer_rsrc(Qbuf + s0 * 16, (short)0, has_prev ? wb : 0, 0x00020000);
+        const uint32_t o = (uint32_t)(lane * 32);  // row lane >> 2, doubles 4 (lane & 3) .. + 3
+        P.wr[0] = pf_ld16d(wr, o);
+        P.wr[1] = pf_ld16d(wr, o + 16);
+        P.qr[0] = pf_ld16d(qr, o);
+        P.qr[1] = pf_ld16d(qr, o + 16);
+    };
+
+    PfRegs P;
+    int64_t R0 = 0, R1 = 0;
+    if (nt > 0) {
+        R0 = pf_rp_fix(pf_rp_load(rp, strip0(0), n, true, lane_), strip0(0), n, nnz, lane_);
+        R1 = pf_rp_load(rp, strip0(1), n, nt > 1, lane_);
+        issue(strip0(0), R0, true, P, lane_);
+    }
+    d4_t macc = {0.0, 0.0, 0.0, 0.0};
+    for (int64_t i = 0; i < nt; ++i) {
+        // lane-derived LDS addresses are recomputed per strip (a few VALU ops)
+        // rather than hoisted out of the loop and spilled
+        int lane = lane_;
+        asm volatile("" : "+v"(lane));
+        const int q = lane >> 2, ar = lane & 15;  // group q gathers row s0 + q
+        const uint32_t lane_off = 32u * (lane & 3);
+        const int64_t s0 = strip0(i);
+        const int64_t kA = pf_lane(R0, 0), kB = pf_lane(R0, 16);
+        const int co = (int)(kA & 3), vo = (int)(kA & 1);
+        const bool fast = co + (int)(kB - kA) <= kPfCap;
+        // ---- commit the prefetched registers to the wave's LDS
+        *reinterpret_cast<uint4 *>(&L.col[4 * lane]) = P.c;
+        *reinterpret_cast<double2 *>(&L.val[2 * lane]) = P.v[0];
+        *reinterpret_cast<double2 *>(&L.val[128 + 2 * lane]) = P.v[1];
+        {
+            const int r = lane >> 2, c = 4 * (lane & 3);
+            L.wq[0][fw_sw(r, c + 0)] = P.wr[0].x;
+            L.wq[0][fw_sw(r, c + 1)] = P.wr[0].y;
+            L.wq[0][fw_sw(r, c + 2)] = P.wr[1].x;
+            L.wq[0][fw_sw(r, c + 3)] = P.wr[1].y;
+            L.wq[1][fw_sw(r, c + 0)] = P.qr[0].x;
+            L.wq[1][fw_sw(r, c + 1)] = P.qr[0].y;
+            L.wq[1][fw_sw(r, c + 2)] = P.qr[1].x;
+            L.wq[1][fw_sw(r, c + 3)] = P.qr[1].y;
+        }
+        // this group's row: entries [o, o + len) of the run; steps: the longest row
+        const int o = (int)(pf_shfl(R0, q) - kA);
+        const int len = (int)(pf_shfl(R0, q + 1) - kA) - o;
+        int mx = len;
+#pragma unroll
+        for (int d = 4; d < 64; d <<= 1) mx = max(mx, __shfl_xor(mx, d));
+        const int maxlen = __builtin_amdgcn_readfirstlane(mx);
+        wave_lds_sync();
+        const int32_t *cp = L.col + co + o;
+        const double *vp = L.val + vo + o;
+        double y[4] = {0.0, 0.0, 0.0, 0.0};
+        // UNR slots of this group's row from entry f: 2 x 16-B loads per lane
+        auto gather_issue = [&](int f, double2 (*xs)[2]) {
+            int32_t c[UNR];
+#pragma unroll
+            for (int tt = 0; tt < UNR; ++tt) c[tt] = cp[f + tt];
+            if (dbg & 2) {  // streams masked: synthetic in-band columns
+#pragma unroll
+                for (int tt = 0; tt < UNR; ++tt) {
+                    const int64_t cc = s0 + ((q * 8 + f + tt) * 131) % 8192 - 4096;
+                    c[tt] = (int)(cc < 0 ? 0 : cc >= nx ? nx - 1 : cc);
+                }
+            }
+#pragma unroll
+            for (int tt = 0; tt < UNR; ++tt) {
+                // slots past the row end load a live entry of a later row (or,
+                // past the run, any row: buffer-clamped) and are skipped below
+                const uint32_t off = (dbg & 1) ? 0x80000000u : __umul24((unsigned)c[tt], 128u) + lane_off;
+                const auto u0 = __builtin_amdgcn_raw_buffer_load_b128(xr, off, 0, 0);
+                const auto u1 = __builtin_amdgcn_raw_buffer_load_b128(xr, off + 16, 0, 0);
+                __builtin_memcpy(&xs[tt][0], &u0, 16);
+                __builtin_memcpy(&xs[tt][1], &u1, 16);
+            }
+        };
+        auto fma_step = [&](int f, double2 (*xs)[2]) {
+#pragma unroll
+            for (int tt = 0; tt < UNR; ++tt) {
+                const double v = vp[f + tt];
+                if (f + tt < len) {
+                    y[0] = fma(v, xs[tt][0].x, y[0]);
+                    y[1] = fma(v, xs[tt][0].y, y[1]);
+                    y[2] = fma(v, xs[tt][1].x, y[2]);
+                    y[3] = fma(v, xs[tt][1].y, y[3]);
+                }
+            }
+        };
+        // ---- gather step 0 (every lane)
+        double2 xs[UNR][2];
+        gather_issue(0, xs);
+        // ---- prefetch strip i + 1 and the row pointers of strip i + 2
+        asm volatile("" ::: "memory");
+        const int64_t s1 = strip0(i + 1);
+        issue(s1, pf_rp_fix(R1, s1, n, nnz, lane), i + 1 < nt, P, lane);
+        const int64_t R2 = pf_rp_load(rp, strip0(i + 2), n, i + 2 < nt, lane);
+        asm volatile("" ::: "memory");
+        if (fast) {
+            fma_step(0, xs);
+            for (int f = UNR; f < maxlen; f += UNR) {  // wave-uniform
+                gather_issue(f, xs);
+                fma_step(f, xs);
+            }
+        } else {  // long run (rare): gather from global
+            const int64_t ko = kA + o;
+            for (int f = 0; f < maxlen; ++f) {
+                const bool on = f < len;
+                const int32_t c = on ? col[ko + f] : 0;
+                const double v = on ? val[ko + f] : 0.0;
+                const uint32_t off = on ? __umul24((unsigned)c, 128u) + lane_off : 0x80000000u;
+                const auto u0 = __builtin_amdgcn_raw_buffer_load_b128(xr, off, 0, 0);
+                const auto u1 = __builtin_amdgcn_raw_buffer_load_b128(xr, off + 16, 0, 0);
+                double2 x0, x1;
+                __builtin_memcpy(&x0, &u0, 16);
+                __builtin_memcpy(&x1, &u1, 16);
+                y[0] = fma(v, x0.x, y[0]);
+                y[1] = fma(v, x0.y, y[1]);
+                y[2] = fma(v, x1.x, y[2]);
+                y[3] = fma(v, x1.y, y[3]);
+            }
+        }
+        // ---- epilogue: operands from LDS, products on the matrix cores
+        double ya[4], wa[4], qa[4];
+#pragma unroll
+        for (int kc = 0; kc < 4; ++kc) {
+            wa[kc] = L.wq[0][fw_sw(ar, 4 * kc + (lane >> 4))];
+            qa[kc] = L.wq[1][fw_sw(ar, 4 * kc + (lane >> 4))];
+        }
+        wave_lds_sync();
+        {
+            const int r = lane >> 2, c = 4 * (lane & 3);
+#pragma unroll
+            for (int e = 0; e < 4; ++e) L.wq[0][fw_sw(r, c + e)] = y[e];
+        }
+        wave_lds_sync();
+#pragma unroll
+        for (int kc = 0; kc < 4; ++kc) ya[kc] = L.wq[0][fw_sw(ar, 4 * kc + (lane >> 4))];
+        d4_t q1 = {0.0, 0.0, 0.0, 0.0}, wn = {0.0, 0.0, 0.0, 0.0};
+#pragma unroll
+        for (int kc = 0; kc < 4; ++kc) q1 = mfma16(wa[kc], ops[0][64 * kc + lane], q1);
+#pragma unroll
+        for (int kc = 0; kc < 4; ++kc) wn = mfma16(ya[kc], ops[0][64 * kc + lane], wn);
+#pragma unroll
+        for (int kc = 0; kc < 4; ++kc) wn = mfma16(qa[kc], ops[1][64 * kc + lane], wn);  // 0 if !has_prev
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+            const int64_t row = s0 + (lane >> 4) + 4 * r;
+            if (row < n && !(dbg & 4)) {
+                Qbuf[s0 * 16 + 64 * r + lane] = q1[r];
+                Wn[s0 * 16 + 64 * r + lane] = wn[r];
+                if (row == lc) qrow[lane & 15] = q1[r];
+            }
+        }
+#pragma unroll
+        for (int r = 0; r < 4; ++r) macc = mfma16(q1[r], wn[r], macc);
+        R0 = pf_rp_fix(R1, s1, n, nnz, lane);
+        R1 = R2;
+    }
+    double *slab = part + ((int64_t)blockIdx.x * 8 + w) * 256;
+#pragma unroll
+    for (int r = 0; r < 4; ++r) slab[((lane_ >> 4) + 4 * r) * 16 + (lane_ & 15)] = macc[r];
+}
+
 int fused_spmm16(lz_handle *h, int64_t n, const int64_t *rp, const int32_t *col, const double *val,
                  const double *Wg, int64_t nx, const double *Wown, double *Qbuf, double *Wn, const double *binv,
                  const double *beta, int64_t lc, double *qrow, int *nparts)
@@ -638,6 +948,21 @@ int fused_spmm16(lz_handle *h, int64_t n, const int64_t *rp, const int32_t *col,
     LZ_ARG_CHECK(tiles >= 1 && tiles < (1LL << 31), "tile count");
     const bool buf = nx * 128 < (1LL << 31) && nx < (1 << 24);
     static const char *variant = getenv("LZ_FUSED_KERNEL");  // "tile": the tile-per-block kernel
+    if (buf && variant && variant[0] == 'p') {
+        const int grid = (int)std::max<int64_t>(1, std::min<int64_t>(ceil_div(ceil_div(n, (int64_t)16), 8),
+                                                                     2 * (int64_t)h->n_cu));
+        LZ_TRY(ensure_partials(h, (size_t)grid * 8 * 256));
+        const int ev = prof_begin(h, PROF_SPMM_PASS);
+        if (variant[1] == '8')
+            hipLaunchKernelGGL(k_fused_pf16<8>, dim3(grid), dim3(512), 0, h->stream, n, rp, col, val, Wg, nx,
+                               Wown, Qbuf, Wn, binv, beta, lc, qrow, h->partials, 0);
+        else
+            hipLaunchKernelGGL(k_fused_pf16<4>, dim3(grid), dim3(512), 0, h->stream, n, rp, col, val, Wg, nx,
+                               Wown, Qbuf, Wn, binv, beta, lc, qrow, h->partials, 0);
+        prof_end(h, ev);
+        LZ_LAUNCH_CHECK();
+        return fold_slabs(h, h->partials, (int64_t)grid * 8, 256, nparts);
+    }
     if (buf && !(variant && variant[0] == 't')) {
         // LZ_FUSED_KERNEL=ws<NC digit>: consumer waves per CU (default 15)
         const int nc = (variant && variant[0] == 'w' && variant[2]) ? (variant[2] == '8' ? 8 : 15) : 15;
