@@ -169,3 +169,5 @@ def test_block_b16_long_runs(lz, orc, handle, torch_cuda):
     m, lc = 6, 4321
     got = gpu_block(lz, handle, torch_cuda, A, B, m, lc)
     assert_close_run(lz, m, 16, got, orc.block_lanczos(A, B, m, lc))
+    # the persistent pass-1 kernels' bounded spins never timed out
+    assert handle.device_error() == 0
