@@ -45,15 +45,19 @@ def fused_pass_bytes(n, nnz, b, sv=8):
 
 def fused_kernel():
     """(full name, PMC short name) of the pass-1 kernel lz_fused.hip launches for
-    b = 16 fp64 (LZ_FUSED_KERNEL selects the diagnostic alternatives)."""
+    b = 16 fp64 (LZ_FUSED_KERNEL selects the alternatives kept for A/B runs)."""
     v = os.environ.get("LZ_FUSED_KERNEL", "")
     if v.startswith("t"):
         return "k_fused_spmm16<true>", "k_fused_spmm16"
     if v.startswith("p"):
         return f"k_fused_pf16<{8 if v[1:2] == '8' else 4}>", "k_fused_pf16"
-    if v.startswith("ws8"):
-        return "k_fused_ws16<8,1784,3>", "k_fused_ws16"
-    return "k_fused_ws16<15,2536,2>", "k_fused_ws16"
+    if v.startswith("r"):
+        return "k_fused_pp16<14,2376,3,2>", "k_fused_pp16"
+    if v.startswith("wsq"):
+        return "k_fused_ws16<15,2536,2>", "k_fused_ws16"
+    if v.startswith("n"):
+        return "k_fused_ws16<14,2376,3,true,2>", "k_fused_ws16"
+    return "k_fused_ws16<15,2536,3,true>", "k_fused_ws16"
 
 
 def pmc_traffic(kernel, n, nnz, hw):

@@ -376,32 +376,38 @@ __global__ __launch_bounds__(512) void k_fused_update16(int64_t n, double *__res
 // ---------------------------------------------------------------------------
 // Wave-specialised persistent pass 1 (the k_spmm_ws structure, lz_spmm.hip,
 // plus the fused epilogue).  One block per CU: a LOADER wave streams, per tile
-// of 16*NC rows, the CSR run and the tile's Q_{j-1} rows into a double-buffered
-// LDS stage with LDS-DMA (a fixed number of DMA instructions per tile, so its
-// landing wait is a compile-time vmcnt); NC CONSUMER waves (one 16-row strip
-// each) gather X from L2 (8 loads in flight per lane; gather throughput scales
-// with the number of consumer waves, so NC is as large as LDS and VGPRs allow),
-// load their own W rows (L2-resident: just gathered by neighbouring tiles), run
-// the MFMA epilogue, store Q_j and W', and accumulate Q_j^T W' in registers
-// across their tiles -- one 16x16 slab per consumer wave, no block barrier
-// after the first.  The consumers' memory waits cover only L2 traffic and their
-// own stores, never the HBM streams.  Q strips land in chunk-column-major order
-// (slot c4*16 + r); after reading its Q operand a consumer reuses its strip of
-// the stage as the XOR-swizzled transpose scratch for W and Y.  Rows past n are
-// out of range for the DMA and land as zeros.
-template <int NC, int CAP>
+// of 16*NC rows, the tile's row pointers and CSR run into a ring of FW_K LDS
+// stages with LDS-DMA (a fixed number of DMA instructions per tile, so "the
+// previous tile has landed" is a compile-time vmcnt); NC CONSUMER waves (one
+// 16-row strip each) gather X from L2 (8 loads in flight per lane), load their
+// own W rows (L2-resident: just gathered by neighbouring tiles), run the MFMA
+// epilogue, store Q_j and W', and accumulate Q_j^T W' in registers across
+// their tiles -- one 16x16 slab per consumer wave, no block barrier after the
+// first.  The consumers' memory waits never cover the CSR stream.
+//   QREG (default build): the stage holds only the CSR run, so three stages
+//     fit; each consumer loads its Q_{j-1} strip into registers at the start
+//     of its tile and releases the stage right after its gather.  Measured
+//     1.87 ms against 1.94 ms for the Q-in-stage form at C3.
+//   !QREG: Q_{j-1} strips also land in the stage (chunk-column order, slot
+//     c4*16 + r); a consumer reuses its strip as the XOR-swizzled transpose
+//     scratch and releases the stage after the epilogue.
+//   NL > 1: NL loader waves stage alternate tiles, each publishing its tile as
+//     soon as it lands.
+// Rows past n are out of range for the DMA and land as zeros.
+template <int NC, int CAP, bool QREG = false>
 struct FwCfg {
     static constexpr int TR = 16 * NC;
     static constexpr int RP_PIECES = (TR + 2) * 8 / 16;
     static constexpr int COL_PIECES = (CAP + 8) * 4 / 16;
     static constexpr int VAL_PIECES = (CAP + 4) * 8 / 16;
-    static constexpr int DMA_INSTR = ws_instr(RP_PIECES) + ws_instr(COL_PIECES) + ws_instr(VAL_PIECES) + 2 * NC;
+    static constexpr int DMA_INSTR =
+        ws_instr(RP_PIECES) + ws_instr(COL_PIECES) + ws_instr(VAL_PIECES) + (QREG ? 0 : 2 * NC);
     static_assert(DMA_INSTR <= 63, "vmcnt immediate");
     struct Stage {
         int64_t rp[ws_instr(RP_PIECES) * 128];
         int32_t col[ws_instr(COL_PIECES) * 256];
         double val[ws_instr(VAL_PIECES) * 128];
-        double qt[TR * 16];  // Q_{j-1} rows, per strip in slot order; then scratch
+        double qt[QREG ? 2 : TR * 16];  // Q_{j-1} rows, per strip in slot order; then scratch
     };
 };
 
@@ -425,19 +431,26 @@ __device__ __forceinline__ void fw_strips_dma(__amdgpu_buffer_rsrc_t r, double *
 // operand read (16 rows, one column per lane group) hits 16 distinct banks.
 __device__ __forceinline__ int fw_sw(int r, int c) { return r * 16 + (c ^ r); }
 
-template <int NC, int CAP, int FW_K>
-__global__ __launch_bounds__(64 * (NC + 1)) void k_fused_ws16(
+template <int NC, int CAP, int FW_K, bool QREG = false, int NL = 1>
+__global__ __launch_bounds__(64 * (NC + NL)) void k_fused_ws16(
     int64_t n, const int64_t *__restrict__ rp, const int32_t *__restrict__ col,
     const double *__restrict__ val, const double *__restrict__ Wg, int64_t nx,
     const double *__restrict__ Wown, double *__restrict__ Qbuf, double *__restrict__ Wn,
     const double *__restrict__ binv, const double *__restrict__ beta, int64_t lc,
     double *__restrict__ qrow, double *__restrict__ part, int *__restrict__ err)
 {
-    using C = FwCfg<NC, CAP>;
+    using C = FwCfg<NC, CAP, QREG>;
     constexpr int TR = C::TR;
+#ifdef LZ_WS_PROBE
+    // diagnostic timing masks (results invalid): bit 0 Q DMA, bit 2 stores, bit 3 gathers
+    const int dbg = lz_ws_dbg;
+#else
+    constexpr int dbg = 0;
+#endif
     __shared__ typename C::Stage st[FW_K];
     __shared__ double ops[2][256];  // beta^-1, -beta in MFMA B-operand order
     __shared__ int ready[FW_K], done[FW_K];
+    __shared__ double scr[QREG ? NC : 1][256];  // QREG: per-consumer transpose scratch
     const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
     const bool has_prev = beta != nullptr;
     if (threadIdx.x < FW_K) {
@@ -467,6 +480,47 @@ __global__ __launch_bounds__(64 * (NC + 1)) void k_fused_ws16(
     }
     const int64_t nt = (end - begin - k + K - 1) / K > 0 ? (end - begin - k + K - 1) / K : 0;
     auto tile_r0 = [&](int64_t i) { return (begin + k + i * K) * TR; };
+    if (NL > 1 && w < NL) {
+        // ------------------------------------------------ NL parallel loaders
+        // loader l stages tiles l, l + NL, ...: one tile in flight per loader,
+        // published as soon as it lands (its own vmcnt(0)), so NL tiles are in
+        // flight and a slow consumer delays only the slot it holds
+        __builtin_amdgcn_s_setprio(3);
+        const int64_t nnz = rp[n];
+        for (int64_t i = w; i < nt; i += NL) {
+            const int s = (int)(i % FW_K);
+            const int64_t r0 = tile_r0(i), r1 = (r0 + TR < n) ? r0 + TR : n;
+            const int64_t kA = rp[r0];
+            if (i >= FW_K) {
+                long spin = 0;
+                const uint32_t da = ws_lds_addr(&done[s]);
+                while (ws_lds_read(da) < NC * (int)(i / FW_K) && ++spin < kWsSpin) __builtin_amdgcn_s_sleep(1);
+                if (spin >= kWsSpin) { *err = 3; break; }
+            }
+            WS_TL(i, 0);
+            const int64_t ca = kA & ~(int64_t)3, va = kA & ~(int64_t)1;
+            const int64_t cb = (nnz - ca) * 4, vb = (nnz - va) * 8;
+            const auto rr = __builtin_amdgcn_make_buffer_rsrc(const_cast<int64_t *>(rp + r0), (short)0,
+                                                              (int)((r1 - r0 + 1) * 8), 0x00020000);
+            const auto cr = __builtin_amdgcn_make_buffer_rsrc(const_cast<int32_t *>(col + ca), (short)0,
+                                                              (int)(cb < 0x7fffffff ? cb : 0x7fffffff), 0x00020000);
+            const auto vr = __builtin_amdgcn_make_buffer_rsrc(const_cast<double *>(val + va), (short)0,
+                                                              (int)(vb < 0x7fffffff ? vb : 0x7fffffff), 0x00020000);
+            ws_dma(rr, st[s].rp, C::RP_PIECES, lane);
+            ws_dma(cr, st[s].col, C::COL_PIECES, lane);
+            ws_dma(vr, st[s].val, C::VAL_PIECES, lane);
+            if constexpr (!QREG) {
+                const auto qr = __builtin_amdgcn_make_buffer_rsrc(Qbuf + r0 * 16, (short)0,
+                                                                  has_prev && !(dbg & 1) ? (int)((r1 - r0) * 128) : 0,
+                                                                  0x00020000);
+                fw_strips_dma<NC>(qr, st[s].qt, lane);
+            }
+            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+            if (lane == 0) ws_lds_write(ws_lds_addr(&ready[s]), (int)i);
+            WS_TL(i, 1);
+        }
+        return;
+    }
     if (w == 0) {
         // ------------------------------------------------------------ loader
         // highest issue priority: the loader's DMA must not queue behind the
@@ -493,6 +547,7 @@ __global__ __launch_bounds__(64 * (NC + 1)) void k_fused_ws16(
                 c_done += clock64() - t0;
 #endif
             }
+            WS_TL(i, 0);
             const int64_t ca = kA & ~(int64_t)3, va = kA & ~(int64_t)1;
             const int64_t cb = (nnz - ca) * 4, vb = (nnz - va) * 8;
             const auto rr = __builtin_amdgcn_make_buffer_rsrc(const_cast<int64_t *>(rp + r0), (short)0,
@@ -502,14 +557,16 @@ __global__ __launch_bounds__(64 * (NC + 1)) void k_fused_ws16(
             const auto vr = __builtin_amdgcn_make_buffer_rsrc(const_cast<double *>(val + va), (short)0,
                                                               (int)(vb < 0x7fffffff ? vb : 0x7fffffff), 0x00020000);
             const auto qr = __builtin_amdgcn_make_buffer_rsrc(Qbuf + r0 * 16, (short)0,
-                                                              has_prev ? (int)((r1 - r0) * 128) : 0, 0x00020000);
+                                                              has_prev && !(dbg & 1) ? (int)((r1 - r0) * 128) : 0,
+                                                              0x00020000);
             ws_dma(rr, st[s].rp, C::RP_PIECES, lane);
             ws_dma(cr, st[s].col, C::COL_PIECES, lane);
             ws_dma(vr, st[s].val, C::VAL_PIECES, lane);
-            fw_strips_dma<NC>(qr, st[s].qt, lane);
+            if constexpr (!QREG) fw_strips_dma<NC>(qr, st[s].qt, lane);
             if (i >= 1) {  // tile i-1 has landed once only tile i's DMA is younger
                 asm volatile("s_waitcnt vmcnt(%0)" ::"n"(C::DMA_INSTR) : "memory");
                 if (lane == 0) ws_lds_write(ws_lds_addr(&ready[(int)((i - 1) % FW_K)]), (int)(i - 1));
+                WS_TL(i - 1, 1);
             }
         }
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
@@ -524,9 +581,9 @@ __global__ __launch_bounds__(64 * (NC + 1)) void k_fused_ws16(
         return;
     }
     // -------------------------------------------------------------- consumers
-    const int cw = w - 1, g = lane >> 3, p = lane & 7;
-    const __amdgpu_buffer_rsrc_t xr =
-        __builtin_amdgcn_make_buffer_rsrc(const_cast<double *>(Wg), (short)0, (int)(nx * 128), 0x00020000);
+    const int cw = w - NL, g = lane >> 3, p = lane & 7;
+    const __amdgpu_buffer_rsrc_t xr = __builtin_amdgcn_make_buffer_rsrc(const_cast<double *>(Wg), (short)0,
+                                                                        (dbg & 8) ? 0 : (int)(nx * 128), 0x00020000);
     const uint32_t lane_off = 16u * p;
     d4_t macc = {0.0, 0.0, 0.0, 0.0};
 #ifdef LZ_WS_PROBE
@@ -538,8 +595,9 @@ __global__ __launch_bounds__(64 * (NC + 1)) void k_fused_ws16(
         const int64_t r0 = tile_r0(i);
         const int64_t s0 = r0 + 16 * cw;  // this wave's strip
         // own W rows (L2): lane holds row s0 + (lane >> 2), doubles 4(lane&3)..+3
-        double wv[4];
+        double wv[4], qv[4] = {0.0, 0.0, 0.0, 0.0};
         tile_load(Wown, s0, n, lane, wv);
+        if (QREG && has_prev) tile_load(Qbuf, s0, n, lane, qv);  // Q_{j-1} rows (L2: touched)
         long spin = 0;
         WS_T(t2);
         while (__hip_atomic_load(&ready[s], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP) != (int)i &&
@@ -549,6 +607,7 @@ __global__ __launch_bounds__(64 * (NC + 1)) void k_fused_ws16(
 #ifdef LZ_WS_PROBE
         c_ready += clock64() - t2;
 #endif
+        WS_TL(i, 2 + 2 * cw);
         asm volatile("" ::: "memory");
         typename C::Stage &S = st[s];
         const int64_t kA = S.rp[0];
@@ -569,14 +628,26 @@ __global__ __launch_bounds__(64 * (NC + 1)) void k_fused_ws16(
 #ifdef LZ_WS_PROBE
         c_gather += clock64() - t3;
 #endif
+        if constexpr (QREG) {  // the stage holds only the CSR run: release it now
+            asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+            if (lane == 0) atomicAdd(&done[s], 1);
+        }
         // ---- epilogue operands (A operand a[kc] = M[l&15][4kc + (l>>4)])
-        double *Sc = S.qt + 256 * cw;  // Q strip, then this wave's scratch
+        double *Sc = QREG ? scr[cw] : S.qt + 256 * cw;  // Q strip, then this wave's scratch
         double ya[4], wa[4], qa[4];
         const int ar = lane & 15;
+        if constexpr (QREG) {
 #pragma unroll
-        for (int kc = 0; kc < 4; ++kc) {
-            const int c = 4 * kc + (lane >> 4);
-            qa[kc] = Sc[((c >> 1) * 16 + ar) * 2 + (c & 1)];
+            for (int q = 0; q < 4; ++q) Sc[fw_sw(lane >> 2, 4 * (lane & 3) + q)] = qv[q];
+            wave_lds_sync();
+#pragma unroll
+            for (int kc = 0; kc < 4; ++kc) qa[kc] = Sc[fw_sw(ar, 4 * kc + (lane >> 4))];
+        } else {
+#pragma unroll
+            for (int kc = 0; kc < 4; ++kc) {
+                const int c = 4 * kc + (lane >> 4);
+                qa[kc] = Sc[((c >> 1) * 16 + ar) * 2 + (c & 1)];
+            }
         }
         wave_lds_sync();
         // W rows -> scratch -> operand
@@ -594,9 +665,10 @@ __global__ __launch_bounds__(64 * (NC + 1)) void k_fused_ws16(
         wave_lds_sync();
 #pragma unroll
         for (int kc = 0; kc < 4; ++kc) ya[kc] = Sc[fw_sw(ar, 4 * kc + (lane >> 4))];
-        // the stage is no longer used by this wave
-        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-        if (lane == 0) atomicAdd(&done[s], 1);
+        if constexpr (!QREG) {  // the stage is no longer used by this wave
+            asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+            if (lane == 0) atomicAdd(&done[s], 1);
+        }
         d4_t q1 = {0.0, 0.0, 0.0, 0.0}, wn = {0.0, 0.0, 0.0, 0.0};
 #pragma unroll
         for (int kc = 0; kc < 4; ++kc) q1 = mfma16(wa[kc], ops[0][64 * kc + lane], q1);
@@ -609,7 +681,7 @@ __global__ __launch_bounds__(64 * (NC + 1)) void k_fused_ws16(
 #pragma unroll
         for (int r = 0; r < 4; ++r) {
             const int64_t row = s0 + (lane >> 4) + 4 * r;
-            if (row < n) {
+            if (row < n && !(dbg & 4)) {
                 Qbuf[s0 * 16 + 64 * r + lane] = q1[r];
                 Wn[s0 * 16 + 64 * r + lane] = wn[r];
                 if (row == lc) qrow[lane & 15] = q1[r];
@@ -617,6 +689,7 @@ __global__ __launch_bounds__(64 * (NC + 1)) void k_fused_ws16(
         }
 #pragma unroll
         for (int r = 0; r < 4; ++r) macc = mfma16(q1[r], wn[r], macc);
+        WS_TL(i, 3 + 2 * cw);
     }
     double *slab = part + ((int64_t)blockIdx.x * NC + cw) * 256;
 #pragma unroll
@@ -628,6 +701,275 @@ __global__ __launch_bounds__(64 * (NC + 1)) void k_fused_ws16(
         lz_ws_probe[8 * blockIdx.x + 0] = c_gather;
     }
 #endif
+}
+
+// ---------------------------------------------------------------------------
+// Pipelined wave-specialised pass 1.  Timelines of k_fused_ws16
+// (scripts/probe/tl_probe.hip) show two serialisations: a single loader
+// publishes a stage only after issuing the next one (so a stage's readiness
+// waits on the slowest consumer), and each consumer runs gather -> epilogue ->
+// gather with nothing in flight during its epilogue.  Here
+// - NL loader waves stage tiles l, l + NL, ... (CSR run only), each publishing
+//   its tile as soon as it lands (its own vmcnt(0));
+// - a consumer issues the first gather step of strip i, THEN runs the epilogue
+//   of strip i-1 (its Y tile parked in LDS, its W / Q_{j-1} rows loaded into
+//   registers after strip i-1's gather), so the epilogue hides the first
+//   gather round trip;
+template <int NC, int CAP, int K, int NL>
+__global__ __launch_bounds__(64 * (NC + NL)) void k_fused_pp16(
+    int64_t n, const int64_t *__restrict__ rp, const int32_t *__restrict__ col,
+    const double *__restrict__ val, const double *__restrict__ Wg, int64_t nx,
+    const double *__restrict__ Wown, double *__restrict__ Qbuf, double *__restrict__ Wn,
+    const double *__restrict__ binv, const double *__restrict__ beta, int64_t lc,
+    double *__restrict__ qrow, double *__restrict__ part, int *__restrict__ err)
+{
+    using C = FwCfg<NC, CAP, true>;
+    constexpr int TR = C::TR;
+#ifdef LZ_WS_PROBE
+    const int dbg = lz_ws_dbg;  // timing masks: bit 0 skips the Q_{j-1} loads, bit 1 the W loads
+#else
+    constexpr int dbg = 0;
+#endif
+    __shared__ typename C::Stage st[K];
+    __shared__ double scr[NC][256];  // per consumer: the parked Y tile (swizzled)
+    __shared__ double ops[2][256];      // beta^-1, -beta in MFMA B-operand order
+    __shared__ int ready[K], done[K];
+    const int lane = threadIdx.x & 63, w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    const bool has_prev = beta != nullptr;
+    if (threadIdx.x < K) {
+        ready[threadIdx.x] = -1;
+        done[threadIdx.x] = 0;
+    }
+    for (int e = threadIdx.x; e < 256; e += blockDim.x) {
+        const int kc = e >> 6, l = e & 63;
+        const int idx = (4 * kc + (l >> 4)) * 16 + (l & 15);
+        ops[0][e] = binv[idx];
+        ops[1][e] = has_prev ? -beta[idx] : 0.0;
+    }
+    __syncthreads();  // the only block barrier
+    const int64_t T = ceil_div(n, (int64_t)TR);
+    int64_t begin, end, kb, KB;
+    {
+        const int64_t G = gridDim.x, b = blockIdx.x;
+        if (G < 8) {
+            begin = 0; end = T; kb = b; KB = G;
+        } else {
+            const int64_t x = b & 7;
+            begin = T * x / 8;
+            end = T * (x + 1) / 8;
+            kb = b >> 3;
+            KB = (G - x + 7) >> 3;
+        }
+    }
+    const int64_t nt = (end - begin - kb + KB - 1) / KB > 0 ? (end - begin - kb + KB - 1) / KB : 0;
+    auto tile_r0 = [&](int64_t i) { return (begin + kb + i * KB) * TR; };
+    if (w < NL) {
+        // ------------------------------------------------------------ loaders
+        __builtin_amdgcn_s_setprio(3);
+        const int64_t nnz = rp[n];
+        for (int64_t i = w; i < nt; i += NL) {
+            const int s = (int)(i % K);
+            const int64_t r0 = tile_r0(i), r1 = (r0 + TR < n) ? r0 + TR : n;
+            const int64_t kA = rp[r0];
+            if (i >= K) {
+                long spin = 0;
+                const uint32_t da = ws_lds_addr(&done[s]);
+                while (ws_lds_read(da) < NC * (int)(i / K) && ++spin < kWsSpin) __builtin_amdgcn_s_sleep(1);
+                if (spin >= kWsSpin) { *err = 3; break; }
+            }
+            WS_TL(i, 0);
+            const int64_t ca = kA & ~(int64_t)3, va = kA & ~(int64_t)1;
+            const int64_t cb = (nnz - ca) * 4, vb = (nnz - va) * 8;
+            const auto rr = __builtin_amdgcn_make_buffer_rsrc(const_cast<int64_t *>(rp + r0), (short)0,
+                                                              (int)((r1 - r0 + 1) * 8), 0x00020000);
+            const auto cr = __builtin_amdgcn_make_buffer_rsrc(const_cast<int32_t *>(col + ca), (short)0,
+                                                              (int)(cb < 0x7fffffff ? cb : 0x7fffffff), 0x00020000);
+            const auto vr = __builtin_amdgcn_make_buffer_rsrc(const_cast<double *>(val + va), (short)0,
+                                                              (int)(vb < 0x7fffffff ? vb : 0x7fffffff), 0x00020000);
+            ws_dma(rr, st[s].rp, C::RP_PIECES, lane);
+            ws_dma(cr, st[s].col, C::COL_PIECES, lane);
+            ws_dma(vr, st[s].val, C::VAL_PIECES, lane);
+            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+            if (lane == 0) ws_lds_write(ws_lds_addr(&ready[s]), (int)i);
+            WS_TL(i, 1);
+        }
+        return;
+    }
+    // -------------------------------------------------------------- consumers
+    const int cw = w - NL;
+    // The SQ favours older (lower-numbered) waves at equal priority: measured
+    // per-consumer strip times rise ~35 % from the first to the last consumer,
+    // and every tile waits for its slowest consumer.  Later consumers get a
+    // higher issue priority (the loaders keep the highest).
+#ifdef LZ_WS_PROBE
+    if (!(lz_ws_dbg & 16))
+#endif
+    {
+        const int pr = (cw * 3) / NC;
+        if (pr == 1) __builtin_amdgcn_s_setprio(1);
+        else if (pr == 2) __builtin_amdgcn_s_setprio(2);
+    }
+    const __amdgpu_buffer_rsrc_t xr =
+        __builtin_amdgcn_make_buffer_rsrc(const_cast<double *>(Wg), (short)0, (int)(nx * 128), 0x00020000);
+    double *S0 = scr[cw];
+    d4_t macc = {0.0, 0.0, 0.0, 0.0};
+    // the pending strip's W and Q_{j-1} rows, loaded straight into MFMA
+    // A-operand order (a[kc] = M[l & 15][4 kc + (l >> 4)]: four 8-B loads per
+    // lane, 512 B per instruction), so the epilogue needs no LDS transpose for them
+    double wa[4] = {0.0, 0.0, 0.0, 0.0}, qa[4] = {0.0, 0.0, 0.0, 0.0};
+    auto aop_load = [&](const double *src, int64_t s0, double a[4]) {
+        const int rows = (int)(n - s0 < 16 ? (n - s0 > 0 ? n - s0 : 0) : 16);  // strips past n: none
+        const auto r = __builtin_amdgcn_make_buffer_rsrc(const_cast<double *>(src + (s0 < n ? s0 : 0) * 16), (short)0,
+                                                         rows * 128, 0x00020000);
+#pragma unroll
+        for (int kc = 0; kc < 4; ++kc) {
+            const auto u = __builtin_amdgcn_raw_buffer_load_b64(
+                r, (uint32_t)((lane & 15) * 128 + (4 * kc + (lane >> 4)) * 8), 0, 0);
+            __builtin_memcpy(&a[kc], &u, 8);
+        }
+    };
+    int64_t s0p = -1;  // strip whose epilogue is pending
+#ifdef LZ_WS_PROBE
+    long long ph[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+#define PP_T(v) const long long v = clock64()
+#else
+#define PP_T(v)
+#endif
+    // epilogue of the pending strip: Y parked in S0 (swizzled), W/Q rows in wv/qv
+    auto epilogue = [&]() {
+        const int ar = lane & 15;
+        double ya[4];
+#pragma unroll
+        for (int kc = 0; kc < 4; ++kc) ya[kc] = S0[fw_sw(ar, 4 * kc + (lane >> 4))];
+        d4_t q1 = {0.0, 0.0, 0.0, 0.0}, wn = {0.0, 0.0, 0.0, 0.0};
+#pragma unroll
+        for (int kc = 0; kc < 4; ++kc) q1 = mfma16(wa[kc], ops[0][64 * kc + lane], q1);
+#pragma unroll
+        for (int kc = 0; kc < 4; ++kc) wn = mfma16(qa[kc], ops[1][64 * kc + lane], wn);  // qa == 0 if !has_prev
+#pragma unroll
+        for (int kc = 0; kc < 4; ++kc) wn = mfma16(ya[kc], ops[0][64 * kc + lane], wn);
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+            const int64_t row = s0p + (lane >> 4) + 4 * r;
+            if (row < n) {
+                Qbuf[s0p * 16 + 64 * r + lane] = q1[r];
+                Wn[s0p * 16 + 64 * r + lane] = wn[r];
+                if (row == lc) qrow[lane & 15] = q1[r];
+            }
+        }
+#pragma unroll
+        for (int r = 0; r < 4; ++r) macc = mfma16(q1[r], wn[r], macc);
+    };
+    for (int64_t i = 0; i < nt; ++i) {
+        const int s = (int)(i % K);
+        const int64_t r0 = tile_r0(i);
+        const int64_t s0 = r0 + 16 * cw;
+        const int g = lane >> 3, p = lane & 7;
+        const uint32_t lane_off = 16u * p;
+        long spin = 0;
+        PP_T(ta);
+        while (__hip_atomic_load(&ready[s], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP) != (int)i &&
+               ++spin < kWsSpin)
+            __builtin_amdgcn_s_sleep(1);
+        if (spin >= kWsSpin) { *err = 4; break; }
+        PP_T(tb);
+        WS_TL(i, 2 + 2 * cw);
+        asm volatile("" ::: "memory");
+        typename C::Stage &S = st[s];
+        const int64_t kA = S.rp[0];
+        const int co = (int)(kA & 3), vo = (int)(kA & 1);
+        const int nrow = (int)(n - r0 < TR ? n - r0 : TR);
+        const int runlen = (int)(S.rp[nrow] - kA);
+        const int lr = 16 * cw + g;
+        const int o0 = lr < nrow ? (int)(S.rp[lr] - kA) : 0;
+        const int len0 = lr < nrow ? (int)(S.rp[lr + 1] - kA) - o0 : 0;
+        const int o1 = lr + 8 < nrow ? (int)(S.rp[lr + 8] - kA) : 0;
+        const int len1 = lr + 8 < nrow ? (int)(S.rp[lr + 9] - kA) - o1 : 0;
+        const int cnt = len0 + len1;
+        double y[4] = {0.0, 0.0, 0.0, 0.0};
+        if (runlen <= CAP) {  // tile-uniform
+            const int32_t *cp = S.col + co;
+            const double *vp = S.val + vo;
+            auto slot = [&](int ff) {
+                const int o = ff < len0 ? o0 + ff : o1 + (ff - len0);
+                return ff < cnt ? o : o0;
+            };
+            auto issue = [&](int f, double2 *xs) {
+                int32_t c[8];
+#pragma unroll
+                for (int tt = 0; tt < 8; ++tt) c[tt] = cp[slot(f + tt)];
+#pragma unroll
+                for (int tt = 0; tt < 8; ++tt) {
+                    const uint32_t off =
+                        f + tt < cnt ? __umul24((unsigned)c[tt], 128u) + lane_off : 0x80000000u;
+                    const auto u4 = __builtin_amdgcn_raw_buffer_load_b128(xr, off, 0, 0);
+                    __builtin_memcpy(&xs[tt], &u4, 16);
+                }
+            };
+            auto fmas = [&](int f, const double2 *xs) {
+#pragma unroll
+                for (int tt = 0; tt < 8; ++tt) {
+                    const double v = vp[slot(f + tt)];
+                    if (f + tt < len0) {
+                        y[0] = fma(v, xs[tt].x, y[0]);
+                        y[1] = fma(v, xs[tt].y, y[1]);
+                    } else {  // masked entries: x == 0, v finite
+                        y[2] = fma(v, xs[tt].x, y[2]);
+                        y[3] = fma(v, xs[tt].y, y[3]);
+                    }
+                }
+            };
+            double2 xs[8];
+            PP_T(tc);
+            issue(0, xs);  // step 0 for every lane (masked past cnt)
+            PP_T(td);
+            if (s0p >= 0) epilogue();
+            PP_T(te);
+            fmas(0, xs);
+            PP_T(tf);
+            for (int f = 8; f < cnt; f += 8) {  // group-uniform
+                issue(f, xs);
+                fmas(f, xs);
+            }
+            PP_T(tg);
+#ifdef LZ_WS_PROBE
+            ph[1] += tc - tb; ph[2] += td - tc; ph[3] += te - td; ph[4] += tf - te; ph[5] += tg - tf;
+#endif
+        } else {  // long run (rare): epilogue first, then gather from global
+            if (s0p >= 0) epilogue();
+            ws_gather(col + kA, val + kA, o0, len0, o1, cnt, xr, lane_off, y);
+        }
+        // the CSR stage is no longer read by this wave
+        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+        if (lane == 0) atomicAdd(&done[s], 1);
+        // park Y (swizzled) and fetch this strip's W and Q_{j-1} rows for its
+        // epilogue, which runs behind the next strip's first gather step
+        S0[fw_sw(g, 2 * p)] = y[0];
+        S0[fw_sw(g, 2 * p + 1)] = y[1];
+        S0[fw_sw(g + 8, 2 * p)] = y[2];
+        S0[fw_sw(g + 8, 2 * p + 1)] = y[3];
+        if (!(dbg & 2)) aop_load(Wown, s0, wa);
+        if (has_prev && !(dbg & 1)) aop_load(Qbuf, s0, qa);
+        s0p = s0;
+        wave_lds_sync();
+        WS_TL(i, 3 + 2 * cw);
+#ifdef LZ_WS_PROBE
+        {
+            PP_T(th);
+            ph[0] += tb - ta;
+            ph[6] += th - ta;
+        }
+#endif
+    }
+#ifdef LZ_WS_PROBE
+    if (cw == 0 && lane == 0)
+        for (int j = 0; j < 7; ++j) lz_ws_probe[8 * blockIdx.x + j] = ph[j];
+    if (cw == 0 && lane == 0) lz_ws_probe[8 * blockIdx.x + 7] = nt;
+#endif
+    if (s0p >= 0) epilogue();
+    double *slab = part + ((int64_t)blockIdx.x * NC + cw) * 256;
+#pragma unroll
+    for (int r = 0; r < 4; ++r) slab[((lane >> 4) + 4 * r) * 16 + (lane & 15)] = macc[r];
 }
 
 // ---------------------------------------------------------------------------
@@ -963,19 +1305,36 @@ int fused_spmm16(lz_handle *h, int64_t n, const int64_t *rp, const int32_t *col,
         LZ_LAUNCH_CHECK();
         return fold_slabs(h, h->partials, (int64_t)grid * 8, 256, nparts);
     }
+    if (buf && variant && variant[0] == 'r') {  // pipelined consumers, two parallel loaders
+        constexpr int NCR = 14;
+        const int grid = (int)std::max<int64_t>(1, std::min<int64_t>(ceil_div(n, (int64_t)16 * NCR), h->n_cu));
+        LZ_TRY(ensure_partials(h, (size_t)grid * NCR * 256));
+        const int ev = prof_begin(h, PROF_SPMM_PASS);
+        hipLaunchKernelGGL((k_fused_pp16<NCR, 2376, 3, 2>), dim3(grid), dim3(64 * 16), 0, h->stream, n, rp, col,
+                           val, Wg, nx, Wown, Qbuf, Wn, binv, beta, lc, qrow, h->partials, h->err_flag);
+        prof_end(h, ev);
+        LZ_LAUNCH_CHECK();
+        return fold_slabs(h, h->partials, (int64_t)grid * NCR, 256, nparts);
+    }
     if (buf && !(variant && variant[0] == 't')) {
-        // LZ_FUSED_KERNEL=ws<NC digit>: consumer waves per CU (default 15)
-        const int nc = (variant && variant[0] == 'w' && variant[2]) ? (variant[2] == '8' ? 8 : 15) : 15;
-        const int tr = 16 * nc;
-        const int grid = (int)std::max<int64_t>(1, std::min<int64_t>(ceil_div(n, (int64_t)tr), h->n_cu));
+        // default: one loader, CSR-only stages (3), Q_{j-1} rows loaded by the
+        // consumers; LZ_FUSED_KERNEL=wsq: Q_{j-1} strips in the stage (2 stages);
+        // LZ_FUSED_KERNEL=nl2: two loaders staging alternate tiles, 14 consumers
+        const bool wsq = variant && variant[0] == 'w' && variant[2] == 'q';
+        const bool nl2 = variant && variant[0] == 'n';
+        const int nc = nl2 ? 14 : 15;
+        const int grid = (int)std::max<int64_t>(1, std::min<int64_t>(ceil_div(n, (int64_t)16 * nc), h->n_cu));
         LZ_TRY(ensure_partials(h, (size_t)grid * nc * 256));
         const int ev = prof_begin(h, PROF_SPMM_PASS);
-        if (nc == 8)
-            hipLaunchKernelGGL((k_fused_ws16<8, 1784, 3>), dim3(grid), dim3(64 * 9), 0, h->stream, n, rp, col,
-                               val, Wg, nx, Wown, Qbuf, Wn, binv, beta, lc, qrow, h->partials, h->err_flag);
-        else
+        if (wsq)
             hipLaunchKernelGGL((k_fused_ws16<15, 2536, 2>), dim3(grid), dim3(64 * 16), 0, h->stream, n, rp, col,
                                val, Wg, nx, Wown, Qbuf, Wn, binv, beta, lc, qrow, h->partials, h->err_flag);
+        else if (nl2)
+            hipLaunchKernelGGL((k_fused_ws16<14, 2376, 3, true, 2>), dim3(grid), dim3(64 * 16), 0, h->stream, n,
+                               rp, col, val, Wg, nx, Wown, Qbuf, Wn, binv, beta, lc, qrow, h->partials, h->err_flag);
+        else
+            hipLaunchKernelGGL((k_fused_ws16<15, 2536, 3, true>), dim3(grid), dim3(64 * 16), 0, h->stream, n, rp,
+                               col, val, Wg, nx, Wown, Qbuf, Wn, binv, beta, lc, qrow, h->partials, h->err_flag);
         prof_end(h, ev);
         LZ_LAUNCH_CHECK();
         return fold_slabs(h, h->partials, (int64_t)grid * nc, 256, nparts);

@@ -108,9 +108,21 @@ constexpr int ws_instr(int pieces) { return (pieces + 63) / 64; }
 #ifdef LZ_WS_PROBE
 // diagnostic builds (scripts/probe/ws_probe*.hip): per-block wait/cycle records
 __device__ long long *lz_ws_probe;
+__device__ int lz_ws_dbg;  // diagnostic timing masks (probe builds only)
 #define WS_T(v) const long long v = clock64()
 #else
 #define WS_T(v)
+#endif
+#ifdef LZ_WS_PROBE_TL
+// per-tile event timeline of blocks 0-3 (tiles < 256): 32 stamps per tile
+__device__ long long *lz_ws_tl;
+#define WS_TL(tile, slot)                                                                        \
+    do {                                                                                         \
+        if (blockIdx.x < 4 && (tile) < 256 && (threadIdx.x & 63) == 0)                         \
+            lz_ws_tl[((int64_t)blockIdx.x * 256 + (tile)) * 32 + (slot)] = clock64();           \
+    } while (0)
+#else
+#define WS_TL(tile, slot)
 #endif
 constexpr long kWsSpin = 1L << 24;
 

@@ -13,7 +13,7 @@ void prof_end(lz_handle *, int) {}
 int ensure_partials(lz_handle *, size_t) { return 0; }
 }  // namespace lzprobe
 
-template <int NC, int CAP, int KS>
+template <int NC, int CAP, int KS, bool QREG = false>
 static void run(int64_t n, const int64_t *drp, const int32_t *dcol, const double *dval, const double *W, double *Q,
                 double *Wn, const double *bi, const double *be, double *qrow, double *part, int *err, long long *rec)
 {
@@ -22,7 +22,7 @@ static void run(int64_t n, const int64_t *drp, const int32_t *dcol, const double
     hipEventCreate(&e0); hipEventCreate(&e1);
     for (int it = 0; it < 3; ++it) {
         hipEventRecord(e0);
-        hipLaunchKernelGGL((lzprobe::k_fused_ws16<NC, CAP, KS>), dim3(grid), dim3(64 * (NC + 1)), 0, 0, n, drp, dcol, dval,
+        hipLaunchKernelGGL((lzprobe::k_fused_ws16<NC, CAP, KS, QREG>), dim3(grid), dim3(64 * (NC + 1)), 0, 0, n, drp, dcol, dval,
                            W, n, W, Q, Wn, bi, be, (int64_t)-1, qrow, part, err);
         hipEventRecord(e1);
         hipEventSynchronize(e1);
@@ -32,8 +32,8 @@ static void run(int64_t n, const int64_t *drp, const int32_t *dcol, const double
     hipMemcpy(h.data(), rec, grid * 64, hipMemcpyDeviceToHost);
     double s[6] = {0};
     for (int b = 0; b < grid; ++b) for (int j = 0; j < 6; ++j) s[j] += h[8 * b + j];
-    printf("NC=%d CAP=%d K=%d: %.3f ms; per block: loader %.0f cyc (done-wait %.0f); consumer0 %.0f (ready-wait %.0f, "
-           "gather %.0f); tiles %.1f\n", NC, CAP, KS, ms, s[4] / grid, s[1] / grid, s[3] / grid, s[2] / grid, s[0] / grid,
+    printf("NC=%d CAP=%d K=%d QREG=%d: %.3f ms; per block: loader %.0f cyc (done-wait %.0f); consumer0 %.0f (ready-wait %.0f, "
+           "gather %.0f); tiles %.1f\n", NC, CAP, KS, (int)QREG, ms, s[4] / grid, s[1] / grid, s[3] / grid, s[2] / grid, s[0] / grid,
            s[5] / grid);
 }
 
@@ -59,10 +59,14 @@ int main()
     hipMemcpy(bi, eye.data(), 2048, hipMemcpyHostToDevice);
     hipMemcpy(be, eye.data(), 2048, hipMemcpyHostToDevice);
     hipMemcpyToSymbol(HIP_SYMBOL(lzprobe::lz_ws_probe), &rec, sizeof(rec));
-    run<15, 2536, 2>(n, drp, dcol, dval, W, Q, Wn, bi, be, qrow, part, err, rec);
-    run<8, 1784, 2>(n, drp, dcol, dval, W, Q, Wn, bi, be, qrow, part, err, rec);
-    run<8, 1784, 3>(n, drp, dcol, dval, W, Q, Wn, bi, be, qrow, part, err, rec);
-    run<12, 1936, 2>(n, drp, dcol, dval, W, Q, Wn, bi, be, qrow, part, err, rec);
+    // dbg masks (timing only): 1 = no Q DMA, 4 = no stores, 8 = no gathers
+    for (int dbg : {0, 8}) {
+        hipMemcpyToSymbol(HIP_SYMBOL(lzprobe::lz_ws_dbg), &dbg, sizeof(dbg));
+        printf("dbg=%2d (gathers %s)\n  ", dbg, dbg & 8 ? "off" : "on");
+        run<15, 2536, 2>(n, drp, dcol, dval, W, Q, Wn, bi, be, qrow, part, err, rec);
+        printf("  ");
+        run<15, 2536, 3, true>(n, drp, dcol, dval, W, Q, Wn, bi, be, qrow, part, err, rec);
+    }
     int e; hipMemcpy(&e, err, 4, hipMemcpyDeviceToHost);
     printf("err=%d\n", e);
     return 0;
