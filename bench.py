@@ -90,6 +90,10 @@ def main():
     ap.add_argument("--cpu-iters", type=int, default=3)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--spmm-reps", type=int, default=20)
+    ap.add_argument("--exchange", choices=["halo", "allgather"], default="halo",
+                    help="multi-GPU Krylov-block exchange (N > 1, or with --dist at N = 1)")
+    ap.add_argument("--dist", action="store_true",
+                    help="run the distributed entry point even at N = 1 (rehearsal of the N > 1 path)")
     args = ap.parse_args()
 
     import torch
@@ -109,33 +113,52 @@ def main():
     b, n = args.b, args.n
     seed = 20261015
     t_gen = time.time()
+    dist_path = world > 1 or args.dist
     if world == 1:
         A = lz.gen_banded(n, args.nnz_per_row, args.halfwidth, seed)
     else:
         A = lz.gen_banded_local(n * world, rank * n, (rank + 1) * n, args.nnz_per_row, args.halfwidth, seed)
     B = lz.uniform_B(n, b, seed + rank)
     log(f"[rank {rank}] generated n={A.n} nnz={A.nnz} in {time.time() - t_gen:.1f}s")
-    Ad = lz.CsrDevice.from_host(A, n_cols=n * world)
-    Bd = torch.from_numpy(B).cuda()
     kw = dict(dtype=torch.float64, device="cuda")
     m_max = max(args.steps, args.warmup, 1)
     q = torch.zeros(m_max * b, **kw)
     alpha = torch.zeros(m_max, b, b, **kw)
     beta = torch.zeros(m_max + 1, b, b, **kw)
-    Q0, Q1, W = (torch.zeros(n, b, **kw) for _ in range(3))
-    lc = 84 if rank == 0 else -1
+    Bd = torch.from_numpy(B).cuda()
+    halo_rows = 0
 
-    if world == 1:
+    if not dist_path:
+        Ad = lz.CsrDevice.from_host(A)
+        Q0, Q1, W = (torch.zeros(n, b, **kw) for _ in range(3))
+
         def run(m):
             h.block_lanczos_blas(Ad, Bd, m, 84, q, alpha, beta, Q0, Q1, W, fused=not args.unfused)
     else:
         uid = [lz.comm_unique_id() if rank == 0 else None]
-        dist.broadcast_object_list(uid, src=0)
+        if world > 1:
+            dist.broadcast_object_list(uid, src=0)
         h.comm_init(world, rank, uid[0])
-        X_full = torch.zeros(n * world, b, **kw)
+        if args.exchange == "halo":
+            # rank g owns rows [g n, (g+1) n); only referenced off-rank rows move
+            bounds = np.arange(world + 1, dtype=np.int64) * n
+            ccol, rcnt, hrows = lz.halo_plan(A.col, bounds, rank)
+            h.halo_init(rank * n, n, rcnt, hrows)
+            halo_rows = int(hrows.size)
+            Ad = lz.CsrDevice.from_host(lz.CsrHost(A.n, A.row_ptr, ccol, A.val), n_cols=n + halo_rows)
+            Q0 = torch.zeros(n, b, **kw)
+            X0, X1 = (torch.zeros(n + halo_rows, b, **kw) for _ in range(2))
+            log(f"[rank {rank}] halo rows {halo_rows}")
 
-        def run(m):
-            h.block_lanczos_dist(Ad, n, n * world, Bd, m, 84, 0, q, alpha, beta, Q0, W, X_full)
+            def run(m):
+                h.block_lanczos_halo(Ad, Bd, m, 84, 0, q, alpha, beta, Q0, X0, X1)
+        else:
+            Ad = lz.CsrDevice.from_host(A, n_cols=n * world)
+            Q0, W = (torch.zeros(n, b, **kw) for _ in range(2))
+            X_full = torch.zeros(n * world, b, **kw)
+
+            def run(m):
+                h.block_lanczos_dist(Ad, n, n * world, Bd, m, 84, 0, q, alpha, beta, Q0, W, X_full)
 
     # ---- warmup
     if args.warmup > 0:
@@ -231,7 +254,9 @@ def main():
                                    f"n={n} per GPU, nnz~{args.nnz_per_row:g}/row, halfwidth {args.halfwidth}",
                        "n_per_gpu": n, "nnz_per_gpu": A.nnz, "b": b, "m_timed": K,
                        "path": "fused" if fused else "unfused",
-                       "parallelism": "single" if world == 1 else f"rows{world}+rccl_allgather"},
+                       "parallelism": ("single" if not dist_path else
+                                       f"rows{world}+rccl_{args.exchange}" + (f"({halo_rows} halo rows/rank)"
+                                                                              if args.exchange == "halo" else ""))},
             "roofline": roof,
             "cpu_baseline": cpu,
             "extra": {

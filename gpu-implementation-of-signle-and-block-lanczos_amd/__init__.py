@@ -77,6 +77,11 @@ HIP_SYMBOLS = [
                                _c_i64, _c_dbl, _c_i64, _c_vp, _c_vp, _c_vp]),
     ("lz_comm_unique_id", _c_int, [_c_vp]),
     ("lz_comm_init", _c_int, [_c_vp, _c_int, _c_int, _c_vp]),
+    ("lz_halo_init", _c_int, [_c_vp, _c_i64, _c_i64, _c_vp, _c_vp]),
+    ("lz_halo_sizes", _c_int, [_c_vp, _c_vp, _c_vp]),
+    ("lz_halo_exchange", _c_int, [_c_vp, _c_int, _c_int, _c_vp]),
+    ("lz_block_lanczos_halo", _c_int, [_c_vp, _c_i64, _c_i64, _c_vp, _c_vp, _c_vp, _c_int, _c_int, _c_int,
+                                       _c_i64, _c_int, _c_vp, _c_vp, _c_vp, _c_vp, _c_vp, _c_vp, _c_vp]),
     ("lz_comm_destroy", _c_int, [_c_vp]),
     ("lz_block_lanczos_dist", _c_int, [_c_vp, _c_i64, _c_i64, _c_i64, _c_i64, _c_vp, _c_vp, _c_vp,
                                        _c_int, _c_int, _c_int, _c_i64, _c_int, _c_vp, _c_vp, _c_vp,
@@ -104,6 +109,7 @@ HOST_SYMBOLS = [
     ("lzh_block_solution", _c_int, [_c_int, _c_int, _c_dbl, _c_vp, _c_vp, _c_vp, _c_vp]),
     ("lzh_partition_rows", _c_int, [_c_i64, _c_vp, _c_int, _c_vp]),
     ("lzh_remap_cols_padded", _c_int, [_c_i64, _c_vp, _c_int, _c_vp, _c_i64, _c_vp]),
+    ("lzh_halo_plan", _c_i64, [_c_i64, _c_vp, _c_int, _c_vp, _c_int, _c_vp, _c_vp, _c_vp]),
     ("lzh_csr_write", _c_int, [ctypes.c_char_p, _c_i64, _c_i64, _c_i64, _c_vp, _c_vp, _c_vp, _c_int]),
     ("lzh_csr_read_header", _c_int, [ctypes.c_char_p, _c_vp, _c_vp, _c_vp, _c_vp]),
     ("lzh_csr_read", _c_int, [ctypes.c_char_p, _c_vp, _c_vp, _c_vp]),
@@ -331,6 +337,21 @@ def remap_cols_padded(col: np.ndarray, bounds: np.ndarray, n_pad: int) -> np.nda
     return out
 
 
+def halo_plan(col: np.ndarray, bounds: np.ndarray, rank: int):
+    """lzh_halo_plan: (compact columns, recv_counts[parts], halo_rows[n_halo]) for part
+    `rank` of the row partition `bounds` (columns global on input)."""
+    col = np.ascontiguousarray(col, np.int32)
+    bounds = np.ascontiguousarray(bounds, np.int64)
+    parts = bounds.size - 1
+    out = np.empty_like(col)
+    counts = np.zeros(parts, np.int64)
+    rows = np.empty(max(col.size, 1), np.int32)
+    nh = host_lib().lzh_halo_plan(col.size, _p(col), parts, _p(bounds), rank, _p(out), _p(counts), _p(rows))
+    if nh < 0:
+        raise LanczosError(f"lzh_halo_plan failed ({nh})")
+    return out, counts, rows[:nh].copy()
+
+
 def csr_write(path: str, A: CsrHost) -> None:
     dt = 0 if A.val.dtype == np.float64 else 1
     if host_lib().lzh_csr_write(path.encode(), A.n, A.n, A.nnz, _p(A.row_ptr), _p(A.col), _p(A.val), dt):
@@ -536,6 +557,31 @@ class Handle:
                                             A_local.dtype, b, m, lc_local, lc_rank, _ptr(B_local), _ptr(q),
                                             _ptr(alpha), _ptr(beta), _ptr(Q0), None, _ptr(W), _ptr(X_full)),
                "lz_block_lanczos_dist")
+
+
+    def halo_init(self, row0: int, n_local: int, recv_counts: np.ndarray, halo_rows: np.ndarray):
+        rc = np.ascontiguousarray(recv_counts, np.int64)
+        hr = np.ascontiguousarray(halo_rows, np.int32)
+        _check(self.L.lz_halo_init(self.ptr, row0, n_local, _p(rc), _p(hr) if hr.size else None),
+               "lz_halo_init")
+
+    def halo_sizes(self):
+        nh, ns = _c_i64(), _c_i64()
+        _check(self.L.lz_halo_sizes(self.ptr, ctypes.byref(nh), ctypes.byref(ns)), "lz_halo_sizes")
+        return nh.value, ns.value
+
+    def halo_exchange(self, X):
+        _check(self.L.lz_halo_exchange(self.ptr, _dt(X), X.shape[1], _ptr(X)), "lz_halo_exchange")
+
+    def block_lanczos_halo(self, A_local: CsrDevice, B_local, m: int, lc_local: int, lc_rank: int,
+                           q, alpha, beta, Q0, X0, X1):
+        """Distributed block Lanczos over the halo plan (A_local.col in the compact numbering)."""
+        n_local, b = A_local.n, B_local.shape[1]
+        _check(self.L.lz_block_lanczos_halo(self.ptr, n_local, A_local.nnz, _ptr(A_local.row_ptr),
+                                            _ptr(A_local.col), _ptr(A_local.val), A_local.dtype, b, m,
+                                            lc_local, lc_rank, _ptr(B_local), _ptr(q), _ptr(alpha),
+                                            _ptr(beta), _ptr(Q0), _ptr(X0), _ptr(X1)),
+               "lz_block_lanczos_halo")
 
 
 def comm_unique_id() -> bytes:

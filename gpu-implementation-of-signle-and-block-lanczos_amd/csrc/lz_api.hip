@@ -4,7 +4,9 @@
 
 #include <cstdarg>
 #include <cstring>
+#include <algorithm>
 #include <utility>
+#include <vector>
 
 #include "lz_common.hpp"
 #include "lz_internal.hpp"
@@ -90,7 +92,7 @@ static int block_lanczos_unfused(lz_handle *h, int64_t n, const int64_t *rp, con
     LZ_TRY(sqrtm_pair<T>(h, b, nullptr, P, beta, binv, nullptr));
     LZ_TRY(tsmm<T>(h, n, b, T(0), T(1), B, binv, Q0, b));          // Q0 = B*beta_inv (:114)
     LZ_TRY(copy_row<T>(h, b, Q0, b, 0, lc, q));                     // (:118)
-    LZ_TRY(spmm_rm<T>(h, n, rp, col, val, b, Q0, b, W, b));          // W = A*Q0 (:121)
+    LZ_TRY(spmm_rm<T>(h, n, rp, col, val, b, Q0, b, n, W, b));          // W = A*Q0 (:121)
     LZ_TRY(gram_partials<T>(h, n, b, W, Q0, b, &P));                 // alpha[0] (:124)
     LZ_TRY(gram_finish<T>(h, b, P, 1, alpha));
     LZ_TRY(tsmm<T>(h, n, b, T(1), T(-1), Q0, alpha, W, b));          // W -= Q0*alpha (:128)
@@ -99,7 +101,7 @@ static int block_lanczos_unfused(lz_handle *h, int64_t n, const int64_t *rp, con
         LZ_TRY(gram_partials<T>(h, n, b, W, W, b, &P));              // (:137)
         LZ_TRY(sqrtm_pair<T>(h, b, nullptr, P, bj, binv, nullptr));  // (:142)
         LZ_TRY(tsmm<T>(h, n, b, T(0), T(1), W, binv, Q1, b));        // Q1 = W*beta_inv (:145)
-        LZ_TRY(spmm_rm<T>(h, n, rp, col, val, b, Q1, b, W, b));      // W = A*Q1 (:149)
+        LZ_TRY(spmm_rm<T>(h, n, rp, col, val, b, Q1, b, n, W, b));      // W = A*Q1 (:149)
         LZ_TRY(tsmm<T>(h, n, b, T(1), T(-1), Q0, bj, W, b));         // W -= Q0*beta (:152)
         LZ_TRY(gram_partials<T>(h, n, b, W, Q1, b, &P));             // alpha[j] (:155)
         LZ_TRY(gram_finish<T>(h, b, P, 1, aj));
@@ -144,7 +146,7 @@ static int fdtd_block(lz_handle *h, int64_t n, const int64_t *rp, const int32_t 
     const T dt = (T)(T_end / (double)steps);   // fdtd.hpp:41
     LZ_HIP_TRY(hipMemcpyAsync(U, U0, sizeof(T) * n * b, hipMemcpyDeviceToDevice, h->stream));
     for (int64_t s = 0; s < steps; ++s) {
-        LZ_TRY(spmm_rm<T>(h, n, rp, col, val, b, U, b, D, b));      // fdtd.hpp:48
+        LZ_TRY(spmm_rm<T>(h, n, rp, col, val, b, U, b, n, D, b));      // fdtd.hpp:48
         LZ_TRY(axpy<T>(h, n * b, dt, D, U));                         // fdtd.hpp:49
     }
     return copy_row<T>(h, b, U, b, 0, lc, out);                      // fdtd.hpp:52
@@ -194,6 +196,117 @@ static int block_lanczos_dist16(lz_handle *h, int64_t n_local, int64_t n_pad, co
             LZ_NCCL_TRY(ncclAllReduce(slab, slab, bb, ncclDouble, ncclSum, comm, h->stream));
             LZ_TRY(sqrtm_pair<double>(h, 16, nullptr, 1, beta + (j + 1) * bb, binv, nullptr, slab));
             LZ_NCCL_TRY(ncclAllGather(W, X, n_pad * 16, ncclDouble, comm, h->stream));
+        }
+    }
+    return LZ_OK;
+}
+
+// ---------------------------------------------------- halo exchange (8e)
+// Row-partitioned iteration that moves only the rows other ranks reference
+// ("halo exchange of only the referenced columns"): each rank's
+// Krylov blocks live in X buffers of n_local + n_halo rows -- its own rows,
+// then the halo rows in the order lzh_halo_plan numbered them (ascending
+// global row, so each peer's rows are one contiguous run).  Per step the owner
+// packs the requested rows (k_halo_pack16) and one grouped ncclSend/ncclRecv
+// round moves them straight into the receivers' halo runs.  For a banded
+// operator that is 2 * halfwidth rows per rank instead of the all-gather's
+// (nranks - 1) * n_local, and the gather source stays < 2 GiB / 2^24 rows, so
+// the buffer-addressed fused pass applies at every rank count.
+struct HaloPlan {
+    int64_t n_local = 0, n_halo = 0, n_send = 0;
+    std::vector<int64_t> soff, roff;  // nranks + 1 row offsets per peer
+    int32_t *send_idx = nullptr;      // device: local rows to pack, grouped by peer
+    double *sendbuf = nullptr;        // device: n_send x 16
+};
+
+static void halo_free(lz_handle *h)
+{
+    if (!h->halo) return;
+    HaloPlan *hp = static_cast<HaloPlan *>(h->halo);
+    (void)hipFree(hp->send_idx);
+    (void)hipFree(hp->sendbuf);
+    delete hp;
+    h->halo = nullptr;
+}
+
+__global__ void k_halo_pack16(int64_t ns, const int32_t *__restrict__ idx, const double *__restrict__ X,
+                              double *__restrict__ out)
+{
+    // one 16-B piece per thread, 8 pieces per 128-B row
+    for (int64_t t = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; t < ns * 8;
+         t += (int64_t)gridDim.x * blockDim.x) {
+        const int64_t r = t >> 3;
+        const int p = (int)(t & 7);
+        reinterpret_cast<double2 *>(out)[t] =
+            reinterpret_cast<const double2 *>(X + (int64_t)idx[r] * 16)[p];
+    }
+}
+
+// fill rows [n_local, n_local + n_halo) of X from their owners
+static int halo_exchange16(lz_handle *h, const HaloPlan &hp, double *X)
+{
+    if (h->nranks == 1 || !h->comm) return LZ_OK;
+    if (hp.n_send > 0) {
+        const int grid = (int)std::min<int64_t>(ceil_div(hp.n_send * 8, 256), (int64_t)h->n_cu * 4);
+        hipLaunchKernelGGL(k_halo_pack16, dim3(grid), dim3(256), 0, h->stream, hp.n_send, hp.send_idx, X,
+                           hp.sendbuf);
+        LZ_LAUNCH_CHECK();
+    }
+    ncclComm_t comm = comm_of(h);
+    LZ_NCCL_TRY(ncclGroupStart());
+    ncclResult_t r = ncclSuccess;
+    for (int p = 0; p < h->nranks && r == ncclSuccess; ++p) {
+        if (p == h->rank) continue;
+        const int64_t sc = hp.soff[p + 1] - hp.soff[p], rc = hp.roff[p + 1] - hp.roff[p];
+        if (sc) r = ncclSend(hp.sendbuf + hp.soff[p] * 16, (size_t)sc * 16, ncclDouble, p, comm, h->stream);
+        if (rc && r == ncclSuccess)
+            r = ncclRecv(X + (hp.n_local + hp.roff[p]) * 16, (size_t)rc * 16, ncclDouble, p, comm, h->stream);
+    }
+    const ncclResult_t e = ncclGroupEnd();
+    LZ_NCCL_TRY(r);
+    LZ_NCCL_TRY(e);
+    return LZ_OK;
+}
+
+static int allreduce_bb(lz_handle *h, double *slab)
+{
+    if (h->nranks == 1 || !h->comm) return LZ_OK;
+    LZ_NCCL_TRY(ncclAllReduce(slab, slab, 256, ncclDouble, ncclSum, comm_of(h), h->stream));
+    return LZ_OK;
+}
+
+// b = 16 fp64.  Same step as block_lanczos_dist16 with the all-gather replaced
+// by the halo exchange; the residual alternates between X0 and X1 (the fused
+// pass gathers from one while writing the other), Q_j stays in Q0.
+static int block_lanczos_halo16(lz_handle *h, const HaloPlan &hp, const int64_t *rp, const int32_t *col,
+                                const double *val, int m, int64_t lc_local, const double *B, double *q,
+                                double *alpha, double *beta, double *Q0, double *X0, double *X1)
+{
+    constexpr int64_t bb = 256;
+    const int64_t n = hp.n_local, nx = hp.n_local + hp.n_halo;
+    double *binv = beta + m * bb;
+    double *slab = h->scratch;
+    int P = 0;
+    LZ_TRY(gram_partials<double>(h, n, 16, B, B, 16, &P));
+    LZ_TRY(gram_finish<double>(h, 16, P, 0, slab));
+    LZ_TRY(allreduce_bb(h, slab));
+    LZ_TRY(sqrtm_pair<double>(h, 16, nullptr, 1, beta, binv, nullptr, slab));
+    LZ_HIP_TRY(hipMemcpyAsync(X0, B, sizeof(double) * n * 16, hipMemcpyDeviceToDevice, h->stream));
+    LZ_TRY(halo_exchange16(h, hp, X0));
+    double *xs[2] = {X0, X1};
+    for (int j = 0; j < m; ++j) {
+        double *in = xs[j & 1], *out = xs[(j + 1) & 1];
+        LZ_TRY(fused_spmm16(h, n, rp, col, val, in, nx, in, Q0, out, binv, j ? beta + j * bb : nullptr,
+                            lc_local, q + j * 16, &P));
+        LZ_TRY(gram_finish<double>(h, 16, P, 0, slab, h->partials2));
+        LZ_TRY(allreduce_bb(h, slab));
+        LZ_TRY(gram_finish<double>(h, 16, 1, 1, alpha + j * bb, slab));
+        LZ_TRY(fused_update16(h, n, out, Q0, alpha + j * bb, &P));
+        if (j + 1 < m) {
+            LZ_TRY(gram_finish<double>(h, 16, P, 0, slab));
+            LZ_TRY(allreduce_bb(h, slab));
+            LZ_TRY(sqrtm_pair<double>(h, 16, nullptr, 1, beta + (j + 1) * bb, binv, nullptr, slab));
+            LZ_TRY(halo_exchange16(h, hp, out));
         }
     }
     return LZ_OK;
@@ -259,6 +372,7 @@ int lz_finalize(lz_handle *h)
 {
     if (!h) return LZ_OK;
     (void)hipSetDevice(h->device);
+    halo_free(h);
     if (h->comm) ncclCommDestroy(comm_of(h));
     if (h->ev_pool) {
         for (int i = 0; i < h->ev_cap; ++i) (void)hipEventDestroy(h->ev_pool[i]);
@@ -331,9 +445,9 @@ int lz_csr_spmm(lz_handle *h, int64_t n_rows, int64_t n_cols, int64_t nnz, const
         LZ_ARG_CHECK(ldx >= b && ldy >= b, "row-major ld >= b");
         if (dtype == LZ_F64)
             return spmm_rm<double>(h, n_rows, rp, col, (const double *)val, b, (const double *)X,
-                                   ldx, (double *)Y, ldy);
+                                   ldx, n_cols, (double *)Y, ldy);
         return spmm_rm<float>(h, n_rows, rp, col, (const float *)val, b, (const float *)X, ldx,
-                              (float *)Y, ldy);
+                              n_cols, (float *)Y, ldy);
     }
     LZ_ARG_CHECK(ldx >= n_cols && ldy >= n_rows, "column-major ld >= rows");
     if (dtype == LZ_F64)
@@ -521,6 +635,7 @@ int lz_comm_init(lz_handle *h, int nranks, int rank, const unsigned char id[128]
 int lz_comm_destroy(lz_handle *h)
 {
     LZ_HANDLE_CHECK(h);
+    halo_free(h);
     if (h->comm) ncclCommDestroy(comm_of(h));
     h->comm = nullptr;
     h->nranks = 1;
@@ -545,6 +660,157 @@ int lz_block_lanczos_dist(lz_handle *h, int64_t n_local, int64_t n_pad, int64_t 
     return block_lanczos_dist16(h, n_local, n_pad, rp, col, (const double *)val, m, lc,
                                 (const double *)B_local, (double *)q, (double *)alpha,
                                 (double *)beta, (double *)Q0, (double *)W, (double *)X_full);
+}
+
+static int halo_init_impl(lz_handle *h, int64_t row0, int64_t n_local, const int64_t *recv_counts,
+                          const int32_t *halo_rows)
+{
+    LZ_ARG_CHECK(n_local >= 0 && row0 >= 0 && recv_counts, "halo args");
+    const int nr = h->nranks;
+    LZ_ARG_CHECK(nr == 1 || h->comm != nullptr, "lz_comm_init first");
+    LZ_ARG_CHECK(recv_counts[h->rank] == 0, "recv_counts[rank] must be 0 (own rows are not halo)");
+    halo_free(h);
+    HaloPlan *hp = new HaloPlan();
+    h->halo = hp;
+    hp->n_local = n_local;
+    hp->roff.assign(nr + 1, 0);
+    hp->soff.assign(nr + 1, 0);
+    for (int p = 0; p < nr; ++p) {
+        LZ_ARG_CHECK(recv_counts[p] >= 0, "negative recv count");
+        hp->roff[p + 1] = hp->roff[p] + recv_counts[p];
+    }
+    hp->n_halo = hp->roff[nr];
+    LZ_ARG_CHECK(hp->n_halo == 0 || halo_rows, "halo_rows is NULL");
+    LZ_ARG_CHECK(n_local + hp->n_halo < (1LL << 31), "n_local + n_halo must fit int32 columns");
+    if (nr == 1) return LZ_OK;
+    ncclComm_t comm = comm_of(h);
+    // 1. counts: rank p tells rank q how many of q's rows it needs
+    int64_t *dcnt = nullptr;
+    LZ_HIP_TRY(hipMalloc(&dcnt, sizeof(int64_t) * 2 * nr));
+    std::vector<int64_t> scnt(nr, 0);
+    int rc = LZ_OK;
+    do {
+        if (hipMemcpy(dcnt, recv_counts, sizeof(int64_t) * nr, hipMemcpyHostToDevice) != hipSuccess ||
+            hipMemset(dcnt + nr, 0, sizeof(int64_t) * nr) != hipSuccess) {
+            set_error("lz_halo_init: staging counts failed");
+            rc = LZ_E_HIP;
+            break;
+        }
+        ncclResult_t r = ncclGroupStart();
+        for (int p = 0; p < nr && r == ncclSuccess; ++p) {
+            if (p == h->rank) continue;
+            r = ncclSend(dcnt + p, 1, ncclInt64, p, comm, h->stream);
+            if (r == ncclSuccess) r = ncclRecv(dcnt + nr + p, 1, ncclInt64, p, comm, h->stream);
+        }
+        const ncclResult_t e = ncclGroupEnd();
+        if (r != ncclSuccess || e != ncclSuccess) {
+            set_error("lz_halo_init: count exchange: %s", ncclGetErrorString(r != ncclSuccess ? r : e));
+            rc = LZ_E_COMM;
+            break;
+        }
+        if (hipStreamSynchronize(h->stream) != hipSuccess ||
+            hipMemcpy(scnt.data(), dcnt + nr, sizeof(int64_t) * nr, hipMemcpyDeviceToHost) != hipSuccess) {
+            set_error("lz_halo_init: reading counts failed");
+            rc = LZ_E_HIP;
+        }
+    } while (0);
+    (void)hipFree(dcnt);
+    if (rc != LZ_OK) return rc;
+    for (int p = 0; p < nr; ++p) {
+        LZ_ARG_CHECK(scnt[p] >= 0 && scnt[p] <= n_local, "peer requested more rows than this rank owns");
+        hp->soff[p + 1] = hp->soff[p] + scnt[p];
+    }
+    hp->n_send = hp->soff[nr];
+    // 2. the request lists (global rows) travel to their owners
+    int32_t *dreq = nullptr;
+    LZ_HIP_TRY(hipMalloc(&dreq, sizeof(int32_t) * std::max<int64_t>(1, hp->n_halo)));
+    LZ_HIP_TRY(hipMalloc(&hp->send_idx, sizeof(int32_t) * std::max<int64_t>(1, hp->n_send)));
+    LZ_HIP_TRY(hipMalloc(&hp->sendbuf, sizeof(double) * 16 * std::max<int64_t>(1, hp->n_send)));
+    std::vector<int32_t> sidx(hp->n_send);
+    do {
+        if (hp->n_halo &&
+            hipMemcpy(dreq, halo_rows, sizeof(int32_t) * hp->n_halo, hipMemcpyHostToDevice) != hipSuccess) {
+            set_error("lz_halo_init: staging requests failed");
+            rc = LZ_E_HIP;
+            break;
+        }
+        ncclResult_t r = ncclGroupStart();
+        for (int p = 0; p < nr && r == ncclSuccess; ++p) {
+            if (p == h->rank) continue;
+            const int64_t sc = hp->soff[p + 1] - hp->soff[p], rcv = hp->roff[p + 1] - hp->roff[p];
+            if (rcv) r = ncclSend(dreq + hp->roff[p], (size_t)rcv, ncclInt32, p, comm, h->stream);
+            if (sc && r == ncclSuccess)
+                r = ncclRecv(hp->send_idx + hp->soff[p], (size_t)sc, ncclInt32, p, comm, h->stream);
+        }
+        const ncclResult_t e = ncclGroupEnd();
+        if (r != ncclSuccess || e != ncclSuccess) {
+            set_error("lz_halo_init: request exchange: %s", ncclGetErrorString(r != ncclSuccess ? r : e));
+            rc = LZ_E_COMM;
+            break;
+        }
+        if (hipStreamSynchronize(h->stream) != hipSuccess ||
+            (hp->n_send && hipMemcpy(sidx.data(), hp->send_idx, sizeof(int32_t) * hp->n_send,
+                                     hipMemcpyDeviceToHost) != hipSuccess)) {
+            set_error("lz_halo_init: reading requests failed");
+            rc = LZ_E_HIP;
+        }
+    } while (0);
+    (void)hipFree(dreq);
+    if (rc != LZ_OK) return rc;
+    // 3. global -> local row; every requested row must be ours
+    for (int64_t i = 0; i < hp->n_send; ++i) {
+        const int64_t g = (int64_t)sidx[i] - row0;
+        LZ_ARG_CHECK(g >= 0 && g < n_local, "a peer requested a row this rank does not own");
+        sidx[i] = (int32_t)g;
+    }
+    if (hp->n_send)
+        LZ_HIP_TRY(hipMemcpy(hp->send_idx, sidx.data(), sizeof(int32_t) * hp->n_send, hipMemcpyHostToDevice));
+    return LZ_OK;
+}
+
+int lz_halo_init(lz_handle *h, int64_t row0, int64_t n_local, const int64_t *recv_counts,
+                 const int32_t *halo_rows)
+{
+    LZ_HANDLE_CHECK(h);
+    const int rc = halo_init_impl(h, row0, n_local, recv_counts, halo_rows);
+    if (rc != LZ_OK) halo_free(h);  // never leave a half-built plan behind
+    return rc;
+}
+
+int lz_halo_sizes(lz_handle *h, int64_t *n_halo, int64_t *n_send)
+{
+    LZ_ARG_CHECK(h && h->halo, "lz_halo_init first");
+    const HaloPlan *hp = static_cast<const HaloPlan *>(h->halo);
+    if (n_halo) *n_halo = hp->n_halo;
+    if (n_send) *n_send = hp->n_send;
+    return LZ_OK;
+}
+
+int lz_halo_exchange(lz_handle *h, lz_dtype dtype, int b, void *X)
+{
+    LZ_HANDLE_CHECK(h);
+    LZ_ARG_CHECK(h->halo, "lz_halo_init first");
+    LZ_ARG_CHECK(dtype == LZ_F64 && b == 16 && X, "halo exchange: b = 16 fp64");
+    return halo_exchange16(h, *static_cast<const HaloPlan *>(h->halo), (double *)X);
+}
+
+int lz_block_lanczos_halo(lz_handle *h, int64_t n_local, int64_t nnz_local, const int64_t *rp,
+                          const int32_t *col, const void *val, lz_dtype dtype, int b, int m,
+                          int64_t lc_local, int lc_rank, const void *B_local, void *q, void *alpha,
+                          void *beta, void *Q0, void *X0, void *X1)
+{
+    LZ_HANDLE_CHECK(h);
+    LZ_ARG_CHECK(h->halo, "lz_halo_init first");
+    const HaloPlan &hp = *static_cast<const HaloPlan *>(h->halo);
+    LZ_TRY(check_csr(n_local, nnz_local, rp, col, val));
+    LZ_ARG_CHECK(n_local == hp.n_local, "n_local differs from lz_halo_init");
+    LZ_ARG_CHECK(dtype == LZ_F64 && b == 16, "halo path: b = 16 fp64");
+    LZ_ARG_CHECK(m >= 1 && n_local >= 1, "sizes");
+    LZ_ARG_CHECK(B_local && q && alpha && beta && Q0 && X0 && X1 && X0 != X1, "NULL / aliased buffer");
+    const int64_t lc = (lc_rank == h->rank) ? lc_local : -1;
+    return block_lanczos_halo16(h, hp, rp, col, (const double *)val, m, lc, (const double *)B_local,
+                                (double *)q, (double *)alpha, (double *)beta, (double *)Q0, (double *)X0,
+                                (double *)X1);
 }
 
 }  // extern "C"

@@ -69,6 +69,7 @@ struct lz_handle {
     int *err_flag = nullptr;      // device: nonzero if a persistent kernel gave up a bounded spin
     void *comm = nullptr;         // ncclComm_t when lz_comm_init was called
     int nranks = 1, rank = 0;
+    void *halo = nullptr;         // lz::HaloPlan when lz_halo_init was called
     // optional per-kernel-class timing with hipEvents on the handle's stream
     // (lz_prof_enable / lz_prof_read): events recorded around each launch of
     // the class, elapsed times summed at read time.

@@ -597,6 +597,40 @@ int lzh_remap_cols_padded(int64_t nnz, const int32_t *col, int parts, const int6
     return 0;
 }
 
+// Halo plan (SURVEY.md 8e "halo exchange of only the referenced columns"):
+// the distinct off-rank columns of the local CSR, sorted ascending (so grouped
+// by owner in rank order), and the columns rewritten into the compact
+// numbering [0, n_local) = own rows, n_local + i = i-th halo row.
+int64_t lzh_halo_plan(int64_t nnz, const int32_t *col, int parts, const int64_t *bounds, int rank,
+                      int32_t *col_out, int64_t *recv_counts, int32_t *halo_rows)
+{
+    if (nnz < 0 || !col || !col_out || !bounds || !recv_counts || !halo_rows || parts < 1 ||
+        rank < 0 || rank >= parts)
+        return -1;
+    const int64_t r0 = bounds[rank], r1 = bounds[rank + 1], nl = r1 - r0;
+    std::vector<int32_t> off;
+    off.reserve(1024);
+    for (int64_t k = 0; k < nnz; ++k)
+        if (col[k] < r0 || col[k] >= r1) off.push_back(col[k]);
+    std::sort(off.begin(), off.end());
+    off.erase(std::unique(off.begin(), off.end()), off.end());
+    const int64_t nh = (int64_t)off.size();
+    if ((double)nl + (double)nh > 2147483647.0) return -2;
+    if (nh && (off.front() < 0 || off.back() >= bounds[parts])) return -3;
+    std::copy(off.begin(), off.end(), halo_rows);
+    for (int p = 0; p < parts; ++p)
+        recv_counts[p] = std::lower_bound(off.begin(), off.end(), (int32_t)bounds[p + 1]) -
+                         std::lower_bound(off.begin(), off.end(), (int32_t)bounds[p]);
+#pragma omp parallel for schedule(static)
+    for (int64_t k = 0; k < nnz; ++k) {
+        const int32_t j = col[k];
+        col_out[k] = (j >= r0 && j < r1)
+                         ? (int32_t)(j - r0)
+                         : (int32_t)(nl + (std::lower_bound(off.begin(), off.end(), j) - off.begin()));
+    }
+    return nh;
+}
+
 static const char kMagic[8] = {'L', 'Z', 'C', 'S', 'R', '0', '0', '1'};
 
 int lzh_csr_write(const char *path, int64_t n, int64_t nc, int64_t nnz, const int64_t *rp,

@@ -7,7 +7,7 @@ namespace lz {
 // ---- sparse (lz_spmm.hip)
 template <typename T>
 int spmm_rm(lz_handle *h, int64_t n, const int64_t *rp, const int32_t *col, const T *val, int b,
-            const T *X, int64_t ldx, T *Y, int64_t ldy);
+            const T *X, int64_t ldx, int64_t nx, T *Y, int64_t ldy);  // nx: rows of X
 template <typename T>
 int spmm_cm(lz_handle *h, int64_t n, const int64_t *rp, const int32_t *col, const T *val, int b,
             const T *X, int64_t ldx, T *Y, int64_t ldy);

@@ -40,7 +40,7 @@ template <typename T, int B, int CAP, int RPG>
 __global__ __launch_bounds__(256) void k_spmm_lds(int64_t n, const int64_t *__restrict__ rp,
                                                   const int32_t *__restrict__ col,
                                                   const T *__restrict__ val,
-                                                  const T *__restrict__ X, int64_t ldx,
+                                                  const T *__restrict__ X, int64_t ldx, int64_t /*nx*/,
                                                   T *__restrict__ Y, int64_t ldy)
 {
     using S = SpmmShape<T, B>;
@@ -145,7 +145,7 @@ template <typename T, int B, int CAP, int RPG, int UNR = 8, int MINW = 1>
 __global__ __launch_bounds__(256, MINW) void k_spmm_buf(int64_t n, const int64_t *__restrict__ rp,
                                                   const int32_t *__restrict__ col,
                                                   const T *__restrict__ val,
-                                                  const T *__restrict__ X, int64_t ldx,
+                                                  const T *__restrict__ X, int64_t ldx, int64_t nx,
                                                   T *__restrict__ Y, int64_t ldy)
 {
     using S = SpmmShape<T, B>;
@@ -164,7 +164,7 @@ __global__ __launch_bounds__(256, MINW) void k_spmm_buf(int64_t n, const int64_t
     const int64_t nnz = rp[n];
     // the tile's row pointers: one load per thread, shared through LDS
     for (int t = tid; t <= TR; t += 256) rps[t] = rp[(r0 + t < rend) ? r0 + t : rend];
-    const __amdgpu_buffer_rsrc_t xr = lz_rsrc(X, (uint32_t)(n * ldx * (int64_t)sizeof(T)));
+    const __amdgpu_buffer_rsrc_t xr = lz_rsrc(X, (uint32_t)(nx * ldx * (int64_t)sizeof(T)));
     const uint32_t rowb = (uint32_t)(ldx * sizeof(T)), lane_off = p * VEC * sizeof(T);
     T acc[RPG][VEC];
 #pragma unroll
@@ -316,7 +316,7 @@ template <int WS_NC, int WS_K, int WS_D, int WS_CAP>
 __global__ __launch_bounds__(64 * (WS_NC + 1)) void k_spmm_ws(int64_t n, const int64_t *__restrict__ rp,
                                                            const int32_t *__restrict__ col,
                                                            const double *__restrict__ val,
-                                                           const double *__restrict__ X,
+                                                           const double *__restrict__ X, int64_t nx,
                                                            double *__restrict__ Y, int *__restrict__ err)
 {
     using C = WsCfg<WS_NC, WS_K, WS_D, WS_CAP>;
@@ -409,7 +409,7 @@ __global__ __launch_bounds__(64 * (WS_NC + 1)) void k_spmm_ws(int64_t n, const i
     // -------------------------------------------------------------- consumers
     const int cw = w - 1, g = lane >> 3, p = lane & 7;
     const __amdgpu_buffer_rsrc_t xr =
-        __builtin_amdgcn_make_buffer_rsrc(const_cast<double *>(X), (short)0, (int)(n * 128), 0x00020000);
+        __builtin_amdgcn_make_buffer_rsrc(const_cast<double *>(X), (short)0, (int)(nx * 128), 0x00020000);
     const uint32_t lane_off = 16u * p;
 #ifdef LZ_WS_PROBE
     long long c_ready = 0, c_gather = 0, c_steps = 0;
@@ -493,7 +493,7 @@ template <typename T, int B, int TR, int CAP>
 __global__ __launch_bounds__(256) void k_spmm_merge(int64_t n, const int64_t *__restrict__ rp,
                                                     const int32_t *__restrict__ col,
                                                     const T *__restrict__ val,
-                                                    const T *__restrict__ X, int64_t ldx,
+                                                    const T *__restrict__ X, int64_t ldx, int64_t nx,
                                                     T *__restrict__ Y, int64_t ldy)
 {
     using S = SpmmShape<T, B>;
@@ -511,7 +511,7 @@ __global__ __launch_bounds__(256) void k_spmm_merge(int64_t n, const int64_t *__
     const int64_t kA = rp[r0];
     if (tid <= nrows) rel[tid] = (int)(rp[r0 + tid] - kA);
     const int64_t N64 = rp[r0 + nrows] - kA;
-    const __amdgpu_buffer_rsrc_t xr = lz_rsrc(X, (uint32_t)(n * ldx * (int64_t)sizeof(T)));
+    const __amdgpu_buffer_rsrc_t xr = lz_rsrc(X, (uint32_t)(nx * ldx * (int64_t)sizeof(T)));
     const uint32_t rowb = (uint32_t)(ldx * sizeof(T)), lane_off = p * VEC * sizeof(T);
     auto store_row = [&](int r, const Vec<T, VEC> &o) { stv<T, VEC>(Y + (r0 + r) * ldy + p * VEC, o); };
     if (N64 > CAP) {  // block-uniform: long rows -- row-wise straight from global
@@ -683,7 +683,7 @@ __global__ __launch_bounds__(256) void k_spmv(int64_t n, const int64_t *__restri
 
 template <typename T, int B>
 static int launch_spmm_rm(lz_handle *h, int64_t n, const int64_t *rp, const int32_t *col,
-                          const T *val, const T *X, int64_t ldx, T *Y, int64_t ldy)
+                          const T *val, const T *X, int64_t ldx, int64_t nx, T *Y, int64_t ldy)
 {
     using S = SpmmShape<T, B>;
     constexpr int CAP = S::RB * 32 < 1024 ? 1024 : (S::RB * 32 > 4096 ? 4096 : S::RB * 32);
@@ -695,7 +695,8 @@ static int launch_spmm_rm(lz_handle *h, int64_t n, const int64_t *rp, const int3
     const int rpg = rpg_env ? atoi(rpg_env) : 2;
     const int64_t tiles = ceil_div(n, (int64_t)S::RB * rpg);
     LZ_ARG_CHECK(tiles < (1LL << 31), "too many row tiles");
-    const bool buf_ok = n * ldx * (int64_t)sizeof(T) < (1LL << 31) && n < (1 << 24);
+    // X has nx rows (the operator's columns), not n
+    const bool buf_ok = nx * ldx * (int64_t)sizeof(T) < (1LL << 31) && nx < (1 << 24);
     constexpr int CAP2 = CAP * 2 < 4096 ? CAP * 2 : 4096;
     const int ev = prof_begin(h, PROF_SPMM);
     if constexpr (B == 16 && std::is_same<T, double>::value) {
@@ -706,7 +707,7 @@ static int launch_spmm_rm(lz_handle *h, int64_t n, const int64_t *rp, const int3
             auto go = [&](auto kern, int tr, int bpc, int threads) {
                 const int grid = (int)std::max<int64_t>(1, std::min<int64_t>(ceil_div(n, (int64_t)tr),
                                                                              (int64_t)h->n_cu * bpc));
-                hipLaunchKernelGGL(kern, dim3(grid), dim3(threads), 0, h->stream, n, rp, col, val, X, Y,
+                hipLaunchKernelGGL(kern, dim3(grid), dim3(threads), 0, h->stream, n, rp, col, val, X, nx, Y,
                                    h->err_flag);
             };
             if (cfg == 1)
@@ -724,41 +725,41 @@ static int launch_spmm_rm(lz_handle *h, int64_t n, const int64_t *rp, const int3
         const int64_t mt = ceil_div(n, (int64_t)128);
         LZ_ARG_CHECK(mt < (1LL << 31), "too many row tiles");
         hipLaunchKernelGGL((k_spmm_merge<T, B, 128, 2048>), dim3((unsigned)mt), dim3(256), 0,
-                           h->stream, n, rp, col, val, X, ldx, Y, ldy);
+                           h->stream, n, rp, col, val, X, ldx, nx, Y, ldy);
     } else if (buf_ok && variant && variant[0] == 'x') {  // occupancy experiments: x<unr><waves/SIMD>
         const int unr = variant[1] - '0', occ = variant[2] - '0';
         if (unr == 4 && occ == 8)
             hipLaunchKernelGGL((k_spmm_buf<T, B, 1024, 2, 4, 8>), dim3((unsigned)tiles), dim3(256), 0,
-                               h->stream, n, rp, col, val, X, ldx, Y, ldy);
+                               h->stream, n, rp, col, val, X, ldx, nx, Y, ldy);
         else if (unr == 4 && occ == 6)
             hipLaunchKernelGGL((k_spmm_buf<T, B, 1024, 2, 4, 6>), dim3((unsigned)tiles), dim3(256), 0,
-                               h->stream, n, rp, col, val, X, ldx, Y, ldy);
+                               h->stream, n, rp, col, val, X, ldx, nx, Y, ldy);
         else if (unr == 8 && occ == 6)
             hipLaunchKernelGGL((k_spmm_buf<T, B, 1024, 2, 8, 6>), dim3((unsigned)tiles), dim3(256), 0,
-                               h->stream, n, rp, col, val, X, ldx, Y, ldy);
+                               h->stream, n, rp, col, val, X, ldx, nx, Y, ldy);
         else
             hipLaunchKernelGGL((k_spmm_buf<T, B, 1024, 2, 8, 8>), dim3((unsigned)tiles), dim3(256), 0,
-                               h->stream, n, rp, col, val, X, ldx, Y, ldy);
+                               h->stream, n, rp, col, val, X, ldx, nx, Y, ldy);
     } else if (buf_ok && !(variant && variant[0] == 't')) {
         if (rpg == 1)
             hipLaunchKernelGGL((k_spmm_buf<T, B, CAP, 1>), dim3((unsigned)tiles), dim3(256), 0,
-                               h->stream, n, rp, col, val, X, ldx, Y, ldy);
+                               h->stream, n, rp, col, val, X, ldx, nx, Y, ldy);
         else if (rpg == 2)
             hipLaunchKernelGGL((k_spmm_buf<T, B, 1024, 2>), dim3((unsigned)tiles), dim3(256), 0,
-                               h->stream, n, rp, col, val, X, ldx, Y, ldy);
+                               h->stream, n, rp, col, val, X, ldx, nx, Y, ldy);
         else
             hipLaunchKernelGGL((k_spmm_buf<T, B, 4096, 4>), dim3((unsigned)tiles), dim3(256), 0,
-                               h->stream, n, rp, col, val, X, ldx, Y, ldy);
+                               h->stream, n, rp, col, val, X, ldx, nx, Y, ldy);
     } else {
         if (rpg == 1)
             hipLaunchKernelGGL((k_spmm_lds<T, B, CAP, 1>), dim3((unsigned)tiles), dim3(256), 0,
-                               h->stream, n, rp, col, val, X, ldx, Y, ldy);
+                               h->stream, n, rp, col, val, X, ldx, nx, Y, ldy);
         else if (rpg == 2)
             hipLaunchKernelGGL((k_spmm_lds<T, B, CAP2, 2>), dim3((unsigned)tiles), dim3(256), 0,
-                               h->stream, n, rp, col, val, X, ldx, Y, ldy);
+                               h->stream, n, rp, col, val, X, ldx, nx, Y, ldy);
         else
             hipLaunchKernelGGL((k_spmm_lds<T, B, 4096, 4>), dim3((unsigned)tiles), dim3(256), 0,
-                               h->stream, n, rp, col, val, X, ldx, Y, ldy);
+                               h->stream, n, rp, col, val, X, ldx, nx, Y, ldy);
     }
     prof_end(h, ev);
     LZ_LAUNCH_CHECK();
@@ -767,16 +768,18 @@ static int launch_spmm_rm(lz_handle *h, int64_t n, const int64_t *rp, const int3
 
 template <typename T>
 int spmm_rm(lz_handle *h, int64_t n, const int64_t *rp, const int32_t *col, const T *val, int b,
-            const T *X, int64_t ldx, T *Y, int64_t ldy)
+            const T *X, int64_t ldx, int64_t nx, T *Y, int64_t ldy)
 {
     switch (b) {
-    case 1: return spmv<T>(h, n, rp, col, val, X, Y, 0);
-    case 2: return launch_spmm_rm<T, 2>(h, n, rp, col, val, X, ldx, Y, ldy);
-    case 4: return launch_spmm_rm<T, 4>(h, n, rp, col, val, X, ldx, Y, ldy);
-    case 8: return launch_spmm_rm<T, 8>(h, n, rp, col, val, X, ldx, Y, ldy);
-    case 16: return launch_spmm_rm<T, 16>(h, n, rp, col, val, X, ldx, Y, ldy);
-    case 32: return launch_spmm_rm<T, 32>(h, n, rp, col, val, X, ldx, Y, ldy);
-    case 64: return launch_spmm_rm<T, 64>(h, n, rp, col, val, X, ldx, Y, ldy);
+    case 1:
+        LZ_ARG_CHECK(ldx == 1 && ldy == 1, "b = 1 row-major needs ldx = ldy = 1");
+        return spmv<T>(h, n, rp, col, val, X, Y, 0);
+    case 2: return launch_spmm_rm<T, 2>(h, n, rp, col, val, X, ldx, nx, Y, ldy);
+    case 4: return launch_spmm_rm<T, 4>(h, n, rp, col, val, X, ldx, nx, Y, ldy);
+    case 8: return launch_spmm_rm<T, 8>(h, n, rp, col, val, X, ldx, nx, Y, ldy);
+    case 16: return launch_spmm_rm<T, 16>(h, n, rp, col, val, X, ldx, nx, Y, ldy);
+    case 32: return launch_spmm_rm<T, 32>(h, n, rp, col, val, X, ldx, nx, Y, ldy);
+    case 64: return launch_spmm_rm<T, 64>(h, n, rp, col, val, X, ldx, nx, Y, ldy);
     default:
         set_error("row-major SpMM supports b in {1,2,4,8,16,32,64}, got %d", b);
         return LZ_E_ARG;
@@ -824,9 +827,9 @@ int spmv(lz_handle *h, int64_t n, const int64_t *rp, const int32_t *col, const T
 }
 
 template int spmm_rm<double>(lz_handle *, int64_t, const int64_t *, const int32_t *,
-                             const double *, int, const double *, int64_t, double *, int64_t);
+                             const double *, int, const double *, int64_t, int64_t, double *, int64_t);
 template int spmm_rm<float>(lz_handle *, int64_t, const int64_t *, const int32_t *, const float *,
-                            int, const float *, int64_t, float *, int64_t);
+                            int, const float *, int64_t, int64_t, float *, int64_t);
 template int spmm_cm<double>(lz_handle *, int64_t, const int64_t *, const int32_t *,
                              const double *, int, const double *, int64_t, double *, int64_t);
 template int spmm_cm<float>(lz_handle *, int64_t, const int64_t *, const int32_t *, const float *,

@@ -176,6 +176,32 @@ int lz_block_lanczos_dist(lz_handle *h, int64_t n_local, int64_t n_pad, int64_t 
                           int lc_rank, const void *B_local, void *q, void *alpha, void *beta,
                           void *Q0, void *Q1, void *W, void *X_full);
 
+/* Halo-exchange variant: only the rows of other ranks that the
+ * local CSR references move each step (grouped ncclSend/ncclRecv), instead of
+ * the all-gather of every rank's slab.  Collective setup, every rank:
+ *   lzh_halo_plan (liblz_host) on the local CSR with GLOBAL columns gives the
+ *   compact columns, recv_counts[nranks] and halo_rows[n_halo] (host arrays);
+ *   lz_halo_init(h, row0, n_local, recv_counts, halo_rows) exchanges the
+ *   request lists over RCCL and keeps the send lists on the device.
+ * A rank's Krylov blocks then live in X buffers of n_local + n_halo rows:
+ * rows [0, n_local) its own, the rest the halo in plan order.  With one rank
+ * (or no communicator) n_halo = 0 and no collective is issued. */
+int lz_halo_init(lz_handle *h, int64_t row0, int64_t n_local, const int64_t *recv_counts,
+                 const int32_t *halo_rows);
+int lz_halo_sizes(lz_handle *h, int64_t *n_halo, int64_t *n_send);
+/* fill rows [n_local, n_local + n_halo) of X (b = 16 fp64, row-major) from
+ * their owners; rows [0, n_local) must hold this rank's block */
+int lz_halo_exchange(lz_handle *h, lz_dtype dtype, int b, void *X);
+/* Distributed block Lanczos over the halo plan; replaces the single-GPU
+ * block_lanczos_blas (methods/block_lanczos.hpp:88-167) on a row partition.
+ * col: compact numbering from lzh_halo_plan.  B_local, Q0: n_local x 16; X0,
+ * X1: (n_local + n_halo) x 16 workspaces (the residual alternates between them).
+ * alpha/beta identical on every rank; q written on lc_rank only. */
+int lz_block_lanczos_halo(lz_handle *h, int64_t n_local, int64_t nnz_local, const int64_t *row_ptr,
+                          const int32_t *col, const void *val, lz_dtype dtype, int b, int m,
+                          int64_t lc_local, int lc_rank, const void *B_local, void *q, void *alpha,
+                          void *beta, void *Q0, void *X0, void *X1);
+
 #ifdef __cplusplus
 }
 #endif

@@ -91,6 +91,14 @@ int lzh_partition_rows(int64_t n, const int64_t *row_ptr, int parts, int64_t *bo
  * p*n_pad + (j - bounds[p]) -- the row of X_full the all-gather puts it in. */
 int lzh_remap_cols_padded(int64_t nnz, const int32_t *col, int parts, const int64_t *bounds,
                           int64_t n_pad, int32_t *col_out);
+/* Halo plan of part `rank` for lz_block_lanczos_halo: halo_rows[0..n_halo) =
+ * the distinct global columns outside [bounds[rank], bounds[rank+1]) that the
+ * local CSR references, ascending (hence grouped by owner part in part order);
+ * recv_counts[p] = how many of them part p owns; col_out = the columns in the
+ * compact numbering (own row j -> j - bounds[rank], halo_rows[i] -> n_local+i).
+ * halo_rows needs room for nnz entries.  Returns n_halo, < 0 on error. */
+int64_t lzh_halo_plan(int64_t nnz, const int32_t *col, int parts, const int64_t *bounds, int rank,
+                      int32_t *col_out, int64_t *recv_counts, int32_t *halo_rows);
 
 /* ---------------------------------------------------------- CSR files */
 /* binary CSR: "LZCSR001", int64 n_rows, n_cols, nnz, int32 dtype (0 f64, 1 f32),
