@@ -60,6 +60,15 @@ def fused_kernel():
     return "k_fused_ws16<15,2536,3,true>", "k_fused_ws16"
 
 
+def spmm_kernel():
+    """The plain SpMM kernel lz_csr_spmm launches for b = 16 fp64 (LZ_SPMM_KERNEL A/B)."""
+    v = os.environ.get("LZ_SPMM_KERNEL", "")
+    if not v or v[0] == "s":
+        tr = {"3": 32, "6": 64, "9": 96}.get(v[1:2], 48)
+        return f"k_spmm_seg<double,16,{tr},{tr * 16},8,nt>"
+    return "k_spmm_buf<double,16,1024,2>" if v[0] == "b" else f"LZ_SPMM_KERNEL={v}"
+
+
 def pmc_traffic(kernel, n, nnz, hw):
     """HBM bytes per launch of `kernel` from the committed rocprofv3 PMC summary
     (profiles/*_pmc_<kernel>.json, written by scripts/pmc_traffic.py from separate
@@ -202,7 +211,7 @@ def main():
         h.prof_enable(False)
         t_avg = ms / cnt * 1e-3
         gbs = spmm_bytes(n, A.nnz, b) / t_avg / 1e9
-        plain = {"kernel": "k_spmm_buf<double,16,1024,2>", "avg_ms": round(ms / cnt, 4),
+        plain = {"kernel": spmm_kernel(), "avg_ms": round(ms / cnt, 4),
                  "bytes_per_launch": spmm_bytes(n, A.nnz, b), "achieved_GBs": round(gbs, 1),
                  "frac_of_hbm_peak": round(gbs / HBM_PEAK_GBS, 4)}
 

@@ -124,12 +124,12 @@ __device__ __forceinline__ __amdgpu_buffer_rsrc_t lz_rsrc(const void *p, uint32_
     return __builtin_amdgcn_make_buffer_rsrc(const_cast<void *>(p), (short)0, (int)bytes, 0x00020000);
 }
 
-template <typename T, int VEC>
+template <typename T, int VEC, int AUX = 0>
 __device__ __forceinline__ Vec<T, VEC> ldbuf(__amdgpu_buffer_rsrc_t r, uint32_t off)
 {
     Vec<T, VEC> v;
     if constexpr (sizeof(T) * VEC == 16) {
-        const auto u = __builtin_amdgcn_raw_buffer_load_b128(r, off, 0, 0);
+        const auto u = __builtin_amdgcn_raw_buffer_load_b128(r, off, 0, AUX);
         __builtin_memcpy(&v, &u, 16);
     } else if constexpr (sizeof(T) * VEC == 8) {
         const auto u = __builtin_amdgcn_raw_buffer_load_b64(r, off, 0, 0);
@@ -141,7 +141,7 @@ __device__ __forceinline__ Vec<T, VEC> ldbuf(__amdgpu_buffer_rsrc_t r, uint32_t 
     return v;
 }
 
-template <typename T, int B, int CAP, int RPG, int UNR = 8, int MINW = 1>
+template <typename T, int B, int CAP, int RPG, int UNR = 8, int MINW = 1, int PF = 0>
 __global__ __launch_bounds__(256, MINW) void k_spmm_buf(int64_t n, const int64_t *__restrict__ rp,
                                                   const int32_t *__restrict__ col,
                                                   const T *__restrict__ val,
@@ -172,6 +172,7 @@ __global__ __launch_bounds__(256, MINW) void k_spmm_buf(int64_t n, const int64_t
 #pragma unroll
         for (int i = 0; i < VEC; ++i) acc[j][i] = T(0);
     int64_t k0[RPG], k1[RPG];
+    uint32_t pfx = 0;
     for (int64_t c0 = kA; c0 < kB; c0 += CAP) {  // block-uniform
         const int64_t c1 = (c0 + CAP < kB) ? c0 + CAP : kB;
         if (c0 != kA) __syncthreads();
@@ -238,6 +239,18 @@ __global__ __launch_bounds__(256, MINW) void k_spmm_buf(int64_t n, const int64_t
                 k1[j] = rps[r + 1 < TR ? r + 1 : TR];
             }
         }
+        // PF > 0: touch every X row of the chunk once (one dword, one lane per
+        // nonzero) before the gather steps, so the rows' first-touch L2 misses
+        // overlap in one round instead of stalling successive 8-load steps
+        uint32_t pfv[PF > 0 ? PF : 1];
+        if constexpr (PF > 0) {
+#pragma unroll
+            for (int q = 0; q < PF; ++q) {
+                const int k = tid + 256 * q;
+                const uint32_t off = (k < (int)(c1 - c0)) ? __umul24((unsigned)cs[k], rowb) : 0x80000000u;
+                pfv[q] = __builtin_amdgcn_raw_buffer_load_b32(xr, off, 0, 0);
+            }
+        }
 #pragma unroll
         for (int j = 0; j < RPG; ++j) {
             const int a = (int)((k0[j] > c0 ? k0[j] : c0) - c0), e = (int)((k1[j] < c1 ? k1[j] : c1) - c0);
@@ -264,6 +277,10 @@ __global__ __launch_bounds__(256, MINW) void k_spmm_buf(int64_t n, const int64_t
                     for (int i = 0; i < VEC; ++i) acc[j][i] = fma(vv[t], xs[t].v[i], acc[j][i]);
             }
         }
+        if constexpr (PF > 0) {
+#pragma unroll
+            for (int q = 0; q < PF; ++q) pfx ^= pfv[q];
+        }
     }
 #pragma unroll
     for (int j = 0; j < RPG; ++j) {
@@ -274,6 +291,9 @@ __global__ __launch_bounds__(256, MINW) void k_spmm_buf(int64_t n, const int64_t
             for (int i = 0; i < VEC; ++i) o.v[i] = acc[j][i];
             stv<T, VEC>(Y + row * ldy + p * VEC, o);
         }
+    }
+    if constexpr (PF > 0) {  // keeps the touches alive; ldy < 0 never happens
+        if (ldy < 0 && pfx == 0x9e3779b9u) Y[0] = T(0);
     }
 }
 
@@ -489,6 +509,205 @@ __global__ __launch_bounds__(64 * (WS_NC + 1)) void k_spmm_ws(int64_t n, const i
 // finished after a barrier by summing the slots of the groups that cover
 // them, in group order -- deterministic for a given tile size.  Tiles whose
 // run exceeds CAP are processed row-wise from global memory.
+// nnz-split SpMM with row results through LDS.  Every gather wave-instruction
+// costs the texture path the same ~16 cycles whatever its live lanes (the TA
+// is ~97 % busy in k_spmm_buf, PMC r01), so the lever is live lanes per
+// instruction: each group of LPR lanes walks an equal, 8-aligned slice of the
+// tile's nonzero run regardless of row boundaries (all 8 loads of a step live
+// except in a group's last step).  A row that ends inside a group's slice is
+// written to an LDS Y tile (ds_write, no texture-path cost -- the first
+// nnz-split kernel stored it to global from inside the divergent loop, one
+// partial-exec store instruction per row end, which ate the gain); a group's
+// first and last rows go to head/tail slots and are summed in a fixed order,
+// so results stay bitwise reproducible; the Y tile leaves with full-lane
+// coalesced stores.
+template <typename T, int B, int TR, int CAP, int UNR = 8, bool NT = false, int GAUX = 0>
+__global__ __launch_bounds__(256) void k_spmm_seg(int64_t n, const int64_t *__restrict__ rp,
+                                                  const int32_t *__restrict__ col,
+                                                  const T *__restrict__ val,
+                                                  const T *__restrict__ X, int64_t ldx, int64_t nx,
+                                                  T *__restrict__ Y, int64_t ldy)
+{
+    using S = SpmmShape<T, B>;
+    constexpr int VEC = S::VEC, LPR = S::LPR, G = 256 / LPR;
+    static_assert(TR <= 255, "row ids are bytes");
+    __shared__ int32_t rel[TR + 1];
+    __shared__ int32_t cs[CAP + UNR];
+    __shared__ T vs[CAP + UNR];
+    __shared__ uint8_t rid[CAP + UNR];
+    __shared__ Vec<T, VEC> yt[TR][LPR];      // the tile's finished rows
+    __shared__ Vec<T, VEC> head[G][LPR];     // a group's piece of a row begun in an earlier slice
+    const int tid = threadIdx.x;
+    const int gi = tid / LPR, p = tid % LPR;
+    const int64_t r0 = xcd_remap(blockIdx.x, gridDim.x) * TR;
+    const int nrows = (int)((n - r0) < TR ? (n - r0) : TR);
+    const int64_t kA = rp[r0];
+    if (tid <= nrows) rel[tid] = (int)(rp[r0 + tid] - kA);
+    const int64_t N64 = rp[r0 + nrows] - kA;
+    const __amdgpu_buffer_rsrc_t xr = lz_rsrc(X, (uint32_t)(nx * ldx * (int64_t)sizeof(T)));
+    const uint32_t rowb = (uint32_t)(ldx * sizeof(T)), lane_off = p * VEC * sizeof(T);
+    Vec<T, VEC> zero;
+#pragma unroll
+    for (int i = 0; i < VEC; ++i) zero.v[i] = T(0);
+    if (N64 > CAP) {  // block-uniform: long rows -- row-wise straight from global
+        for (int r = gi; r < nrows; r += G) {
+            const int64_t a = rp[r0 + r], e = rp[r0 + r + 1];
+            Vec<T, VEC> acc = zero;
+            for (int64_t k = a; k < e; k += UNR) {
+                Vec<T, VEC> xs[UNR];
+                T vv[UNR];
+#pragma unroll
+                for (int t = 0; t < UNR; ++t) {
+                    const bool ok = k + t < e;
+                    vv[t] = ok ? val[k + t] : T(0);
+                    const uint32_t off = ok ? __umul24((unsigned)col[k + t], rowb) + lane_off : 0x80000000u;
+                    xs[t] = ldbuf<T, VEC>(xr, off);
+                }
+#pragma unroll
+                for (int t = 0; t < UNR; ++t)
+#pragma unroll
+                    for (int i = 0; i < VEC; ++i) acc.v[i] = fma(vv[t], xs[t].v[i], acc.v[i]);
+            }
+            stv<T, VEC>(Y + (r0 + r) * ldy + p * VEC, acc);
+        }
+        return;
+    }
+    const int N = (int)N64;
+    {  // stage the run with 16-B loads (aligned down; a piece reaching past nnz,
+       // last tile only, element-wise), then the row id of every entry
+        constexpr int EPV = 16 / (int)sizeof(T);
+        constexpr int SPTC = ((CAP + 4) / 4 + 255) / 256, SPTV = ((CAP + EPV) / EPV + 255) / 256;
+        const int64_t nnz = rp[n], kB = kA + N;
+        const int64_t bc = kA & ~(int64_t)3, bv = kA & ~(int64_t)(EPV - 1);
+        const __amdgpu_buffer_rsrc_t cr = lz_rsrc(col + bc, 0x7fffffffu);
+        const __amdgpu_buffer_rsrc_t vr = lz_rsrc(val + bv, 0x7fffffffu);
+        constexpr int AUX = NT ? 2 : 0;  // nt: streamed once, keep the X window in L2
+        int4 ct[SPTC];
+        int4 vt[SPTV];
+#pragma unroll
+        for (int q = 0; q < SPTC; ++q) {
+            const int64_t k = bc + 4 * (int64_t)(tid + 256 * q);
+            ct[q] = int4{0, 0, 0, 0};
+            if (k + 4 <= nnz && k < kB)
+                ct[q] = __builtin_bit_cast(int4, __builtin_amdgcn_raw_buffer_load_b128(cr, (uint32_t)((k - bc) * 4), 0, AUX));
+            else if (k < kB) {
+                ct[q].x = col[k];
+                if (k + 1 < nnz) ct[q].y = col[k + 1];
+                if (k + 2 < nnz) ct[q].z = col[k + 2];
+            }
+        }
+#pragma unroll
+        for (int q = 0; q < SPTV; ++q) {
+            const int64_t k = bv + EPV * (int64_t)(tid + 256 * q);
+            vt[q] = int4{0, 0, 0, 0};
+            if (k + EPV <= nnz && k < kB) {
+                vt[q] = __builtin_bit_cast(int4, __builtin_amdgcn_raw_buffer_load_b128(vr, (uint32_t)((k - bv) * sizeof(T)), 0, AUX));
+            } else if (k < kB) {
+                T tv[EPV] = {};
+                for (int e = 0; e < EPV && k + e < nnz; ++e) tv[e] = val[k + e];
+                __builtin_memcpy(&vt[q], tv, 16);
+            }
+        }
+        __syncthreads();  // rel
+        if (tid < nrows)
+            for (int k = rel[tid]; k < rel[tid + 1]; ++k) rid[k] = (uint8_t)tid;
+#pragma unroll
+        for (int q = 0; q < SPTC; ++q) {
+            const int64_t k = bc + 4 * (int64_t)(tid + 256 * q);
+            const int32_t cv[4] = {ct[q].x, ct[q].y, ct[q].z, ct[q].w};
+#pragma unroll
+            for (int e = 0; e < 4; ++e)
+                if (k + e >= kA && k + e < kB) cs[k + e - kA] = cv[e];
+        }
+#pragma unroll
+        for (int q = 0; q < SPTV; ++q) {
+            const int64_t k = bv + EPV * (int64_t)(tid + 256 * q);
+            T tv[EPV];
+            __builtin_memcpy(tv, &vt[q], 16);
+#pragma unroll
+            for (int e = 0; e < EPV; ++e)
+                if (k + e >= kA && k + e < kB) vs[k + e - kA] = tv[e];
+        }
+        if (tid < UNR) {
+            cs[N + tid] = 0;
+            vs[N + tid] = T(0);
+            rid[N + tid] = 255;
+        }
+        __syncthreads();
+    }
+    const int E = ((N + G - 1) / G + UNR - 1) / UNR * UNR;  // slice length, UNR-aligned
+    const int start = gi * E, end = (start + E < N) ? start + E : N;
+    if (start < end) {  // group-uniform
+        int cur = rid[start];
+        bool open = rel[cur] < start;  // cur began in an earlier group's slice
+        Vec<T, VEC> acc = zero;
+        for (int s0 = start; s0 < end; s0 += UNR) {
+            int32_t cc[UNR];
+            T vv[UNR];
+            int rr[UNR];
+#pragma unroll
+            for (int t = 0; t < UNR; ++t) {
+                cc[t] = cs[s0 + t];
+                vv[t] = vs[s0 + t];
+                rr[t] = rid[s0 + t];
+            }
+            Vec<T, VEC> xs[UNR];
+#pragma unroll
+            for (int t = 0; t < UNR; ++t) {
+                const uint32_t off =
+                    s0 + t < end ? __umul24((unsigned)cc[t], rowb) + lane_off : 0x80000000u;
+                xs[t] = ldbuf<T, VEC, GAUX>(xr, off);
+            }
+#pragma unroll
+            for (int t = 0; t < UNR; ++t) {
+                const int r = s0 + t < end ? rr[t] : cur;
+                if (r != cur) {  // row cur ends inside the slice
+                    if (open) head[gi][p] = acc;
+                    else yt[cur][p] = acc;  // a whole row
+                    acc = zero;
+                    cur = r;
+                    open = false;
+                }
+#pragma unroll
+                for (int i = 0; i < VEC; ++i) acc.v[i] = fma(vv[t], xs[t].v[i], acc.v[i]);
+            }
+        }
+        // the slice's last row: whole, or the first piece of a row later slices continue
+        if (open) head[gi][p] = acc;
+        else yt[cur][p] = acc;
+    }
+    __syncthreads();
+    // rows over several slices: first piece (in yt) + the later groups' heads,
+    // in group order; empty rows
+    for (int r = gi; r < nrows; r += G) {
+        const int a = rel[r], e = rel[r + 1];
+        if (a == e) {
+            yt[r][p] = zero;
+            continue;
+        }
+        const int g1 = a / E, g2 = (e - 1) / E;
+        if (g1 == g2) continue;
+        Vec<T, VEC> sum = yt[r][p];
+        for (int g = g1 + 1; g <= g2; ++g) {
+#pragma unroll
+            for (int i = 0; i < VEC; ++i) sum.v[i] += head[g][p].v[i];
+        }
+        yt[r][p] = sum;
+    }
+    __syncthreads();
+    for (int idx = tid; idx < nrows * LPR; idx += 256) {
+        T *dst = Y + (r0 + idx / LPR) * ldy + (idx % LPR) * VEC;
+        if constexpr (NT && sizeof(T) * VEC == 16) {
+            typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
+            u32x4 u;
+            __builtin_memcpy(&u, &yt[idx / LPR][idx % LPR], 16);
+            __builtin_nontemporal_store(u, reinterpret_cast<u32x4 *>(dst));
+        } else {
+            stv<T, VEC>(dst, yt[idx / LPR][idx % LPR]);
+        }
+    }
+}
+
 template <typename T, int B, int TR, int CAP>
 __global__ __launch_bounds__(256) void k_spmm_merge(int64_t n, const int64_t *__restrict__ rp,
                                                     const int32_t *__restrict__ col,
@@ -721,7 +940,31 @@ static int launch_spmm_rm(lz_handle *h, int64_t n, const int64_t *rp, const int3
             return LZ_OK;
         }
     }
-    if (buf_ok && variant && variant[0] == 'm') {
+    // default for 128-B rows (b = 16 fp64, b = 32 fp32): the nnz-split kernel
+    // (48-row tiles, nt CSR stream); LZ_SPMM_KERNEL=b forces k_spmm_buf, s3/s6/s9
+    // other tile heights (A/B)
+    const bool seg = buf_ok && S::LPR == 8 && !(variant && variant[0] != 's');
+    if (seg) {
+        const char c = variant ? variant[1] : '4';
+        const int tr = c == '9' ? 96 : c == '6' ? 64 : c == '3' ? 32 : 48;
+        const int64_t st = ceil_div(n, (int64_t)tr);
+        LZ_ARG_CHECK(st < (1LL << 31), "too many row tiles");
+        auto go = [&](auto kern) {
+            hipLaunchKernelGGL(kern, dim3((unsigned)st), dim3(256), 0, h->stream, n, rp, col, val, X, ldx, nx, Y,
+                               ldy);
+        };
+        if (tr == 96)
+            go(k_spmm_seg<T, B, 96, 1536, 8, true>);
+        else if (tr == 64)
+            go(k_spmm_seg<T, B, 64, 1024, 8, true>);
+        else if (tr == 32)
+            go(k_spmm_seg<T, B, 32, 512, 8, true>);
+        else
+            go(k_spmm_seg<T, B, 48, 768, 8, true>);
+    } else if (buf_ok && variant && variant[0] == 'p') {  // first-touch prefetch round (A/B)
+        hipLaunchKernelGGL((k_spmm_buf<T, B, 1024, 2, 8, 1, 4>), dim3((unsigned)tiles), dim3(256), 0,
+                           h->stream, n, rp, col, val, X, ldx, nx, Y, ldy);
+    } else if (buf_ok && variant && variant[0] == 'm') {
         const int64_t mt = ceil_div(n, (int64_t)128);
         LZ_ARG_CHECK(mt < (1LL << 31), "too many row tiles");
         hipLaunchKernelGGL((k_spmm_merge<T, B, 128, 2048>), dim3((unsigned)mt), dim3(256), 0,
@@ -740,7 +983,7 @@ static int launch_spmm_rm(lz_handle *h, int64_t n, const int64_t *rp, const int3
         else
             hipLaunchKernelGGL((k_spmm_buf<T, B, 1024, 2, 8, 8>), dim3((unsigned)tiles), dim3(256), 0,
                                h->stream, n, rp, col, val, X, ldx, nx, Y, ldy);
-    } else if (buf_ok && !(variant && variant[0] == 't')) {
+    } else if (buf_ok && !(variant && variant[0] == 't')) {  // k_spmm_buf
         if (rpg == 1)
             hipLaunchKernelGGL((k_spmm_buf<T, B, CAP, 1>), dim3((unsigned)tiles), dim3(256), 0,
                                h->stream, n, rp, col, val, X, ldx, nx, Y, ldy);
