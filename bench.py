@@ -47,6 +47,8 @@ def fused_kernel():
     """(full name, PMC short name) of the pass-1 kernel lz_fused.hip launches for
     b = 16 fp64 (LZ_FUSED_KERNEL selects the alternatives kept for A/B runs)."""
     v = os.environ.get("LZ_FUSED_KERNEL", "")
+    if v.startswith("s"):
+        return "k_fused_seg16", "k_fused_seg16"
     if v.startswith("t"):
         return "k_fused_spmm16<true>", "k_fused_spmm16"
     if v.startswith("p"):

@@ -334,6 +334,7 @@ static int fold_slabs(lz_handle *h, const double *part, int64_t P, int bb, int *
     return LZ_OK;
 }
 
+template <bool REV>
 __global__ __launch_bounds__(512) void k_fused_update16(int64_t n, double *__restrict__ Wn,
                                                         const double *__restrict__ Q,
                                                         const double *__restrict__ alpha,
@@ -349,17 +350,36 @@ __global__ __launch_bounds__(512) void k_fused_update16(int64_t n, double *__res
     d4_t gacc = {0.0, 0.0, 0.0, 0.0};
     const int64_t ntile = ceil_div(n, 16);
     XcdSched s(ceil_div(ntile, 8));
-    for (int64_t u = s.begin; u < s.end; u += s.step) {
-        const int64_t r0 = (u * 8 + w) * 16;
-        if (r0 >= n) continue;
-        d4_t acc;
+    // REV: walk this block's units last-first.  Pass 1 writes Q_j and W' first
+    // row to last, so the rows it wrote last are still in the MALL (256 MB)
+    // when a reversed pass 2 starts; pass 2's last-written W'' rows (the first
+    // rows) are in turn the first the next pass 1 gathers.
+    const int64_t cnt = s.begin < s.end ? (s.end - s.begin + s.step - 1) / s.step : 0;
+    auto row0 = [&](int64_t k) { return (s.begin + (REV ? cnt - 1 - k : k) * s.step) * 128 + 16 * w; };
+    // one tile ahead in registers: the W' (accumulator layout) and Q rows of
+    // tile k+1 are in flight while tile k is computed (vmcnt is in order, so
+    // tile k's wait does not cover them)
+    auto fetch = [&](int64_t k, d4_t &a, double qv[4]) {
+        const int64_t r0 = row0(k);
 #pragma unroll
         for (int r = 0; r < 4; ++r) {
             const int64_t row = r0 + (lane >> 4) + 4 * r;
-            acc[r] = row < n ? Wn[r0 * 16 + 64 * r + lane] : 0.0;
+            a[r] = (k < cnt && row < n) ? Wn[r0 * 16 + 64 * r + lane] : 0.0;
         }
+        if (k < cnt) tile_load(Q, r0, n, lane, qv);
+        else qv[0] = qv[1] = qv[2] = qv[3] = 0.0;
+    };
+    d4_t acc_n;
+    double qv_n[4];
+    fetch(0, acc_n, qv_n);
+    for (int64_t k = 0; k < cnt; ++k) {
+        const int64_t r0 = row0(k);
+        d4_t acc = acc_n;
+        double qv[4] = {qv_n[0], qv_n[1], qv_n[2], qv_n[3]};
+        fetch(k + 1, acc_n, qv_n);
+        if (r0 >= n) continue;
         double qa[4];
-        tile_to_aop(T, Q, r0, n, lane, qa);
+        tile_regs_to_aop(T, qv, lane, qa);
 #pragma unroll
         for (int kc = 0; kc < 4; ++kc) acc = mfma16(qa[kc], na_op[kc], acc);
 #pragma unroll
@@ -1282,6 +1302,274 @@ __global__ __launch_bounds__(512, 4) void k_fused_pf16(
     for (int r = 0; r < 4; ++r) slab[((lane_ >> 4) + 4 * r) * 16 + (lane_ & 15)] = macc[r];
 }
 
+// ---------------------------------------------------------------------------
+// nnz-split fused pass 1: the k_spmm_seg structure (lz_spmm.hip) with the
+// fused epilogue.  PMC (r01): the texture path is busy ~97 % of a gather
+// kernel and every load or store wave-instruction costs it about the same
+// whatever its live lanes, so this pass is built to issue as few as possible:
+//   * 48-row tiles; each of the 32 lane groups gathers an equal 8-aligned slice
+//     of the tile's nonzero run (rows split across slices are summed in fixed
+//     order from LDS head slots), so gather instructions run ~94 % lanes live;
+//   * the CSR run arrives by 16-B nt loads, issued together with the tile's
+//     W and Q_{j-1} strips (one HBM round trip for all three);
+//   * A*W rows land in an LDS tile; waves 0-2 each run one 16-row strip's MFMA
+//     epilogue (Q_j = W beta^-1, W' = Y beta^-1 - Q_{j-1} beta) and write Q_j
+//     and W' back with 16-B stores through their LDS scratch;
+//   * persistent blocks over XCD-contiguous tile ranges (XcdSched) keep the
+//     Q_j^T W' accumulator in registers; one slab per block.
+constexpr int kSegTR = 48, kSegCap = 768;
+
+__device__ __forceinline__ __amdgpu_buffer_rsrc_t seg_rsrc(const void *p, uint32_t bytes)
+{
+    return __builtin_amdgcn_make_buffer_rsrc(const_cast<void *>(p), (short)0, (int)bytes, 0x00020000);
+}
+
+__global__ __launch_bounds__(256, 4) void k_fused_seg16(
+    int64_t n, const int64_t *__restrict__ rp, const int32_t *__restrict__ col,
+    const double *__restrict__ val, const double *__restrict__ Wg, int64_t nx,
+    const double *__restrict__ Wown, double *__restrict__ Qbuf,
+    double *__restrict__ Wn, const double *__restrict__ binv, const double *__restrict__ beta,
+    int64_t lc, double *__restrict__ qrow, double *__restrict__ part)
+{
+    constexpr int TR = kSegTR, CAP = kSegCap, G = 32, UNR = 8, YS = 17;
+    constexpr int SPTC = ((CAP + 4) / 4 + 255) / 256, SPTV = ((CAP + 2) / 2 + 255) / 256;
+    __shared__ int32_t rel[TR + 1];
+    __shared__ double sbuf[(CAP + UNR) * 3 / 2 + 2];  // vs | cs during the gather; scratch after
+    __shared__ uint8_t rid[CAP + UNR];
+    __shared__ double yt[TR * YS];                    // the tile's A*W rows (stride 17)
+    __shared__ double2 head[G][8];
+    __shared__ double bsh[2][256];                    // beta^-1, -beta (epilogue operands)
+    double *vs = sbuf;
+    int32_t *cs = reinterpret_cast<int32_t *>(sbuf + CAP + UNR);
+    const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+    const int gi = tid >> 3, p = tid & 7;
+    const bool has_prev = beta != nullptr;
+    bsh[0][tid] = binv[tid];
+    bsh[1][tid] = has_prev ? -beta[tid] : 0.0;
+    const __amdgpu_buffer_rsrc_t xr = seg_rsrc(Wg, (uint32_t)(nx * 128));
+    const uint32_t lane_off = 16u * (uint32_t)p;
+    const int64_t nnz = rp[n];
+    d4_t macc = {0.0, 0.0, 0.0, 0.0};
+    const int64_t ntile = ceil_div(n, (int64_t)TR);
+    XcdSched s(ntile);
+    for (int64_t u = s.begin; u < s.end; u += s.step) {
+        const int64_t r0 = u * TR;
+        const int nrows = (int)((n - r0) < TR ? (n - r0) : TR);
+        const int64_t kA = rp[r0];
+        __syncthreads();  // the previous tile's epilogue is done with sbuf / yt
+        if (tid <= nrows) rel[tid] = (int)(rp[r0 + tid] - kA);
+        const int64_t kB = rp[r0 + nrows];
+        const int N = (int)(kB - kA);
+        // this wave's epilogue strip (waves 0-2): W and Q_{j-1} rows, issued with the CSR run
+        const int64_t rs = r0 + 16 * w;
+        double wv[4] = {0.0, 0.0, 0.0, 0.0}, qv[4] = {0.0, 0.0, 0.0, 0.0};
+        if (w < 3 && 16 * w < nrows) {
+            tile_load(Wown, rs, n, lane, wv);
+            if (has_prev) tile_load(Qbuf, rs, n, lane, qv);
+        }
+        if (N <= CAP) {  // block-uniform
+            const int64_t bc = kA & ~(int64_t)3, bv = kA & ~(int64_t)1;
+            const __amdgpu_buffer_rsrc_t cr = seg_rsrc(col + bc, 0x7fffffffu);
+            const __amdgpu_buffer_rsrc_t vr = seg_rsrc(val + bv, 0x7fffffffu);
+            int4 ct[SPTC], vt[SPTV];
+#pragma unroll
+            for (int q = 0; q < SPTC; ++q) {
+                const int64_t k = bc + 4 * (int64_t)(tid + 256 * q);
+                ct[q] = int4{0, 0, 0, 0};
+                if (k + 4 <= nnz && k < kB)
+                    ct[q] = __builtin_bit_cast(int4, __builtin_amdgcn_raw_buffer_load_b128(cr, (uint32_t)((k - bc) * 4), 0, 2));
+                else if (k < kB) {
+                    ct[q].x = col[k];
+                    if (k + 1 < nnz) ct[q].y = col[k + 1];
+                    if (k + 2 < nnz) ct[q].z = col[k + 2];
+                }
+            }
+#pragma unroll
+            for (int q = 0; q < SPTV; ++q) {
+                const int64_t k = bv + 2 * (int64_t)(tid + 256 * q);
+                vt[q] = int4{0, 0, 0, 0};
+                if (k + 2 <= nnz && k < kB)
+                    vt[q] = __builtin_bit_cast(int4, __builtin_amdgcn_raw_buffer_load_b128(vr, (uint32_t)((k - bv) * 8), 0, 2));
+                else if (k < kB) {
+                    const double t0 = val[k];
+                    __builtin_memcpy(&vt[q], &t0, 8);
+                }
+            }
+            __syncthreads();  // rel
+            if (tid < nrows)
+                for (int k = rel[tid]; k < rel[tid + 1]; ++k) rid[k] = (uint8_t)tid;
+#pragma unroll
+            for (int q = 0; q < SPTC; ++q) {
+                const int64_t k = bc + 4 * (int64_t)(tid + 256 * q);
+                const int32_t cv[4] = {ct[q].x, ct[q].y, ct[q].z, ct[q].w};
+#pragma unroll
+                for (int e = 0; e < 4; ++e)
+                    if (k + e >= kA && k + e < kB) cs[k + e - kA] = cv[e];
+            }
+#pragma unroll
+            for (int q = 0; q < SPTV; ++q) {
+                const int64_t k = bv + 2 * (int64_t)(tid + 256 * q);
+                double tv[2];
+                __builtin_memcpy(tv, &vt[q], 16);
+#pragma unroll
+                for (int e = 0; e < 2; ++e)
+                    if (k + e >= kA && k + e < kB) vs[k + e - kA] = tv[e];
+            }
+            if (tid < UNR) {
+                cs[N + tid] = 0;
+                vs[N + tid] = 0.0;
+                rid[N + tid] = 255;
+            }
+            __syncthreads();
+            const int E = ((N + G - 1) / G + UNR - 1) / UNR * UNR;
+            const int start = gi * E, end = (start + E < N) ? start + E : N;
+            if (start < end) {  // group-uniform
+                int cur = rid[start];
+                bool open = rel[cur] < start;
+                double a0 = 0.0, a1 = 0.0;
+                for (int s0 = start; s0 < end; s0 += UNR) {
+                    int32_t cc[UNR];
+                    double vv[UNR];
+                    int rr[UNR];
+#pragma unroll
+                    for (int t = 0; t < UNR; ++t) {
+                        cc[t] = cs[s0 + t];
+                        vv[t] = vs[s0 + t];
+                        rr[t] = rid[s0 + t];
+                    }
+                    double2 xs[UNR];
+#pragma unroll
+                    for (int t = 0; t < UNR; ++t) {
+                        const uint32_t off = s0 + t < end ? __umul24((unsigned)cc[t], 128u) + lane_off : 0x80000000u;
+                        const auto u4 = __builtin_amdgcn_raw_buffer_load_b128(xr, off, 0, 0);
+                        __builtin_memcpy(&xs[t], &u4, 16);
+                    }
+#pragma unroll
+                    for (int t = 0; t < UNR; ++t) {
+                        const int r = s0 + t < end ? rr[t] : cur;
+                        if (r != cur) {  // row cur ends inside the slice
+                            if (open) head[gi][p] = double2{a0, a1};
+                            else {
+                                yt[cur * YS + 2 * p] = a0;
+                                yt[cur * YS + 2 * p + 1] = a1;
+                            }
+                            a0 = a1 = 0.0;
+                            cur = r;
+                            open = false;
+                        }
+                        a0 = fma(vv[t], xs[t].x, a0);
+                        a1 = fma(vv[t], xs[t].y, a1);
+                    }
+                }
+                if (open) head[gi][p] = double2{a0, a1};
+                else {
+                    yt[cur * YS + 2 * p] = a0;
+                    yt[cur * YS + 2 * p + 1] = a1;
+                }
+            }
+            __syncthreads();
+            for (int r = gi; r < nrows; r += G) {  // rows over several slices; empty rows
+                const int a = rel[r], e = rel[r + 1];
+                if (a == e) {
+                    yt[r * YS + 2 * p] = 0.0;
+                    yt[r * YS + 2 * p + 1] = 0.0;
+                    continue;
+                }
+                const int g1 = a / E, g2 = (e - 1) / E;
+                if (g1 == g2) continue;
+                double s0 = yt[r * YS + 2 * p], s1 = yt[r * YS + 2 * p + 1];
+                for (int g = g1 + 1; g <= g2; ++g) {
+                    s0 += head[g][p].x;
+                    s1 += head[g][p].y;
+                }
+                yt[r * YS + 2 * p] = s0;
+                yt[r * YS + 2 * p + 1] = s1;
+            }
+        } else {  // a run longer than the stage: rows straight from global
+            for (int r = gi; r < nrows; r += G) {
+                const int64_t a = rp[r0 + r], e = rp[r0 + r + 1];
+                double a0 = 0.0, a1 = 0.0;
+                for (int64_t k = a; k < e; k += UNR) {
+                    double2 xs[UNR];
+                    double vv[UNR];
+#pragma unroll
+                    for (int t = 0; t < UNR; ++t) {
+                        const bool ok = k + t < e;
+                        vv[t] = ok ? val[k + t] : 0.0;
+                        const uint32_t off = ok ? __umul24((unsigned)col[k + t], 128u) + lane_off : 0x80000000u;
+                        const auto u4 = __builtin_amdgcn_raw_buffer_load_b128(xr, off, 0, 0);
+                        __builtin_memcpy(&xs[t], &u4, 16);
+                    }
+#pragma unroll
+                    for (int t = 0; t < UNR; ++t) {
+                        a0 = fma(vv[t], xs[t].x, a0);
+                        a1 = fma(vv[t], xs[t].y, a1);
+                    }
+                }
+                yt[r * YS + 2 * p] = a0;
+                yt[r * YS + 2 * p + 1] = a1;
+            }
+        }
+        __syncthreads();  // yt complete; sbuf free for the epilogue scratch
+        if (w < 3 && 16 * w < nrows) {  // wave-uniform
+            double *T = sbuf + w * (16 * 17);
+            const bool live = 16 * w + (lane & 15) < nrows;  // this lane's A-operand row
+            double ya[4], wa[4], qa[4] = {0.0, 0.0, 0.0, 0.0};
+#pragma unroll
+            for (int kc = 0; kc < 4; ++kc)
+                ya[kc] = live ? yt[(16 * w + (lane & 15)) * YS + 4 * kc + (lane >> 4)] : 0.0;
+            tile_regs_to_aop(T, wv, lane, wa);
+            if (has_prev) tile_regs_to_aop(T, qv, lane, qa);
+            double bi_op[4];
+#pragma unroll
+            for (int kc = 0; kc < 4; ++kc) bi_op[kc] = bsh[0][(4 * kc + (lane >> 4)) * 16 + (lane & 15)];
+            d4_t q1 = {0.0, 0.0, 0.0, 0.0}, wn = {0.0, 0.0, 0.0, 0.0};
+#pragma unroll
+            for (int kc = 0; kc < 4; ++kc) q1 = mfma16(wa[kc], bi_op[kc], q1);
+#pragma unroll
+            for (int kc = 0; kc < 4; ++kc) wn = mfma16(ya[kc], bi_op[kc], wn);
+            if (has_prev) {
+#pragma unroll
+                for (int kc = 0; kc < 4; ++kc)
+                    wn = mfma16(qa[kc], bsh[1][(4 * kc + (lane >> 4)) * 16 + (lane & 15)], wn);
+            }
+            // Q_j and W' leave as 16-B row pieces through the scratch
+            const int row = lane >> 3, c2 = 2 * (lane & 7);
+#pragma unroll
+            for (int m = 0; m < 2; ++m) {
+                const d4_t &v = m ? wn : q1;
+                double *dst = m ? Wn : Qbuf;
+#pragma unroll
+                for (int r = 0; r < 4; ++r) T[((lane >> 4) + 4 * r) * 17 + (lane & 15)] = v[r];
+                wave_lds_sync();
+#pragma unroll
+                for (int hh = 0; hh < 2; ++hh) {
+                    const int rr = row + 8 * hh;
+                    const int64_t grow = rs + rr;
+                    const double x0 = T[rr * 17 + c2], x1 = T[rr * 17 + c2 + 1];
+                    if (16 * w + rr < nrows) {
+                        *reinterpret_cast<double2 *>(dst + grow * 16 + c2) = double2{x0, x1};
+                        if (m == 0 && grow == lc) {
+                            qrow[c2] = x0;
+                            qrow[c2 + 1] = x1;
+                        }
+                    }
+                }
+                wave_lds_sync();
+            }
+            // rows past n have zero operands, so they add nothing here
+#pragma unroll
+            for (int r = 0; r < 4; ++r) macc = mfma16(q1[r], wn[r], macc);
+        }
+    }
+    // one slab per block: the waves' accumulators summed in wave order
+    __syncthreads();
+#pragma unroll
+    for (int r = 0; r < 4; ++r) sbuf[w * 256 + ((lane >> 4) + 4 * r) * 16 + (lane & 15)] = macc[r];
+    __syncthreads();
+    part[(int64_t)blockIdx.x * 256 + tid] = ((sbuf[tid] + sbuf[256 + tid]) + sbuf[512 + tid]) + sbuf[768 + tid];
+}
+
 int fused_spmm16(lz_handle *h, int64_t n, const int64_t *rp, const int32_t *col, const double *val,
                  const double *Wg, int64_t nx, const double *Wown, double *Qbuf, double *Wn, const double *binv,
                  const double *beta, int64_t lc, double *qrow, int *nparts)
@@ -1290,6 +1578,22 @@ int fused_spmm16(lz_handle *h, int64_t n, const int64_t *rp, const int32_t *col,
     LZ_ARG_CHECK(tiles >= 1 && tiles < (1LL << 31), "tile count");
     const bool buf = nx * 128 < (1LL << 31) && nx < (1 << 24);
     static const char *variant = getenv("LZ_FUSED_KERNEL");  // "tile": the tile-per-block kernel
+    if (buf && variant && variant[0] == 's') {  // nnz-split tiles (k_fused_seg16)
+        static int bpc = 0;
+        if (!bpc) {
+            LZ_HIP_TRY(hipOccupancyMaxActiveBlocksPerMultiprocessor(&bpc, k_fused_seg16, 256, 0));
+            bpc = std::max(bpc, 1);
+        }
+        const int64_t ntile = ceil_div(n, (int64_t)kSegTR);
+        const int grid = (int)std::max<int64_t>(1, std::min<int64_t>(ntile, (int64_t)h->n_cu * bpc));
+        LZ_TRY(ensure_partials(h, (size_t)grid * 256));
+        const int ev = prof_begin(h, PROF_SPMM_PASS);
+        hipLaunchKernelGGL(k_fused_seg16, dim3(grid), dim3(256), 0, h->stream, n, rp, col, val, Wg, nx, Wown,
+                           Qbuf, Wn, binv, beta, lc, qrow, h->partials);
+        prof_end(h, ev);
+        LZ_LAUNCH_CHECK();
+        return fold_slabs(h, h->partials, grid, 256, nparts);
+    }
     if (buf && variant && variant[0] == 'p') {
         const int grid = (int)std::max<int64_t>(1, std::min<int64_t>(ceil_div(ceil_div(n, (int64_t)16), 8),
                                                                      2 * (int64_t)h->n_cu));
@@ -1358,9 +1662,14 @@ int fused_update16(lz_handle *h, int64_t n, double *Wn, const double *Q, const d
 {
     const int64_t units = ceil_div(ceil_div(n, 16), 8);
     const int grid = (int)std::max<int64_t>(1, std::min<int64_t>(units, h->n_cu * 2));
+    static const char *order = getenv("LZ_UPDATE_ORDER");  // "f": forward (A/B)
     const int ev = prof_begin(h, PROF_UPDATE_PASS);
-    hipLaunchKernelGGL(k_fused_update16, dim3(grid), dim3(512), 0, h->stream, n, Wn, Q, alpha,
-                       h->partials);
+    if (order && order[0] == 'f')
+        hipLaunchKernelGGL(k_fused_update16<false>, dim3(grid), dim3(512), 0, h->stream, n, Wn, Q, alpha,
+                           h->partials);
+    else
+        hipLaunchKernelGGL(k_fused_update16<true>, dim3(grid), dim3(512), 0, h->stream, n, Wn, Q, alpha,
+                           h->partials);
     prof_end(h, ev);
     LZ_LAUNCH_CHECK();
     *nparts = grid;
