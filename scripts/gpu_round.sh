@@ -20,5 +20,5 @@ timeout -k 10 300 rocprofv3 --pmc WRITE_SIZE --output-format csv -d $O/write -o 
 cd $ROOT
 NNZ=$(python -c "import json;print(json.load(open('$O/bench.json'))['config']['nnz_per_gpu'])")
 python scripts/pmc_traffic.py $O/fetch $O/write k_fused_ws16 10000000 $NNZ 4096 $O/pmc_k_fused_ws16.json
-python scripts/pmc_traffic.py $O/fetch $O/write k_spmm_buf 10000000 $NNZ 4096 $O/pmc_k_spmm_buf.json
+python scripts/pmc_traffic.py $O/fetch $O/write k_spmm_seg 10000000 $NNZ 4096 $O/pmc_k_spmm_seg.json
 python scripts/pmc_traffic.py $O/fetch $O/write k_fused_update16 10000000 $NNZ 4096 $O/pmc_k_fused_update16.json
