@@ -38,9 +38,9 @@ def spmm_bytes(n, nnz, b, sv=8):
 
 
 def fused_pass_bytes(n, nnz, b, sv=8):
-    """Algorithmic bytes of one fused pass-1 launch: A, the Krylov block read
-    once, Q_{j-1} read, Q_j and W' written (DESIGN.md "Roofline")."""
-    return nnz * (sv + 4) + (n + 1) * 8 + 4 * n * b * sv
+    """Algorithmic bytes of one fused pass-1 launch (Q-free iteration): A, the
+    Krylov block W_j read once, W_{j-1} read, W' written."""
+    return nnz * (sv + 4) + (n + 1) * 8 + 3 * n * b * sv
 
 
 def fused_kernel():
@@ -157,12 +157,11 @@ def main():
             h.halo_init(rank * n, n, rcnt, hrows)
             halo_rows = int(hrows.size)
             Ad = lz.CsrDevice.from_host(lz.CsrHost(A.n, A.row_ptr, ccol, A.val), n_cols=n + halo_rows)
-            Q0 = torch.zeros(n, b, **kw)
             X0, X1 = (torch.zeros(n + halo_rows, b, **kw) for _ in range(2))
             log(f"[rank {rank}] halo rows {halo_rows}")
 
             def run(m):
-                h.block_lanczos_halo(Ad, Bd, m, 84, 0, q, alpha, beta, Q0, X0, X1)
+                h.block_lanczos_halo(Ad, Bd, m, 84, 0, q, alpha, beta, X0, X1)
         else:
             Ad = lz.CsrDevice.from_host(A, n_cols=n * world)
             Q0, W = (torch.zeros(n, b, **kw) for _ in range(2))
@@ -247,7 +246,7 @@ def main():
                     "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": plain["frac_of_hbm_peak"], "traffic": None}
         else:
             roof = None
-        iter_min_bytes = A.nnz * 12 + (n + 1) * 8 + 8 * n * b * 8
+        iter_min_bytes = A.nnz * 12 + (n + 1) * 8 + 8 * n * b * 8  # SURVEY.md 8(d) convention, fixed
         out = {
             "metric": "block-Lanczos iters/sec + SpMM achieved HBM GB/s vs peak, n=10M nnz=1e8 b=16",
             "value": round(value, 3),

@@ -81,7 +81,7 @@ HIP_SYMBOLS = [
     ("lz_halo_sizes", _c_int, [_c_vp, _c_vp, _c_vp]),
     ("lz_halo_exchange", _c_int, [_c_vp, _c_int, _c_int, _c_vp]),
     ("lz_block_lanczos_halo", _c_int, [_c_vp, _c_i64, _c_i64, _c_vp, _c_vp, _c_vp, _c_int, _c_int, _c_int,
-                                       _c_i64, _c_int, _c_vp, _c_vp, _c_vp, _c_vp, _c_vp, _c_vp, _c_vp]),
+                                       _c_i64, _c_int, _c_vp, _c_vp, _c_vp, _c_vp, _c_vp, _c_vp]),
     ("lz_comm_destroy", _c_int, [_c_vp]),
     ("lz_block_lanczos_dist", _c_int, [_c_vp, _c_i64, _c_i64, _c_i64, _c_i64, _c_vp, _c_vp, _c_vp,
                                        _c_int, _c_int, _c_int, _c_i64, _c_int, _c_vp, _c_vp, _c_vp,
@@ -574,13 +574,13 @@ class Handle:
         _check(self.L.lz_halo_exchange(self.ptr, _dt(X), X.shape[1], _ptr(X)), "lz_halo_exchange")
 
     def block_lanczos_halo(self, A_local: CsrDevice, B_local, m: int, lc_local: int, lc_rank: int,
-                           q, alpha, beta, Q0, X0, X1):
+                           q, alpha, beta, X0, X1):
         """Distributed block Lanczos over the halo plan (A_local.col in the compact numbering)."""
         n_local, b = A_local.n, B_local.shape[1]
         _check(self.L.lz_block_lanczos_halo(self.ptr, n_local, A_local.nnz, _ptr(A_local.row_ptr),
                                             _ptr(A_local.col), _ptr(A_local.val), A_local.dtype, b, m,
                                             lc_local, lc_rank, _ptr(B_local), _ptr(q), _ptr(alpha),
-                                            _ptr(beta), _ptr(Q0), _ptr(X0), _ptr(X1)),
+                                            _ptr(beta), _ptr(X0), _ptr(X1)),
                "lz_block_lanczos_halo")
 
 

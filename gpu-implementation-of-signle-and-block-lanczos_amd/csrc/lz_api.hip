@@ -112,28 +112,47 @@ static int block_lanczos_unfused(lz_handle *h, int64_t n, const int64_t *rp, con
     return LZ_OK;
 }
 
-// Fused device-resident iteration, b = 16 fp64 (lz_fused.hip).
+// Fused device-resident iteration, b = 16 fp64 (lz_fused.hip), Q-free: the
+// normalised block Q_j = W_j beta_j^-1 is formed in registers where it is used
+// (pass 1: the alpha slabs and the row probe; Q_j's other two uses fold into
+// 16 x 16 products: Q_{j-1} beta_j = W_{j-1} (beta_{j-1}^-1 beta_j) in pass 1,
+// Q_j alpha_j = W_j (beta_j^-1 alpha_j) in pass 2), so no pass writes or reads
+// Q: A + 6 n b s bytes per step instead of A + 7 n b s.  Residual buffers:
+// W_0 = B (read only); step j's output W' -> W'' goes to W at j = 0, Q1 at
+// j = 1 and from then on in place over W_{j-1} (row r read, then written, by
+// the same wave).  The inverse square roots of two consecutive steps live in
+// two scratch slots; beta[m] gets the last one, as the reference's.
+struct QfreeBufs {
+    double *binv[2], *P;
+    explicit QfreeBufs(lz_handle *h) : binv{h->scratch + 4 * 256, h->scratch + 5 * 256}, P(h->scratch + 6 * 256) {}
+};
+
 static int block_lanczos_fused16(lz_handle *h, int64_t n, const int64_t *rp, const int32_t *col,
                                  const double *val, int m, int64_t lc, const double *B, double *q,
                                  double *alpha, double *beta, double *Q0, double *Q1, double *W)
 {
     constexpr int64_t bb = 256;
-    double *binv = beta + m * bb;
+    (void)Q0;
+    QfreeBufs qb(h);
     int P = 0;
     LZ_TRY(gram_partials<double>(h, n, 16, B, B, 16, &P));
-    LZ_TRY(sqrtm_pair<double>(h, 16, nullptr, P, beta, binv, nullptr));
-    const double *res_in = B;
-    double *bufs[2] = {W, Q1};  // the residual alternates; Q_j lives in Q0
+    LZ_TRY(sqrtm_pair<double>(h, 16, nullptr, P, beta, qb.binv[0], nullptr));
+    const double *in = B, *prev = nullptr;
     for (int j = 0; j < m; ++j) {
-        double *res_out = bufs[j & 1];
-        LZ_TRY(fused_spmm16(h, n, rp, col, val, res_in, n, res_in, Q0, res_out, binv,
-                            j ? beta + j * bb : nullptr, lc, q + j * 16, &P));
+        double *out = j == 0 ? W : j == 1 ? Q1 : const_cast<double *>(prev);
+        const double *bi = qb.binv[j & 1];
+        if (j) LZ_TRY(mm16(h, qb.binv[(j - 1) & 1], beta + j * bb, qb.P));       // P1
+        LZ_TRY(fused_spmm16(h, n, rp, col, val, in, n, in, prev, out, bi, j ? qb.P : nullptr, lc, q + j * 16, &P));
         LZ_TRY(gram_finish<double>(h, 16, P, 1, alpha + j * bb, h->partials2));
-        LZ_TRY(fused_update16(h, n, res_out, Q0, alpha + j * bb, &P));
+        LZ_TRY(mm16(h, bi, alpha + j * bb, qb.P));                               // P2
+        LZ_TRY(fused_update16(h, n, out, in, qb.P, &P));
         if (j + 1 < m)
-            LZ_TRY(sqrtm_pair<double>(h, 16, nullptr, P, beta + (j + 1) * bb, binv, nullptr));
-        res_in = res_out;
+            LZ_TRY(sqrtm_pair<double>(h, 16, nullptr, P, beta + (j + 1) * bb, qb.binv[(j + 1) & 1], nullptr));
+        prev = in;
+        in = out;
     }
+    LZ_HIP_TRY(hipMemcpyAsync(beta + m * bb, qb.binv[(m - 1) & 1], sizeof(double) * bb, hipMemcpyDeviceToDevice,
+                              h->stream));
     return LZ_OK;
 }
 
@@ -164,9 +183,11 @@ static ncclComm_t comm_of(lz_handle *h) { return reinterpret_cast<ncclComm_t>(h-
         }                                                                            \
     } while (0)
 
-// b = 16 fp64 row-partitioned iteration.  Per step: ncclAllGather of the
-// residual slab into X_full, the fused SpMM pass on local rows, two b x b
-// ncclAllReduce (alpha and Gram partial sums), sqrtm redundantly on every rank.
+// b = 16 fp64 row-partitioned iteration (Q-free, as block_lanczos_fused16).
+// Per step: ncclAllGather of the residual slab into X_full, the fused pass on
+// local rows, two b x b ncclAllReduce (alpha and Gram partial sums), sqrtm
+// redundantly on every rank.  Local residual slabs (n_pad rows): W at step 0,
+// Q0 at step 1, then in place over the previous step's slab.
 static int block_lanczos_dist16(lz_handle *h, int64_t n_local, int64_t n_pad, const int64_t *rp,
                                 const int32_t *col, const double *val, int m, int64_t lc_local,
                                 const double *B, double *q, double *alpha, double *beta, double *Q0,
@@ -174,7 +195,7 @@ static int block_lanczos_dist16(lz_handle *h, int64_t n_local, int64_t n_pad, co
 {
     constexpr int64_t bb = 256;
     ncclComm_t comm = comm_of(h);
-    double *binv = beta + m * bb;
+    QfreeBufs qb(h);
     double *slab = h->scratch;  // one reduced b x b slab, all-reduced in place
     const double *own = X + (int64_t)h->rank * n_pad * 16;
     int P = 0;
@@ -182,22 +203,31 @@ static int block_lanczos_dist16(lz_handle *h, int64_t n_local, int64_t n_pad, co
     LZ_TRY(gram_partials<double>(h, n_local, 16, B, B, 16, &P));
     LZ_TRY(gram_finish<double>(h, 16, P, 0, slab));
     LZ_NCCL_TRY(ncclAllReduce(slab, slab, bb, ncclDouble, ncclSum, comm, h->stream));
-    LZ_TRY(sqrtm_pair<double>(h, 16, nullptr, 1, beta, binv, nullptr, slab));
+    LZ_TRY(sqrtm_pair<double>(h, 16, nullptr, 1, beta, qb.binv[0], nullptr, slab));
     LZ_NCCL_TRY(ncclAllGather(B, X, n_pad * 16, ncclDouble, comm, h->stream));
+    const double *cur = B, *prev = nullptr;  // this rank's W_j, W_{j-1}
     for (int j = 0; j < m; ++j) {
-        LZ_TRY(fused_spmm16(h, n_local, rp, col, val, X, n_pad * h->nranks, own, Q0, W, binv,
-                            j ? beta + j * bb : nullptr, lc_local, q + j * 16, &P));
+        double *out = j == 0 ? W : j == 1 ? Q0 : const_cast<double *>(prev);
+        const double *bi = qb.binv[j & 1];
+        if (j) LZ_TRY(mm16(h, qb.binv[(j - 1) & 1], beta + j * bb, qb.P));
+        LZ_TRY(fused_spmm16(h, n_local, rp, col, val, X, n_pad * h->nranks, own, prev, out, bi,
+                            j ? qb.P : nullptr, lc_local, q + j * 16, &P));
         LZ_TRY(gram_finish<double>(h, 16, P, 0, slab, h->partials2));
         LZ_NCCL_TRY(ncclAllReduce(slab, slab, bb, ncclDouble, ncclSum, comm, h->stream));
         LZ_TRY(gram_finish<double>(h, 16, 1, 1, alpha + j * bb, slab));
-        LZ_TRY(fused_update16(h, n_local, W, Q0, alpha + j * bb, &P));
+        LZ_TRY(mm16(h, bi, alpha + j * bb, qb.P));
+        LZ_TRY(fused_update16(h, n_local, out, cur, qb.P, &P));
         if (j + 1 < m) {
             LZ_TRY(gram_finish<double>(h, 16, P, 0, slab));
             LZ_NCCL_TRY(ncclAllReduce(slab, slab, bb, ncclDouble, ncclSum, comm, h->stream));
-            LZ_TRY(sqrtm_pair<double>(h, 16, nullptr, 1, beta + (j + 1) * bb, binv, nullptr, slab));
-            LZ_NCCL_TRY(ncclAllGather(W, X, n_pad * 16, ncclDouble, comm, h->stream));
+            LZ_TRY(sqrtm_pair<double>(h, 16, nullptr, 1, beta + (j + 1) * bb, qb.binv[(j + 1) & 1], nullptr, slab));
+            LZ_NCCL_TRY(ncclAllGather(out, X, n_pad * 16, ncclDouble, comm, h->stream));
         }
+        prev = cur;
+        cur = out;
     }
+    LZ_HIP_TRY(hipMemcpyAsync(beta + m * bb, qb.binv[(m - 1) & 1], sizeof(double) * bb, hipMemcpyDeviceToDevice,
+                              h->stream));
     return LZ_OK;
 }
 
@@ -276,39 +306,45 @@ static int allreduce_bb(lz_handle *h, double *slab)
 }
 
 // b = 16 fp64.  Same step as block_lanczos_dist16 with the all-gather replaced
-// by the halo exchange; the residual alternates between X0 and X1 (the fused
-// pass gathers from one while writing the other), Q_j stays in Q0.
+// by the halo exchange; the residual alternates between X0 and X1: the fused
+// pass gathers from one and writes the other, whose own rows hold W_{j-1}
+// (read, then overwritten, row by row) -- Q-free as block_lanczos_fused16.
 static int block_lanczos_halo16(lz_handle *h, const HaloPlan &hp, const int64_t *rp, const int32_t *col,
                                 const double *val, int m, int64_t lc_local, const double *B, double *q,
-                                double *alpha, double *beta, double *Q0, double *X0, double *X1)
+                                double *alpha, double *beta, double *X0, double *X1)
 {
     constexpr int64_t bb = 256;
     const int64_t n = hp.n_local, nx = hp.n_local + hp.n_halo;
-    double *binv = beta + m * bb;
+    QfreeBufs qb(h);
     double *slab = h->scratch;
     int P = 0;
     LZ_TRY(gram_partials<double>(h, n, 16, B, B, 16, &P));
     LZ_TRY(gram_finish<double>(h, 16, P, 0, slab));
     LZ_TRY(allreduce_bb(h, slab));
-    LZ_TRY(sqrtm_pair<double>(h, 16, nullptr, 1, beta, binv, nullptr, slab));
+    LZ_TRY(sqrtm_pair<double>(h, 16, nullptr, 1, beta, qb.binv[0], nullptr, slab));
     LZ_HIP_TRY(hipMemcpyAsync(X0, B, sizeof(double) * n * 16, hipMemcpyDeviceToDevice, h->stream));
     LZ_TRY(halo_exchange16(h, hp, X0));
     double *xs[2] = {X0, X1};
     for (int j = 0; j < m; ++j) {
         double *in = xs[j & 1], *out = xs[(j + 1) & 1];
-        LZ_TRY(fused_spmm16(h, n, rp, col, val, in, nx, in, Q0, out, binv, j ? beta + j * bb : nullptr,
+        const double *bi = qb.binv[j & 1];
+        if (j) LZ_TRY(mm16(h, qb.binv[(j - 1) & 1], beta + j * bb, qb.P));
+        LZ_TRY(fused_spmm16(h, n, rp, col, val, in, nx, in, j ? out : nullptr, out, bi, j ? qb.P : nullptr,
                             lc_local, q + j * 16, &P));
         LZ_TRY(gram_finish<double>(h, 16, P, 0, slab, h->partials2));
         LZ_TRY(allreduce_bb(h, slab));
         LZ_TRY(gram_finish<double>(h, 16, 1, 1, alpha + j * bb, slab));
-        LZ_TRY(fused_update16(h, n, out, Q0, alpha + j * bb, &P));
+        LZ_TRY(mm16(h, bi, alpha + j * bb, qb.P));
+        LZ_TRY(fused_update16(h, n, out, in, qb.P, &P));
         if (j + 1 < m) {
             LZ_TRY(gram_finish<double>(h, 16, P, 0, slab));
             LZ_TRY(allreduce_bb(h, slab));
-            LZ_TRY(sqrtm_pair<double>(h, 16, nullptr, 1, beta + (j + 1) * bb, binv, nullptr, slab));
+            LZ_TRY(sqrtm_pair<double>(h, 16, nullptr, 1, beta + (j + 1) * bb, qb.binv[(j + 1) & 1], nullptr, slab));
             LZ_TRY(halo_exchange16(h, hp, out));
         }
     }
+    LZ_HIP_TRY(hipMemcpyAsync(beta + m * bb, qb.binv[(m - 1) & 1], sizeof(double) * bb, hipMemcpyDeviceToDevice,
+                              h->stream));
     return LZ_OK;
 }
 
@@ -797,7 +833,7 @@ int lz_halo_exchange(lz_handle *h, lz_dtype dtype, int b, void *X)
 int lz_block_lanczos_halo(lz_handle *h, int64_t n_local, int64_t nnz_local, const int64_t *rp,
                           const int32_t *col, const void *val, lz_dtype dtype, int b, int m,
                           int64_t lc_local, int lc_rank, const void *B_local, void *q, void *alpha,
-                          void *beta, void *Q0, void *X0, void *X1)
+                          void *beta, void *X0, void *X1)
 {
     LZ_HANDLE_CHECK(h);
     LZ_ARG_CHECK(h->halo, "lz_halo_init first");
@@ -806,11 +842,10 @@ int lz_block_lanczos_halo(lz_handle *h, int64_t n_local, int64_t nnz_local, cons
     LZ_ARG_CHECK(n_local == hp.n_local, "n_local differs from lz_halo_init");
     LZ_ARG_CHECK(dtype == LZ_F64 && b == 16, "halo path: b = 16 fp64");
     LZ_ARG_CHECK(m >= 1 && n_local >= 1, "sizes");
-    LZ_ARG_CHECK(B_local && q && alpha && beta && Q0 && X0 && X1 && X0 != X1, "NULL / aliased buffer");
+    LZ_ARG_CHECK(B_local && q && alpha && beta && X0 && X1 && X0 != X1, "NULL / aliased buffer");
     const int64_t lc = (lc_rank == h->rank) ? lc_local : -1;
     return block_lanczos_halo16(h, hp, rp, col, (const double *)val, m, lc, (const double *)B_local,
-                                (double *)q, (double *)alpha, (double *)beta, (double *)Q0, (double *)X0,
-                                (double *)X1);
+                                (double *)q, (double *)alpha, (double *)beta, (double *)X0, (double *)X1);
 }
 
 }  // extern "C"

@@ -104,8 +104,8 @@ template <bool BUF>
 __global__ __launch_bounds__(512, 4) void k_fused_spmm16(
     int64_t n, const int64_t *__restrict__ rp, const int32_t *__restrict__ col,
     const double *__restrict__ val, const double *__restrict__ Wg, int64_t nx,
-    const double *__restrict__ Wown, double *__restrict__ Qbuf,
-    double *__restrict__ Wn, const double *__restrict__ binv, const double *__restrict__ beta,
+    const double *__restrict__ Wown, const double *Qbuf,
+    double *Wn, const double *__restrict__ binv, const double *__restrict__ beta,
     int64_t lc, double *__restrict__ qrow, double *__restrict__ part)
 {
     __shared__ double tile[8][16 * 17];
@@ -258,7 +258,6 @@ __global__ __launch_bounds__(512, 4) void k_fused_spmm16(
         for (int r = 0; r < 4; ++r) {
             const int64_t row = r0 + (lane >> 4) + 4 * r;
             if (row < n) {
-                Qbuf[r0 * 16 + 64 * r + lane] = q1[r];
                 Wn[r0 * 16 + 64 * r + lane] = wn[r];
                 if (row == lc) qrow[lane & 15] = q1[r];
             }
@@ -455,7 +454,7 @@ template <int NC, int CAP, int FW_K, bool QREG = false, int NL = 1>
 __global__ __launch_bounds__(64 * (NC + NL)) void k_fused_ws16(
     int64_t n, const int64_t *__restrict__ rp, const int32_t *__restrict__ col,
     const double *__restrict__ val, const double *__restrict__ Wg, int64_t nx,
-    const double *__restrict__ Wown, double *__restrict__ Qbuf, double *__restrict__ Wn,
+    const double *__restrict__ Wown, const double *Qbuf, double *Wn,
     const double *__restrict__ binv, const double *__restrict__ beta, int64_t lc,
     double *__restrict__ qrow, double *__restrict__ part, int *__restrict__ err)
 {
@@ -530,7 +529,7 @@ __global__ __launch_bounds__(64 * (NC + NL)) void k_fused_ws16(
             ws_dma(cr, st[s].col, C::COL_PIECES, lane);
             ws_dma(vr, st[s].val, C::VAL_PIECES, lane);
             if constexpr (!QREG) {
-                const auto qr = __builtin_amdgcn_make_buffer_rsrc(Qbuf + r0 * 16, (short)0,
+                const auto qr = __builtin_amdgcn_make_buffer_rsrc(const_cast<double *>(Qbuf) + r0 * 16, (short)0,
                                                                   has_prev && !(dbg & 1) ? (int)((r1 - r0) * 128) : 0,
                                                                   0x00020000);
                 fw_strips_dma<NC>(qr, st[s].qt, lane);
@@ -576,7 +575,7 @@ __global__ __launch_bounds__(64 * (NC + NL)) void k_fused_ws16(
                                                               (int)(cb < 0x7fffffff ? cb : 0x7fffffff), 0x00020000);
             const auto vr = __builtin_amdgcn_make_buffer_rsrc(const_cast<double *>(val + va), (short)0,
                                                               (int)(vb < 0x7fffffff ? vb : 0x7fffffff), 0x00020000);
-            const auto qr = __builtin_amdgcn_make_buffer_rsrc(Qbuf + r0 * 16, (short)0,
+            const auto qr = __builtin_amdgcn_make_buffer_rsrc(const_cast<double *>(Qbuf) + r0 * 16, (short)0,
                                                               has_prev && !(dbg & 1) ? (int)((r1 - r0) * 128) : 0,
                                                               0x00020000);
             ws_dma(rr, st[s].rp, C::RP_PIECES, lane);
@@ -702,7 +701,6 @@ __global__ __launch_bounds__(64 * (NC + NL)) void k_fused_ws16(
         for (int r = 0; r < 4; ++r) {
             const int64_t row = s0 + (lane >> 4) + 4 * r;
             if (row < n && !(dbg & 4)) {
-                Qbuf[s0 * 16 + 64 * r + lane] = q1[r];
                 Wn[s0 * 16 + 64 * r + lane] = wn[r];
                 if (row == lc) qrow[lane & 15] = q1[r];
             }
@@ -739,7 +737,7 @@ template <int NC, int CAP, int K, int NL>
 __global__ __launch_bounds__(64 * (NC + NL)) void k_fused_pp16(
     int64_t n, const int64_t *__restrict__ rp, const int32_t *__restrict__ col,
     const double *__restrict__ val, const double *__restrict__ Wg, int64_t nx,
-    const double *__restrict__ Wown, double *__restrict__ Qbuf, double *__restrict__ Wn,
+    const double *__restrict__ Wown, const double *Qbuf, double *Wn,
     const double *__restrict__ binv, const double *__restrict__ beta, int64_t lc,
     double *__restrict__ qrow, double *__restrict__ part, int *__restrict__ err)
 {
@@ -872,7 +870,6 @@ __global__ __launch_bounds__(64 * (NC + NL)) void k_fused_pp16(
         for (int r = 0; r < 4; ++r) {
             const int64_t row = s0p + (lane >> 4) + 4 * r;
             if (row < n) {
-                Qbuf[s0p * 16 + 64 * r + lane] = q1[r];
                 Wn[s0p * 16 + 64 * r + lane] = wn[r];
                 if (row == lc) qrow[lane & 15] = q1[r];
             }
@@ -1074,7 +1071,7 @@ template <int UNR>
 __global__ __launch_bounds__(512, 4) void k_fused_pf16(
     int64_t n, const int64_t *__restrict__ rp, const int32_t *__restrict__ col,
     const double *__restrict__ val, const double *__restrict__ Wg, int64_t nx,
-    const double *__restrict__ Wown, double *__restrict__ Qbuf, double *__restrict__ Wn,
+    const double *__restrict__ Wown, const double *Qbuf, double *Wn,
     const double *__restrict__ binv, const double *__restrict__ beta, int64_t lc,
     double *__restrict__ qrow, double *__restrict__ part, int dbg)
 {
@@ -1139,7 +1136,7 @@ __global__ __launch_bounds__(512, 4) void k_fused_pf16(
         const int wb = live && !(dbg & 2) ? (int)(rows * 128) : 0;
         const auto wr = __builtin_amdgcn_make_buffer_rsrc(const_cast<double *>(Wown + s0 * 16), (short)0, wb,
                                                           0x00020000);
-        const auto qr = __builtin_amdgcn_make_buffer_rsrc(Qbuf + s0 * 16, (short)0, has_prev ? wb : 0, 0x00020000);
+        const auto qr = __builtin_amdgcn_make_buffer_rsrc(const_cast<double *>(Qbuf) + s0 * 16, (short)0, has_prev ? wb : 0, 0x00020000);
         const uint32_t o = (uint32_t)(lane * 32);  // row lane >> 2, doubles 4 (lane & 3) .. + 3
         P.wr[0] = pf_ld16d(wr, o);
         P.wr[1] = pf_ld16d(wr, o + 16);
@@ -1287,7 +1284,6 @@ __global__ __launch_bounds__(512, 4) void k_fused_pf16(
         for (int r = 0; r < 4; ++r) {
             const int64_t row = s0 + (lane >> 4) + 4 * r;
             if (row < n && !(dbg & 4)) {
-                Qbuf[s0 * 16 + 64 * r + lane] = q1[r];
                 Wn[s0 * 16 + 64 * r + lane] = wn[r];
                 if (row == lc) qrow[lane & 15] = q1[r];
             }
@@ -1327,8 +1323,8 @@ __device__ __forceinline__ __amdgpu_buffer_rsrc_t seg_rsrc(const void *p, uint32
 __global__ __launch_bounds__(256, 4) void k_fused_seg16(
     int64_t n, const int64_t *__restrict__ rp, const int32_t *__restrict__ col,
     const double *__restrict__ val, const double *__restrict__ Wg, int64_t nx,
-    const double *__restrict__ Wown, double *__restrict__ Qbuf,
-    double *__restrict__ Wn, const double *__restrict__ binv, const double *__restrict__ beta,
+    const double *__restrict__ Wown, const double *Qbuf,
+    double *Wn, const double *__restrict__ binv, const double *__restrict__ beta,
     int64_t lc, double *__restrict__ qrow, double *__restrict__ part)
 {
     constexpr int TR = kSegTR, CAP = kSegCap, G = 32, UNR = 8, YS = 17;
@@ -1536,9 +1532,9 @@ __global__ __launch_bounds__(256, 4) void k_fused_seg16(
             // Q_j and W' leave as 16-B row pieces through the scratch
             const int row = lane >> 3, c2 = 2 * (lane & 7);
 #pragma unroll
-            for (int m = 0; m < 2; ++m) {
+            for (int m = 0; m < 2; ++m) {  // m = 0: Q_j (row probe only), m = 1: W'
                 const d4_t &v = m ? wn : q1;
-                double *dst = m ? Wn : Qbuf;
+                double *dst = Wn;
 #pragma unroll
                 for (int r = 0; r < 4; ++r) T[((lane >> 4) + 4 * r) * 17 + (lane & 15)] = v[r];
                 wave_lds_sync();
@@ -1548,7 +1544,7 @@ __global__ __launch_bounds__(256, 4) void k_fused_seg16(
                     const int64_t grow = rs + rr;
                     const double x0 = T[rr * 17 + c2], x1 = T[rr * 17 + c2 + 1];
                     if (16 * w + rr < nrows) {
-                        *reinterpret_cast<double2 *>(dst + grow * 16 + c2) = double2{x0, x1};
+                        if (m == 1) *reinterpret_cast<double2 *>(dst + grow * 16 + c2) = double2{x0, x1};
                         if (m == 0 && grow == lc) {
                             qrow[c2] = x0;
                             qrow[c2 + 1] = x1;
@@ -1570,9 +1566,37 @@ __global__ __launch_bounds__(256, 4) void k_fused_seg16(
     part[(int64_t)blockIdx.x * 256 + tid] = ((sbuf[tid] + sbuf[256 + tid]) + sbuf[512 + tid]) + sbuf[768 + tid];
 }
 
+// C = A * B, 16 x 16 row-major fp64 (the per-step P1 = beta_{j-1}^-1 beta_j and
+// P2 = beta_j^-1 alpha_j of the Q-free iteration, lz_api.hip)
+__global__ __launch_bounds__(256) void k_mm16(const double *__restrict__ A, const double *__restrict__ B,
+                                              double *__restrict__ C)
+{
+    __shared__ double a[256], b[256];
+    const int t = threadIdx.x;
+    a[t] = A[t];
+    b[t] = B[t];
+    __syncthreads();
+    const int i = t >> 4, j = t & 15;
+    double s = 0.0;
+#pragma unroll
+    for (int k = 0; k < 16; ++k) s = fma(a[i * 16 + k], b[k * 16 + j], s);
+    C[t] = s;
+}
+
+int mm16(lz_handle *h, const double *A, const double *B, double *C)
+{
+    const int ev = prof_begin(h, PROF_SMALL);
+    hipLaunchKernelGGL(k_mm16, dim3(1), dim3(256), 0, h->stream, A, B, C);
+    prof_end(h, ev);
+    LZ_LAUNCH_CHECK();
+    return LZ_OK;
+}
+
+// Qbuf: W_{j-1} (own rows; may be the same buffer as Wn, row r is read before
+// it is written by the same wave), beta: P1 = beta_{j-1}^-1 beta_j (or null at j = 0)
 int fused_spmm16(lz_handle *h, int64_t n, const int64_t *rp, const int32_t *col, const double *val,
-                 const double *Wg, int64_t nx, const double *Wown, double *Qbuf, double *Wn, const double *binv,
-                 const double *beta, int64_t lc, double *qrow, int *nparts)
+                 const double *Wg, int64_t nx, const double *Wown, const double *Qbuf, double *Wn,
+                 const double *binv, const double *beta, int64_t lc, double *qrow, int *nparts)
 {
     const int64_t tiles = ceil_div(n, kFusedRows);
     LZ_ARG_CHECK(tiles >= 1 && tiles < (1LL << 31), "tile count");

@@ -35,16 +35,21 @@ template <typename T>
 int copy_row(lz_handle *h, int b, const T *Q, int64_t ld, int col_major, int64_t lc, T *q);
 
 // ---- fused block-Lanczos passes, b = 16 fp64 (lz_fused.hip)
-// Pass 1: Y = A*Wg; Qbuf[r] <- Wg[r]*binv (after reading Qbuf[r] when beta
-// != nullptr); Wn[r] = Y[r]*binv - Qprev[r]*beta; slabs of Qbuf^T Wn; row probe.
-// nx: rows of Wg.  Wown: the rows r of Wg this rank owns (== Wg single-GPU; a slice of the
-// all-gathered block multi-GPU).
+// Q-free form: Q_j = W_j beta_j^-1 is formed in registers wherever it is used
+// and never stored.
+// Pass 1: Y = A*Wg; Q_j[r] = Wown[r]*binv; Wn[r] = Y[r]*binv - Wprev[r]*P1
+// (P1 = beta_{j-1}^-1 beta_j, so Wprev[r]*P1 = Q_{j-1}[r] beta_j; none at j = 0);
+// slabs of Q_j^T Wn; row probe of Q_j.  nx: rows of Wg.  Wown: the rows r of Wg
+// this rank owns (== Wg single-GPU).  Wprev may be the Wn buffer (in place).
 int fused_spmm16(lz_handle *h, int64_t n, const int64_t *rp, const int32_t *col,
-                 const double *val, const double *Wg, int64_t nx, const double *Wown, double *Qbuf, double *Wn,
-                 const double *binv, const double *beta, int64_t lc, double *qrow, int *nparts);
-// Pass 2: Wn <- Wn - Q*alpha; slabs of Wn^T Wn.
-int fused_update16(lz_handle *h, int64_t n, double *Wn, const double *Q, const double *alpha,
+                 const double *val, const double *Wg, int64_t nx, const double *Wown, const double *Wprev,
+                 double *Wn, const double *binv, const double *P1, int64_t lc, double *qrow, int *nparts);
+// Pass 2: Wn <- Wn - Wcur*P2 (P2 = beta_j^-1 alpha_j, so Wcur*P2 = Q_j alpha_j);
+// slabs of Wn^T Wn.
+int fused_update16(lz_handle *h, int64_t n, double *Wn, const double *Wcur, const double *P2,
                    int *nparts);
+// C = A*B, 16 x 16 row-major fp64, on the stream
+int mm16(lz_handle *h, const double *A, const double *B, double *C);
 
 // fp64 scalar helpers for the vector Lanczos (lz_fused.hip)
 int vector_lanczos_dev(lz_handle *h, int64_t n, int64_t nnz, const int64_t *rp, const int32_t *col,

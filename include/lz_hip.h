@@ -168,7 +168,8 @@ int lz_comm_destroy(lz_handle *h);
  * the all-gathered Krylov block every iteration (ncclAllGather over xGMI);
  * row_counts[nranks] (host) = rows per rank (the all-gather needs equal counts:
  * every rank passes max(row_counts) as n_pad and pads its slab).  B_local,
- * Q0,Q1,W: n_local x b.  lc_rank: the rank owning row lc (q written there only;
+ * Q0, W: n_pad x b (the residual slab alternates between W and Q0 and is
+ * all-gathered whole); Q1 unused.  lc_rank: the rank owning row lc (q written there only;
  * other ranks' q untouched).  Outputs alpha/beta identical on every rank. */
 int lz_block_lanczos_dist(lz_handle *h, int64_t n_local, int64_t n_pad, int64_t n_global,
                           int64_t nnz_local, const int64_t *row_ptr, const int32_t *col,
@@ -194,13 +195,13 @@ int lz_halo_sizes(lz_handle *h, int64_t *n_halo, int64_t *n_send);
 int lz_halo_exchange(lz_handle *h, lz_dtype dtype, int b, void *X);
 /* Distributed block Lanczos over the halo plan; replaces the single-GPU
  * block_lanczos_blas (methods/block_lanczos.hpp:88-167) on a row partition.
- * col: compact numbering from lzh_halo_plan.  B_local, Q0: n_local x 16; X0,
- * X1: (n_local + n_halo) x 16 workspaces (the residual alternates between them).
+ * col: compact numbering from lzh_halo_plan.  B_local: n_local x 16; X0, X1:
+ * (n_local + n_halo) x 16 workspaces (the residual alternates between them).
  * alpha/beta identical on every rank; q written on lc_rank only. */
 int lz_block_lanczos_halo(lz_handle *h, int64_t n_local, int64_t nnz_local, const int64_t *row_ptr,
                           const int32_t *col, const void *val, lz_dtype dtype, int b, int m,
                           int64_t lc_local, int lc_rank, const void *B_local, void *q, void *alpha,
-                          void *beta, void *Q0, void *X0, void *X1);
+                          void *beta, void *X0, void *X1);
 
 #ifdef __cplusplus
 }

@@ -32,8 +32,8 @@ def _run_halo(lz, h, torch, A, B, m, lc):
     h.halo_init(0, n, cnt, rows)
     assert h.halo_sizes() == (0, 0)
     Ad = lz.CsrDevice.from_host(lz.CsrHost(n, A.row_ptr, cc, A.val))
-    q, al, be, Q0, X0, X1 = _bufs(torch, n, n, m)
-    h.block_lanczos_halo(Ad, torch.from_numpy(B).cuda(), m, lc, 0, q, al, be, Q0, X0, X1)
+    q, al, be, _, X0, X1 = _bufs(torch, n, n, m)
+    h.block_lanczos_halo(Ad, torch.from_numpy(B).cuda(), m, lc, 0, q, al, be, X0, X1)
     torch.cuda.synchronize()
     return q.cpu().numpy(), al.cpu().numpy(), be.cpu().numpy()
 
@@ -60,7 +60,7 @@ def test_halo_requires_init(lz, torch_cuda):
         q, al, be, Q0, X0, X1 = _bufs(torch_cuda, 16, 16, 1)
         A = lz.CsrDevice.from_host(lz.gen_banded(16, 2.0, 4, seed=1))
         with pytest.raises(lz.LanczosError, match="lz_halo_init"):
-            h.block_lanczos_halo(A, Q0, 1, 0, 0, q, al, be, Q0, X0, X1)
+            h.block_lanczos_halo(A, Q0, 1, 0, 0, q, al, be, X0, X1)
         with pytest.raises(lz.LanczosError):  # own rows listed as halo
             h.halo_init(0, 16, np.array([3], np.int64), np.arange(3, dtype=np.int32))
     finally:
@@ -102,7 +102,7 @@ def test_wide_address_fused_pass(lz, orc, torch_cuda):
         W = torch.zeros(n_pad, 16, **kw)
         X = torch.zeros(n_pad, 16, **kw)
         q, al, be = torch.zeros(m * 16, **kw), torch.zeros(m, 16, 16, **kw), torch.zeros(m + 1, 16, 16, **kw)
-        Q0 = torch.zeros(n, 16, **kw)
+        Q0 = torch.zeros(n_pad, 16, **kw)
         Ad = lz.CsrDevice.from_host(A, n_cols=n_pad)
         h.block_lanczos_dist(Ad, n_pad, n_pad, Bp, m, lc, 0, q, al, be, Q0, W, X)
         torch.cuda.synchronize()
