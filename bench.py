@@ -53,7 +53,7 @@ def fused_kernel():
         return "k_fused_spmm16<true>", "k_fused_spmm16"
     if v.startswith("p"):
         return f"k_fused_pf16<{8 if v[1:2] == '8' else 4}>", "k_fused_pf16"
-    if v.startswith("r"):
+    if not v or v.startswith("r"):
         return "k_fused_pp16<14,2376,3,2>", "k_fused_pp16"
     if v.startswith("wsq"):
         return "k_fused_ws16<15,2536,2>", "k_fused_ws16"

@@ -141,13 +141,13 @@ static int block_lanczos_fused16(lz_handle *h, int64_t n, const int64_t *rp, con
     for (int j = 0; j < m; ++j) {
         double *out = j == 0 ? W : j == 1 ? Q1 : const_cast<double *>(prev);
         const double *bi = qb.binv[j & 1];
-        if (j) LZ_TRY(mm16(h, qb.binv[(j - 1) & 1], beta + j * bb, qb.P));       // P1
         LZ_TRY(fused_spmm16(h, n, rp, col, val, in, n, in, prev, out, bi, j ? qb.P : nullptr, lc, q + j * 16, &P));
-        LZ_TRY(gram_finish<double>(h, 16, P, 1, alpha + j * bb, h->partials2));
-        LZ_TRY(mm16(h, bi, alpha + j * bb, qb.P));                               // P2
+        // alpha_j and P2 = beta_j^-1 alpha_j in one kernel (P1 of this step is consumed)
+        LZ_TRY(gram_finish<double>(h, 16, P, 1, alpha + j * bb, h->partials2, bi, qb.P));
         LZ_TRY(fused_update16(h, n, out, in, qb.P, &P));
-        if (j + 1 < m)
-            LZ_TRY(sqrtm_pair<double>(h, 16, nullptr, P, beta + (j + 1) * bb, qb.binv[(j + 1) & 1], nullptr));
+        if (j + 1 < m)  // beta_{j+1}, its inverse and P1 = beta_j^-1 beta_{j+1}
+            LZ_TRY(sqrtm_pair<double>(h, 16, nullptr, P, beta + (j + 1) * bb, qb.binv[(j + 1) & 1], nullptr,
+                                      nullptr, bi, qb.P));
         prev = in;
         in = out;
     }
@@ -209,18 +209,17 @@ static int block_lanczos_dist16(lz_handle *h, int64_t n_local, int64_t n_pad, co
     for (int j = 0; j < m; ++j) {
         double *out = j == 0 ? W : j == 1 ? Q0 : const_cast<double *>(prev);
         const double *bi = qb.binv[j & 1];
-        if (j) LZ_TRY(mm16(h, qb.binv[(j - 1) & 1], beta + j * bb, qb.P));
         LZ_TRY(fused_spmm16(h, n_local, rp, col, val, X, n_pad * h->nranks, own, prev, out, bi,
                             j ? qb.P : nullptr, lc_local, q + j * 16, &P));
         LZ_TRY(gram_finish<double>(h, 16, P, 0, slab, h->partials2));
         LZ_NCCL_TRY(ncclAllReduce(slab, slab, bb, ncclDouble, ncclSum, comm, h->stream));
-        LZ_TRY(gram_finish<double>(h, 16, 1, 1, alpha + j * bb, slab));
-        LZ_TRY(mm16(h, bi, alpha + j * bb, qb.P));
+        LZ_TRY(gram_finish<double>(h, 16, 1, 1, alpha + j * bb, slab, bi, qb.P));
         LZ_TRY(fused_update16(h, n_local, out, cur, qb.P, &P));
         if (j + 1 < m) {
             LZ_TRY(gram_finish<double>(h, 16, P, 0, slab));
             LZ_NCCL_TRY(ncclAllReduce(slab, slab, bb, ncclDouble, ncclSum, comm, h->stream));
-            LZ_TRY(sqrtm_pair<double>(h, 16, nullptr, 1, beta + (j + 1) * bb, qb.binv[(j + 1) & 1], nullptr, slab));
+            LZ_TRY(sqrtm_pair<double>(h, 16, nullptr, 1, beta + (j + 1) * bb, qb.binv[(j + 1) & 1], nullptr, slab,
+                                      bi, qb.P));
             LZ_NCCL_TRY(ncclAllGather(out, X, n_pad * 16, ncclDouble, comm, h->stream));
         }
         prev = cur;
@@ -328,18 +327,17 @@ static int block_lanczos_halo16(lz_handle *h, const HaloPlan &hp, const int64_t 
     for (int j = 0; j < m; ++j) {
         double *in = xs[j & 1], *out = xs[(j + 1) & 1];
         const double *bi = qb.binv[j & 1];
-        if (j) LZ_TRY(mm16(h, qb.binv[(j - 1) & 1], beta + j * bb, qb.P));
         LZ_TRY(fused_spmm16(h, n, rp, col, val, in, nx, in, j ? out : nullptr, out, bi, j ? qb.P : nullptr,
                             lc_local, q + j * 16, &P));
         LZ_TRY(gram_finish<double>(h, 16, P, 0, slab, h->partials2));
         LZ_TRY(allreduce_bb(h, slab));
-        LZ_TRY(gram_finish<double>(h, 16, 1, 1, alpha + j * bb, slab));
-        LZ_TRY(mm16(h, bi, alpha + j * bb, qb.P));
+        LZ_TRY(gram_finish<double>(h, 16, 1, 1, alpha + j * bb, slab, bi, qb.P));
         LZ_TRY(fused_update16(h, n, out, in, qb.P, &P));
         if (j + 1 < m) {
             LZ_TRY(gram_finish<double>(h, 16, P, 0, slab));
             LZ_TRY(allreduce_bb(h, slab));
-            LZ_TRY(sqrtm_pair<double>(h, 16, nullptr, 1, beta + (j + 1) * bb, qb.binv[(j + 1) & 1], nullptr, slab));
+            LZ_TRY(sqrtm_pair<double>(h, 16, nullptr, 1, beta + (j + 1) * bb, qb.binv[(j + 1) & 1], nullptr, slab,
+                                      bi, qb.P));
             LZ_TRY(halo_exchange16(h, hp, out));
         }
     }

@@ -142,9 +142,11 @@ __device__ void reduce_slabs(const double *__restrict__ part, int P, int bb, dou
 
 template <typename T>
 __global__ __launch_bounds__(kRedThreads) void k_gram_finish(int b, const double *__restrict__ part,
-                                                             int P, int mode, T *__restrict__ R)
+                                                             int P, int mode, T *__restrict__ R,
+                                                             const T *__restrict__ L, T *__restrict__ LR)
 {
     __shared__ double g[kMaxB * kMaxB];
+    __shared__ double r[kMaxB * kMaxB];
     __shared__ double scratch[kRedThreads];
     const int bb = b * b;
     reduce_slabs(part, P, bb, g, scratch);
@@ -152,6 +154,16 @@ __global__ __launch_bounds__(kRedThreads) void k_gram_finish(int b, const double
         const int i = e / b, j = e % b;
         const double v = mode ? 0.5 * (g[i * b + j] + g[j * b + i]) : g[e];
         R[e] = (T)v;
+        r[e] = (double)(T)v;
+    }
+    if (L) {  // LR = L * R (the Q-free iteration's P2 = beta_j^-1 alpha_j)
+        __syncthreads();
+        for (int e = threadIdx.x; e < bb; e += kRedThreads) {
+            const int i = e / b, j = e % b;
+            double s = 0.0;
+            for (int k = 0; k < b; ++k) s = fma((double)L[i * b + k], r[k * b + j], s);
+            LR[e] = (T)s;
+        }
     }
 }
 
@@ -196,12 +208,12 @@ int gram_partials(lz_handle *h, int64_t n, int b, const T *X, const T *Y, int64_
 }
 
 template <typename T>
-int gram_finish(lz_handle *h, int b, int nparts, int mode, T *R, const double *slabs)
+int gram_finish(lz_handle *h, int b, int nparts, int mode, T *R, const double *slabs, const T *L, T *LR)
 {
     {
     const int ev_ = prof_begin(h, PROF_SMALL);
     hipLaunchKernelGGL((k_gram_finish<T>), dim3(1), dim3(kRedThreads), 0, h->stream, b,
-                       slabs ? slabs : h->partials, nparts, mode, R);
+                       slabs ? slabs : h->partials, nparts, mode, R, L, LR);
     prof_end(h, ev_);
     }
     LZ_LAUNCH_CHECK();
@@ -372,7 +384,8 @@ template <typename T, int B>
 __global__ __launch_bounds__(kRedThreads) void k_sqrtm_b(const T *__restrict__ Gin,
                                                          const double *__restrict__ part, int P,
                                                          T *__restrict__ beta, T *__restrict__ binv,
-                                                         T *__restrict__ eig)
+                                                         T *__restrict__ eig, const T *__restrict__ L,
+                                                         T *__restrict__ LB)
 {
 #pragma clang fp contract(off)
     static_assert(B == 8 || B == 16 || B == 32, "B in {8, 16, 32}");
@@ -491,6 +504,18 @@ __global__ __launch_bounds__(kRedThreads) void k_sqrtm_b(const T *__restrict__ G
         }
         if (beta) beta[i * B + j] = (T)s1;
         if (binv) binv[i * B + j] = (T)s2;
+        if (L) g[i * B + j] = s1;  // g (the Gram) is dead: park beta for LB
+    }
+    if (L) {  // LB = L * beta (the Q-free iteration's P1 = beta_{j-1}^-1 beta_j)
+        wave_lds_sync();
+#pragma unroll 1
+        for (int k = 0; k < NE; ++k) {
+            const int i = r0 + RS * k;
+            double s = 0.0;
+#pragma unroll 4
+            for (int kk = 0; kk < B; ++kk) s = fma((double)L[i * B + kk], g[kk * B + j], s);
+            LB[i * B + j] = (T)s;
+        }
     }
     if (eig && tid < B) {
         const double lk = Am[tid * LD + tid];
@@ -505,16 +530,17 @@ __global__ __launch_bounds__(kRedThreads) void k_sqrtm_b(const T *__restrict__ G
 
 template <typename T>
 int sqrtm_pair(lz_handle *h, int b, const T *G, int nparts, T *beta, T *beta_inv, T *eig,
-               const double *slabs)
+               const double *slabs, const T *L, T *LB)
 {
     LZ_ARG_CHECK(b >= 1 && b <= 32, "sqrtm supports b <= 32");
+    LZ_ARG_CHECK(!L || b == 8 || b == 16 || b == 32, "sqrtm_pair L*beta: b in {8, 16, 32}");
     {
     const int ev_ = prof_begin(h, PROF_SMALL);
     const double *sl = slabs ? slabs : h->partials;
 #define LZ_SQRTM_B(BV)                                                                        \
     case BV:                                                                                  \
         hipLaunchKernelGGL((k_sqrtm_b<T, BV>), dim3(1), dim3(kRedThreads), 0, h->stream, G, sl, \
-                           nparts, beta, beta_inv, eig);                                      \
+                           nparts, beta, beta_inv, eig, L, LB);                               \
         break;
     switch (b) {
         LZ_SQRTM_B(8) LZ_SQRTM_B(16) LZ_SQRTM_B(32)
@@ -659,8 +685,8 @@ int copy_row(lz_handle *h, int b, const T *Q, int64_t ld, int col_major, int64_t
 #define LZ_DENSE_INST(T)                                                                       \
     template int gram_partials<T>(lz_handle *, int64_t, int, const T *, const T *, int64_t,    \
                                   int *);                                                      \
-    template int gram_finish<T>(lz_handle *, int, int, int, T *, const double *);              \
-    template int sqrtm_pair<T>(lz_handle *, int, const T *, int, T *, T *, T *, const double *);\
+    template int gram_finish<T>(lz_handle *, int, int, int, T *, const double *, const T *, T *); \
+    template int sqrtm_pair<T>(lz_handle *, int, const T *, int, T *, T *, T *, const double *, const T *, T *);\
     template int tsmm<T>(lz_handle *, int64_t, int, T, T, const T *, const T *, T *, int64_t); \
     template int copy_row<T>(lz_handle *, int, const T *, int64_t, int, int64_t, T *);
 LZ_DENSE_INST(double)

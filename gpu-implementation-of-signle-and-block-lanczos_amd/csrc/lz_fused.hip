@@ -1633,7 +1633,9 @@ int fused_spmm16(lz_handle *h, int64_t n, const int64_t *rp, const int32_t *col,
         LZ_LAUNCH_CHECK();
         return fold_slabs(h, h->partials, (int64_t)grid * 8, 256, nparts);
     }
-    if (buf && variant && variant[0] == 'r') {  // pipelined consumers, two parallel loaders
+    // default: k_fused_pp16 (pipelined consumers, two parallel loaders): 1.65 ms
+    // against 1.73-1.76 for k_fused_ws16 (LZ_FUSED_KERNEL=ws) in the Q-free iteration
+    if (buf && (!variant || variant[0] == 'r')) {
         constexpr int NCR = 14;
         const int grid = (int)std::max<int64_t>(1, std::min<int64_t>(ceil_div(n, (int64_t)16 * NCR), h->n_cu));
         LZ_TRY(ensure_partials(h, (size_t)grid * NCR * 256));
@@ -1645,9 +1647,9 @@ int fused_spmm16(lz_handle *h, int64_t n, const int64_t *rp, const int32_t *col,
         return fold_slabs(h, h->partials, (int64_t)grid * NCR, 256, nparts);
     }
     if (buf && !(variant && variant[0] == 't')) {
-        // default: one loader, CSR-only stages (3), Q_{j-1} rows loaded by the
-        // consumers; LZ_FUSED_KERNEL=wsq: Q_{j-1} strips in the stage (2 stages);
-        // LZ_FUSED_KERNEL=nl2: two loaders staging alternate tiles, 14 consumers
+        // LZ_FUSED_KERNEL=ws: one loader, CSR-only stages (3), W_{j-1} rows loaded by
+        // the consumers; =wsq: W_{j-1} strips in the stage (2 stages);
+        // =nl2: two loaders staging alternate tiles, 14 consumers
         const bool wsq = variant && variant[0] == 'w' && variant[2] == 'q';
         const bool nl2 = variant && variant[0] == 'n';
         const int nc = nl2 ? 14 : 15;

@@ -20,14 +20,17 @@ int spmv(lz_handle *h, int64_t n, const int64_t *rp, const int32_t *col, const T
 // returns the number of slabs in *nparts.
 template <typename T>
 int gram_partials(lz_handle *h, int64_t n, int b, const T *X, const T *Y, int64_t ld, int *nparts);
-// reduce nparts slabs (fixed order); mode 0: R = sum, mode 1: R = 0.5 (S + S^T)
+// reduce nparts slabs (fixed order); mode 0: R = sum, mode 1: R = 0.5 (S + S^T);
+// L != null: also LR = L * R (b x b)
 template <typename T>
-int gram_finish(lz_handle *h, int b, int nparts, int mode, T *R, const double *slabs = nullptr);
+int gram_finish(lz_handle *h, int b, int nparts, int mode, T *R, const double *slabs = nullptr,
+                const T *L = nullptr, T *LR = nullptr);
 // symmetric square root pair of G (device double b x b) or, when nparts > 0,
-// of the sum of the nparts slabs in h->partials.
+// of the sum of the nparts slabs in h->partials.  L != null (b in {8,16,32}):
+// also LB = L * beta.
 template <typename T>
 int sqrtm_pair(lz_handle *h, int b, const T *G, int nparts, T *beta, T *beta_inv, T *eig,
-               const double *slabs = nullptr);
+               const double *slabs = nullptr, const T *L = nullptr, T *LB = nullptr);
 // W = sw*W + sq*Q*S
 template <typename T>
 int tsmm(lz_handle *h, int64_t n, int b, T sw, T sq, const T *Q, const T *S, T *W, int64_t ld);

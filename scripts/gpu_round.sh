@@ -19,6 +19,6 @@ timeout -k 10 300 rocprofv3 --pmc FETCH_SIZE --output-format csv -d $O/fetch -o 
 timeout -k 10 300 rocprofv3 --pmc WRITE_SIZE --output-format csv -d $O/write -o p -- python3 $ROOT/bench.py --no-cpu-baseline --steps 5 --warmup 1 --spmm-reps 2 > $O/write.log 2>&1 || exit $?
 cd $ROOT
 NNZ=$(python -c "import json;print(json.load(open('$O/bench.json'))['config']['nnz_per_gpu'])")
-python scripts/pmc_traffic.py $O/fetch $O/write k_fused_ws16 10000000 $NNZ 4096 $O/pmc_k_fused_ws16.json
+python scripts/pmc_traffic.py $O/fetch $O/write k_fused_pp16 10000000 $NNZ 4096 $O/pmc_k_fused_pp16.json
 python scripts/pmc_traffic.py $O/fetch $O/write k_spmm_seg 10000000 $NNZ 4096 $O/pmc_k_spmm_seg.json
 python scripts/pmc_traffic.py $O/fetch $O/write k_fused_update16 10000000 $NNZ 4096 $O/pmc_k_fused_update16.json
