@@ -333,14 +333,14 @@ static int fold_slabs(lz_handle *h, const double *part, int64_t P, int bb, int *
     return LZ_OK;
 }
 
-template <bool REV>
-__global__ __launch_bounds__(512) void k_fused_update16(int64_t n, double *__restrict__ Wn,
+template <bool REV, int NW = 8>
+__global__ __launch_bounds__(64 * NW) void k_fused_update16(int64_t n, double *__restrict__ Wn,
                                                         const double *__restrict__ Q,
                                                         const double *__restrict__ alpha,
                                                         double *__restrict__ part)
 {
-    __shared__ double tile[8][16 * 17];
-    __shared__ double red[8][256];
+    __shared__ double tile[NW][16 * 17];
+    __shared__ double red[NW][256];
     const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
     double *T = tile[w];
     double na_op[4];
@@ -348,13 +348,13 @@ __global__ __launch_bounds__(512) void k_fused_update16(int64_t n, double *__res
     for (int kc = 0; kc < 4; ++kc) na_op[kc] = -alpha[(4 * kc + (lane >> 4)) * 16 + (lane & 15)];
     d4_t gacc = {0.0, 0.0, 0.0, 0.0};
     const int64_t ntile = ceil_div(n, 16);
-    XcdSched s(ceil_div(ntile, 8));
+    XcdSched s(ceil_div(ntile, NW));
     // REV: walk this block's units last-first.  Pass 1 writes Q_j and W' first
     // row to last, so the rows it wrote last are still in the MALL (256 MB)
     // when a reversed pass 2 starts; pass 2's last-written W'' rows (the first
     // rows) are in turn the first the next pass 1 gathers.
     const int64_t cnt = s.begin < s.end ? (s.end - s.begin + s.step - 1) / s.step : 0;
-    auto row0 = [&](int64_t k) { return (s.begin + (REV ? cnt - 1 - k : k) * s.step) * 128 + 16 * w; };
+    auto row0 = [&](int64_t k) { return (s.begin + (REV ? cnt - 1 - k : k) * s.step) * (16 * NW) + 16 * w; };
     // one tile ahead in registers: the W' (accumulator layout) and Q rows of
     // tile k+1 are in flight while tile k is computed (vmcnt is in order, so
     // tile k's wait does not cover them)
@@ -389,7 +389,16 @@ __global__ __launch_bounds__(512) void k_fused_update16(int64_t n, double *__res
 #pragma unroll
         for (int r = 0; r < 4; ++r) gacc = mfma16(acc[r], acc[r], gacc);
     }
-    wg_slab(red, gacc, lane, w, part);
+    // the waves' accumulators summed in wave order into the block's slab
+#pragma unroll
+    for (int r = 0; r < 4; ++r) red[w][((lane >> 4) + 4 * r) * 16 + (lane & 15)] = gacc[r];
+    __syncthreads();
+    if (threadIdx.x < 256) {
+        double sum = 0.0;
+#pragma unroll
+        for (int ww = 0; ww < NW; ++ww) sum += red[ww][threadIdx.x];
+        part[(int64_t)blockIdx.x * 256 + threadIdx.x] = sum;
+    }
 }
 
 // ---------------------------------------------------------------------------
@@ -1686,16 +1695,33 @@ int fused_spmm16(lz_handle *h, int64_t n, const int64_t *rp, const int32_t *col,
 int fused_update16(lz_handle *h, int64_t n, double *Wn, const double *Q, const double *alpha,
                    int *nparts)
 {
-    const int64_t units = ceil_div(ceil_div(n, 16), 8);
-    const int grid = (int)std::max<int64_t>(1, std::min<int64_t>(units, h->n_cu * 2));
+    // one block per CU (256 slabs for the sqrtm to reduce); LZ_UPDATE_BPC /
+    // LZ_UPDATE_NW (8 or 16 waves per block) for A/B.  Measured (C3): 1 block
+    // of 8 waves 0.723 ms, 2 blocks 0.740, 3 0.758, 4 0.738
+    static const char *gm = getenv("LZ_UPDATE_BPC");
+    static const char *nw_env = getenv("LZ_UPDATE_NW");
+    const int bpc = gm ? std::max(1, atoi(gm)) : 1;
+    const int nw = (nw_env && atoi(nw_env) == 16) ? 16 : 8;
+    const int64_t units = ceil_div(ceil_div(n, 16), nw);
+    const int grid = (int)std::max<int64_t>(1, std::min<int64_t>(units, (int64_t)h->n_cu * bpc));
+    LZ_TRY(ensure_partials(h, (size_t)grid * 256));
     static const char *order = getenv("LZ_UPDATE_ORDER");  // "f": forward (A/B)
+    const bool fwd = order && order[0] == 'f';
     const int ev = prof_begin(h, PROF_UPDATE_PASS);
-    if (order && order[0] == 'f')
-        hipLaunchKernelGGL(k_fused_update16<false>, dim3(grid), dim3(512), 0, h->stream, n, Wn, Q, alpha,
+    if (nw == 16) {
+        if (fwd)
+            hipLaunchKernelGGL((k_fused_update16<false, 16>), dim3(grid), dim3(1024), 0, h->stream, n, Wn, Q, alpha,
+                               h->partials);
+        else
+            hipLaunchKernelGGL((k_fused_update16<true, 16>), dim3(grid), dim3(1024), 0, h->stream, n, Wn, Q, alpha,
+                               h->partials);
+    } else if (fwd) {
+        hipLaunchKernelGGL((k_fused_update16<false, 8>), dim3(grid), dim3(512), 0, h->stream, n, Wn, Q, alpha,
                            h->partials);
-    else
-        hipLaunchKernelGGL(k_fused_update16<true>, dim3(grid), dim3(512), 0, h->stream, n, Wn, Q, alpha,
+    } else {
+        hipLaunchKernelGGL((k_fused_update16<true, 8>), dim3(grid), dim3(512), 0, h->stream, n, Wn, Q, alpha,
                            h->partials);
+    }
     prof_end(h, ev);
     LZ_LAUNCH_CHECK();
     *nparts = grid;
