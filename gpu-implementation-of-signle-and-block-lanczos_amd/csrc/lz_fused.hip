@@ -767,9 +767,14 @@ __global__ __launch_bounds__(64 * (NC + NL)) void k_fused_pp16(
         ready[threadIdx.x] = -1;
         done[threadIdx.x] = 0;
     }
+    // B operands in a permuted contraction order: MFMA step kc, lane l contracts
+    // over k = 4 (l >> 4) + kc (not 4 kc + (l >> 4)), so every A operand a lane
+    // needs is 4 contiguous doubles of one row -- two 16-B loads instead of
+    // four 8-B loads for the W row tiles (C = M B is unchanged: the same k
+    // permutation on both operands)
     for (int e = threadIdx.x; e < 256; e += blockDim.x) {
         const int kc = e >> 6, l = e & 63;
-        const int idx = (4 * kc + (l >> 4)) * 16 + (l & 15);
+        const int idx = (4 * (l >> 4) + kc) * 16 + (l & 15);
         ops[0][e] = binv[idx];
         ops[1][e] = has_prev ? -beta[idx] : 0.0;
     }
@@ -840,19 +845,20 @@ __global__ __launch_bounds__(64 * (NC + NL)) void k_fused_pp16(
         __builtin_amdgcn_make_buffer_rsrc(const_cast<double *>(Wg), (short)0, (int)(nx * 128), 0x00020000);
     double *S0 = scr[cw];
     d4_t macc = {0.0, 0.0, 0.0, 0.0};
-    // the pending strip's W and Q_{j-1} rows, loaded straight into MFMA
-    // A-operand order (a[kc] = M[l & 15][4 kc + (l >> 4)]: four 8-B loads per
-    // lane, 512 B per instruction), so the epilogue needs no LDS transpose for them
+    // the pending strip's W_j and W_{j-1} rows, loaded straight into MFMA
+    // A-operand order (permuted contraction, see ops: two 16-B loads per lane),
+    // so the epilogue needs no LDS transpose for them
     double wa[4] = {0.0, 0.0, 0.0, 0.0}, qa[4] = {0.0, 0.0, 0.0, 0.0};
     auto aop_load = [&](const double *src, int64_t s0, double a[4]) {
         const int rows = (int)(n - s0 < 16 ? (n - s0 > 0 ? n - s0 : 0) : 16);  // strips past n: none
         const auto r = __builtin_amdgcn_make_buffer_rsrc(const_cast<double *>(src + (s0 < n ? s0 : 0) * 16), (short)0,
                                                          rows * 128, 0x00020000);
+        // a[kc] = M[l & 15][4 (l >> 4) + kc]: 32 contiguous bytes per lane
 #pragma unroll
-        for (int kc = 0; kc < 4; ++kc) {
-            const auto u = __builtin_amdgcn_raw_buffer_load_b64(
-                r, (uint32_t)((lane & 15) * 128 + (4 * kc + (lane >> 4)) * 8), 0, 0);
-            __builtin_memcpy(&a[kc], &u, 8);
+        for (int hh = 0; hh < 2; ++hh) {
+            const auto u = __builtin_amdgcn_raw_buffer_load_b128(
+                r, (uint32_t)((lane & 15) * 128 + (lane >> 4) * 32 + hh * 16), 0, 0);
+            __builtin_memcpy(&a[2 * hh], &u, 16);
         }
     };
     int64_t s0p = -1;  // strip whose epilogue is pending
@@ -867,7 +873,7 @@ __global__ __launch_bounds__(64 * (NC + NL)) void k_fused_pp16(
         const int ar = lane & 15;
         double ya[4];
 #pragma unroll
-        for (int kc = 0; kc < 4; ++kc) ya[kc] = S0[fw_sw(ar, 4 * kc + (lane >> 4))];
+        for (int kc = 0; kc < 4; ++kc) ya[kc] = S0[fw_sw(ar, 4 * (lane >> 4) + kc)];
         d4_t q1 = {0.0, 0.0, 0.0, 0.0}, wn = {0.0, 0.0, 0.0, 0.0};
 #pragma unroll
         for (int kc = 0; kc < 4; ++kc) q1 = mfma16(wa[kc], ops[0][64 * kc + lane], q1);
