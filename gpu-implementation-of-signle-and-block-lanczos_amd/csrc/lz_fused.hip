@@ -339,13 +339,14 @@ __global__ __launch_bounds__(64 * NW) void k_fused_update16(int64_t n, double *_
                                                         const double *__restrict__ alpha,
                                                         double *__restrict__ part)
 {
-    __shared__ double tile[NW][16 * 17];
     __shared__ double red[NW][256];
     const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
-    double *T = tile[w];
+    // permuted contraction order (as k_fused_pp16): step kc, lane l contracts
+    // over k = 4 (l >> 4) + kc, so a lane's A operands are 32 contiguous bytes
+    // of one W_j row -- two 16-B loads, no LDS transpose
     double na_op[4];
 #pragma unroll
-    for (int kc = 0; kc < 4; ++kc) na_op[kc] = -alpha[(4 * kc + (lane >> 4)) * 16 + (lane & 15)];
+    for (int kc = 0; kc < 4; ++kc) na_op[kc] = -alpha[(4 * (lane >> 4) + kc) * 16 + (lane & 15)];
     d4_t gacc = {0.0, 0.0, 0.0, 0.0};
     const int64_t ntile = ceil_div(n, 16);
     XcdSched s(ceil_div(ntile, NW));
@@ -365,8 +366,13 @@ __global__ __launch_bounds__(64 * NW) void k_fused_update16(int64_t n, double *_
             const int64_t row = r0 + (lane >> 4) + 4 * r;
             a[r] = (k < cnt && row < n) ? Wn[r0 * 16 + 64 * r + lane] : 0.0;
         }
-        if (k < cnt) tile_load(Q, r0, n, lane, qv);
-        else qv[0] = qv[1] = qv[2] = qv[3] = 0.0;
+        qv[0] = qv[1] = qv[2] = qv[3] = 0.0;
+        const int64_t row = r0 + (lane & 15);
+        if (k < cnt && row < n) {  // qv[kc] = W_j[r0 + (l & 15)][4 (l >> 4) + kc]
+            const double2 *p2 = reinterpret_cast<const double2 *>(Q + row * 16 + 4 * (lane >> 4));
+            const double2 x = p2[0], y = p2[1];
+            qv[0] = x.x; qv[1] = x.y; qv[2] = y.x; qv[3] = y.y;
+        }
     };
     d4_t acc_n;
     double qv_n[4];
@@ -377,10 +383,8 @@ __global__ __launch_bounds__(64 * NW) void k_fused_update16(int64_t n, double *_
         double qv[4] = {qv_n[0], qv_n[1], qv_n[2], qv_n[3]};
         fetch(k + 1, acc_n, qv_n);
         if (r0 >= n) continue;
-        double qa[4];
-        tile_regs_to_aop(T, qv, lane, qa);
 #pragma unroll
-        for (int kc = 0; kc < 4; ++kc) acc = mfma16(qa[kc], na_op[kc], acc);
+        for (int kc = 0; kc < 4; ++kc) acc = mfma16(qv[kc], na_op[kc], acc);
 #pragma unroll
         for (int r = 0; r < 4; ++r) {
             const int64_t row = r0 + (lane >> 4) + 4 * r;
