@@ -135,13 +135,16 @@ static int block_lanczos_fused16(lz_handle *h, int64_t n, const int64_t *rp, con
     (void)Q0;
     QfreeBufs qb(h);
     int P = 0;
+    const uint64_t *pairs = nullptr;
+    LZ_TRY(strip_pairs(h, n, rp, &pairs));
     LZ_TRY(gram_partials<double>(h, n, 16, B, B, 16, &P));
     LZ_TRY(sqrtm_pair<double>(h, 16, nullptr, P, beta, qb.binv[0], nullptr));
     const double *in = B, *prev = nullptr;
     for (int j = 0; j < m; ++j) {
         double *out = j == 0 ? W : j == 1 ? Q1 : const_cast<double *>(prev);
         const double *bi = qb.binv[j & 1];
-        LZ_TRY(fused_spmm16(h, n, rp, col, val, in, n, in, prev, out, bi, j ? qb.P : nullptr, lc, q + j * 16, &P));
+        LZ_TRY(fused_spmm16(h, n, rp, col, val, in, n, in, prev, out, bi, j ? qb.P : nullptr, lc, q + j * 16, &P,
+                            pairs));
         // alpha_j and P2 = beta_j^-1 alpha_j in one kernel (P1 of this step is consumed)
         LZ_TRY(gram_finish<double>(h, 16, P, 1, alpha + j * bb, h->partials2, bi, qb.P));
         LZ_TRY(fused_update16(h, n, out, in, qb.P, &P));
@@ -199,6 +202,8 @@ static int block_lanczos_dist16(lz_handle *h, int64_t n_local, int64_t n_pad, co
     double *slab = h->scratch;  // one reduced b x b slab, all-reduced in place
     const double *own = X + (int64_t)h->rank * n_pad * 16;
     int P = 0;
+    const uint64_t *pairs = nullptr;
+    LZ_TRY(strip_pairs(h, n_local, rp, &pairs));
     // beta_0 from the global Gram of B
     LZ_TRY(gram_partials<double>(h, n_local, 16, B, B, 16, &P));
     LZ_TRY(gram_finish<double>(h, 16, P, 0, slab));
@@ -210,7 +215,7 @@ static int block_lanczos_dist16(lz_handle *h, int64_t n_local, int64_t n_pad, co
         double *out = j == 0 ? W : j == 1 ? Q0 : const_cast<double *>(prev);
         const double *bi = qb.binv[j & 1];
         LZ_TRY(fused_spmm16(h, n_local, rp, col, val, X, n_pad * h->nranks, own, prev, out, bi,
-                            j ? qb.P : nullptr, lc_local, q + j * 16, &P));
+                            j ? qb.P : nullptr, lc_local, q + j * 16, &P, pairs));
         LZ_TRY(gram_finish<double>(h, 16, P, 0, slab, h->partials2));
         LZ_NCCL_TRY(ncclAllReduce(slab, slab, bb, ncclDouble, ncclSum, comm, h->stream));
         LZ_TRY(gram_finish<double>(h, 16, 1, 1, alpha + j * bb, slab, bi, qb.P));
@@ -317,6 +322,8 @@ static int block_lanczos_halo16(lz_handle *h, const HaloPlan &hp, const int64_t 
     QfreeBufs qb(h);
     double *slab = h->scratch;
     int P = 0;
+    const uint64_t *pairs = nullptr;
+    LZ_TRY(strip_pairs(h, n, rp, &pairs));
     LZ_TRY(gram_partials<double>(h, n, 16, B, B, 16, &P));
     LZ_TRY(gram_finish<double>(h, 16, P, 0, slab));
     LZ_TRY(allreduce_bb(h, slab));
@@ -328,7 +335,7 @@ static int block_lanczos_halo16(lz_handle *h, const HaloPlan &hp, const int64_t 
         double *in = xs[j & 1], *out = xs[(j + 1) & 1];
         const double *bi = qb.binv[j & 1];
         LZ_TRY(fused_spmm16(h, n, rp, col, val, in, nx, in, j ? out : nullptr, out, bi, j ? qb.P : nullptr,
-                            lc_local, q + j * 16, &P));
+                            lc_local, q + j * 16, &P, pairs));
         LZ_TRY(gram_finish<double>(h, 16, P, 0, slab, h->partials2));
         LZ_TRY(allreduce_bb(h, slab));
         LZ_TRY(gram_finish<double>(h, 16, 1, 1, alpha + j * bb, slab, bi, qb.P));
@@ -407,6 +414,7 @@ int lz_finalize(lz_handle *h)
     if (!h) return LZ_OK;
     (void)hipSetDevice(h->device);
     halo_free(h);
+    (void)hipFree(h->pairs);
     if (h->comm) ncclCommDestroy(comm_of(h));
     if (h->ev_pool) {
         for (int i = 0; i < h->ev_cap; ++i) (void)hipEventDestroy(h->ev_pool[i]);

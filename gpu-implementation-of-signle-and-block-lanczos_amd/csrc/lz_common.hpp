@@ -70,6 +70,8 @@ struct lz_handle {
     void *comm = nullptr;         // ncclComm_t when lz_comm_init was called
     int nranks = 1, rank = 0;
     void *halo = nullptr;         // lz::HaloPlan when lz_halo_init was called
+    uint64_t *pairs = nullptr;    // per-16-row-strip row order by length (k_strip_pairs)
+    size_t pairs_cap = 0;         // entries
     // optional per-kernel-class timing with hipEvents on the handle's stream
     // (lz_prof_enable / lz_prof_read): events recorded around each launch of
     // the class, elapsed times summed at read time.

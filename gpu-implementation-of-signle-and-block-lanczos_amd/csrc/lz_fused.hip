@@ -426,7 +426,7 @@ __global__ __launch_bounds__(64 * NW) void k_fused_update16(int64_t n, double *_
 //   NL > 1: NL loader waves stage alternate tiles, each publishing its tile as
 //     soon as it lands.
 // Rows past n are out of range for the DMA and land as zeros.
-template <int NC, int CAP, bool QREG = false>
+template <int NC, int CAP, bool QREG = false, bool PR = false>
 struct FwCfg {
     static constexpr int TR = 16 * NC;
     static constexpr int RP_PIECES = (TR + 2) * 8 / 16;
@@ -440,8 +440,62 @@ struct FwCfg {
         int32_t col[ws_instr(COL_PIECES) * 256];
         double val[ws_instr(VAL_PIECES) * 128];
         double qt[QREG ? 2 : TR * 16];  // Q_{j-1} rows, per strip in slot order; then scratch
+        uint64_t pr[PR ? 128 : 1];        // PR: the tile's strips' row orders (k_strip_pairs)
     };
+    static constexpr int PR_PIECES = NC * 8 / 16 > 0 ? (NC * 8 + 15) / 16 : 1;
 };
+
+// Per 16-row strip: the strip's rows sorted by length (ties by row), packed
+// as 16 nibbles (nibble i = row of rank i; rows past n have length 0).
+// Computed once per solve; k_fused_pp16 pairs rank g with rank 15 - g so each
+// lane group's two-row list is a long row plus a short one.  (C3 rows: 10 +-
+// 2.2 nnz; a wave steps as long as its longest list: 3.48 steps per strip for
+// the rows (g, g+8), 3.03 for the ranked pairs, 3.00 ideal.)
+__global__ __launch_bounds__(256) void k_strip_pairs(int64_t n, const int64_t *__restrict__ rp,
+                                                     uint64_t *__restrict__ out)
+{
+    const int64_t ns = (n + 15) / 16;
+    for (int64_t st = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; st < ns;
+         st += (int64_t)gridDim.x * blockDim.x) {
+        uint32_t key[16];
+        const int64_t r0 = st * 16;
+#pragma unroll
+        for (int i = 0; i < 16; ++i) {
+            const int64_t r = r0 + i;
+            const int64_t len = r < n ? rp[r + 1] - rp[r] : 0;
+            key[i] = ((uint32_t)(len < (1 << 27) ? len : (1 << 27)) << 4) | (uint32_t)i;
+        }
+#pragma unroll
+        for (int i = 1; i < 16; ++i)  // insertion sort, ascending
+#pragma unroll
+            for (int j = i; j > 0; --j) {
+                const uint32_t a = key[j - 1], b = key[j];
+                key[j - 1] = a < b ? a : b;
+                key[j] = a < b ? b : a;
+            }
+        uint64_t w = 0;
+#pragma unroll
+        for (int i = 0; i < 16; ++i) w |= (uint64_t)(key[i] & 15) << (4 * i);
+        out[st] = w;
+    }
+}
+
+int strip_pairs(lz_handle *h, int64_t n, const int64_t *rp, const uint64_t **out)
+{
+    const int64_t ns = ceil_div(n, (int64_t)16);
+    if ((size_t)ns > h->pairs_cap) {
+        LZ_HIP_TRY(hipStreamSynchronize(h->stream));
+        (void)hipFree(h->pairs);
+        h->pairs = nullptr;
+        LZ_HIP_TRY(hipMalloc(&h->pairs, sizeof(uint64_t) * (size_t)ns));
+        h->pairs_cap = (size_t)ns;
+    }
+    const int grid = (int)std::max<int64_t>(1, std::min<int64_t>(ceil_div(ns, (int64_t)256), (int64_t)h->n_cu * 4));
+    hipLaunchKernelGGL(k_strip_pairs, dim3(grid), dim3(256), 0, h->stream, n, rp, h->pairs);
+    LZ_LAUNCH_CHECK();
+    *out = h->pairs;
+    return LZ_OK;
+}
 
 // DMA NC 16-row strips of a row-major n x 16 block (buffer `r` based at the
 // tile's first row) into dst in slot order: strip j, slot c4*16 + r holds row
@@ -746,15 +800,16 @@ __global__ __launch_bounds__(64 * (NC + NL)) void k_fused_ws16(
 //   of strip i-1 (its Y tile parked in LDS, its W / Q_{j-1} rows loaded into
 //   registers after strip i-1's gather), so the epilogue hides the first
 //   gather round trip;
-template <int NC, int CAP, int K, int NL>
+template <int NC, int CAP, int K, int NL, bool BP = false>
 __global__ __launch_bounds__(64 * (NC + NL)) void k_fused_pp16(
     int64_t n, const int64_t *__restrict__ rp, const int32_t *__restrict__ col,
     const double *__restrict__ val, const double *__restrict__ Wg, int64_t nx,
     const double *__restrict__ Wown, const double *Qbuf, double *Wn,
     const double *__restrict__ binv, const double *__restrict__ beta, int64_t lc,
-    double *__restrict__ qrow, double *__restrict__ part, int *__restrict__ err)
+    double *__restrict__ qrow, double *__restrict__ part, int *__restrict__ err,
+    const uint64_t *__restrict__ pairs)
 {
-    using C = FwCfg<NC, CAP, true>;
+    using C = FwCfg<NC, CAP, true, BP>;
     constexpr int TR = C::TR;
 #ifdef LZ_WS_PROBE
     const int dbg = lz_ws_dbg;  // timing masks: bit 0 skips the Q_{j-1} loads, bit 1 the W loads
@@ -825,6 +880,12 @@ __global__ __launch_bounds__(64 * (NC + NL)) void k_fused_pp16(
             ws_dma(rr, st[s].rp, C::RP_PIECES, lane);
             ws_dma(cr, st[s].col, C::COL_PIECES, lane);
             ws_dma(vr, st[s].val, C::VAL_PIECES, lane);
+            if constexpr (BP) {  // the tile's strips' row orders (past the last strip: zeros)
+                const int64_t s0i = r0 / 16, ns = (n + 15) / 16;
+                const auto pr = __builtin_amdgcn_make_buffer_rsrc(const_cast<uint64_t *>(pairs + s0i), (short)0,
+                                                                  (int)((ns - s0i) * 8), 0x00020000);
+                ws_dma(pr, st[s].pr, C::PR_PIECES, lane);
+            }
             asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
             if (lane == 0) ws_lds_write(ws_lds_addr(&ready[s]), (int)i);
             WS_TL(i, 1);
@@ -916,11 +977,20 @@ __global__ __launch_bounds__(64 * (NC + NL)) void k_fused_pp16(
         const int co = (int)(kA & 3), vo = (int)(kA & 1);
         const int nrow = (int)(n - r0 < TR ? n - r0 : TR);
         const int runlen = (int)(S.rp[nrow] - kA);
-        const int lr = 16 * cw + g;
-        const int o0 = lr < nrow ? (int)(S.rp[lr] - kA) : 0;
-        const int len0 = lr < nrow ? (int)(S.rp[lr + 1] - kA) - o0 : 0;
-        const int o1 = lr + 8 < nrow ? (int)(S.rp[lr + 8] - kA) : 0;
-        const int len1 = lr + 8 < nrow ? (int)(S.rp[lr + 9] - kA) - o1 : 0;
+        // the group's two rows of the strip: g and g + 8, or (BP) the rows of
+        // length rank g and 15 - g (a long row plus a short one: a wave steps
+        // as long as its longest list)
+        int ra = g, rb = g + 8;
+        if constexpr (BP) {
+            const uint64_t pw = S.pr[cw];
+            ra = (int)(pw >> (4 * g)) & 15;
+            rb = (int)(pw >> (4 * (15 - g))) & 15;
+        }
+        const int lra = 16 * cw + ra, lrb = 16 * cw + rb;
+        const int o0 = lra < nrow ? (int)(S.rp[lra] - kA) : 0;
+        const int len0 = lra < nrow ? (int)(S.rp[lra + 1] - kA) - o0 : 0;
+        const int o1 = lrb < nrow ? (int)(S.rp[lrb] - kA) : 0;
+        const int len1 = lrb < nrow ? (int)(S.rp[lrb + 1] - kA) - o1 : 0;
         const int cnt = len0 + len1;
         double y[4] = {0.0, 0.0, 0.0, 0.0};
         if (runlen <= CAP) {  // tile-uniform
@@ -980,10 +1050,10 @@ __global__ __launch_bounds__(64 * (NC + NL)) void k_fused_pp16(
         if (lane == 0) atomicAdd(&done[s], 1);
         // park Y (swizzled) and fetch this strip's W and Q_{j-1} rows for its
         // epilogue, which runs behind the next strip's first gather step
-        S0[fw_sw(g, 2 * p)] = y[0];
-        S0[fw_sw(g, 2 * p + 1)] = y[1];
-        S0[fw_sw(g + 8, 2 * p)] = y[2];
-        S0[fw_sw(g + 8, 2 * p + 1)] = y[3];
+        S0[fw_sw(ra, 2 * p)] = y[0];
+        S0[fw_sw(ra, 2 * p + 1)] = y[1];
+        S0[fw_sw(rb, 2 * p)] = y[2];
+        S0[fw_sw(rb, 2 * p + 1)] = y[3];
         if (!(dbg & 2)) aop_load(Wown, s0, wa);
         if (has_prev && !(dbg & 1)) aop_load(Qbuf, s0, qa);
         s0p = s0;
@@ -1615,7 +1685,8 @@ int mm16(lz_handle *h, const double *A, const double *B, double *C)
 // it is written by the same wave), beta: P1 = beta_{j-1}^-1 beta_j (or null at j = 0)
 int fused_spmm16(lz_handle *h, int64_t n, const int64_t *rp, const int32_t *col, const double *val,
                  const double *Wg, int64_t nx, const double *Wown, const double *Qbuf, double *Wn,
-                 const double *binv, const double *beta, int64_t lc, double *qrow, int *nparts)
+                 const double *binv, const double *beta, int64_t lc, double *qrow, int *nparts,
+                 const uint64_t *pairs)
 {
     const int64_t tiles = ceil_div(n, kFusedRows);
     LZ_ARG_CHECK(tiles >= 1 && tiles < (1LL << 31), "tile count");
@@ -1659,8 +1730,14 @@ int fused_spmm16(lz_handle *h, int64_t n, const int64_t *rp, const int32_t *col,
         const int grid = (int)std::max<int64_t>(1, std::min<int64_t>(ceil_div(n, (int64_t)16 * NCR), h->n_cu));
         LZ_TRY(ensure_partials(h, (size_t)grid * NCR * 256));
         const int ev = prof_begin(h, PROF_SPMM_PASS);
-        hipLaunchKernelGGL((k_fused_pp16<NCR, 2376, 3, 2>), dim3(grid), dim3(64 * 16), 0, h->stream, n, rp, col,
-                           val, Wg, nx, Wown, Qbuf, Wn, binv, beta, lc, qrow, h->partials, h->err_flag);
+        if (pairs && !(variant && variant[1] == 'p'))  // LZ_FUSED_KERNEL=rp: rows (g, g+8)
+            hipLaunchKernelGGL((k_fused_pp16<NCR, 2376, 3, 2, true>), dim3(grid), dim3(64 * 16), 0, h->stream, n, rp,
+                               col, val, Wg, nx, Wown, Qbuf, Wn, binv, beta, lc, qrow, h->partials, h->err_flag,
+                               pairs);
+        else
+            hipLaunchKernelGGL((k_fused_pp16<NCR, 2376, 3, 2>), dim3(grid), dim3(64 * 16), 0, h->stream, n, rp, col,
+                               val, Wg, nx, Wown, Qbuf, Wn, binv, beta, lc, qrow, h->partials, h->err_flag,
+                               nullptr);
         prof_end(h, ev);
         LZ_LAUNCH_CHECK();
         return fold_slabs(h, h->partials, (int64_t)grid * NCR, 256, nparts);

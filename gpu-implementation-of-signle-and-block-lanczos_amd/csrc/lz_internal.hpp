@@ -46,7 +46,10 @@ int copy_row(lz_handle *h, int b, const T *Q, int64_t ld, int col_major, int64_t
 // this rank owns (== Wg single-GPU).  Wprev may be the Wn buffer (in place).
 int fused_spmm16(lz_handle *h, int64_t n, const int64_t *rp, const int32_t *col,
                  const double *val, const double *Wg, int64_t nx, const double *Wown, const double *Wprev,
-                 double *Wn, const double *binv, const double *P1, int64_t lc, double *qrow, int *nparts);
+                 double *Wn, const double *binv, const double *P1, int64_t lc, double *qrow, int *nparts,
+                 const uint64_t *pairs = nullptr);
+// per-16-row-strip row order by length for fused_spmm16's `pairs` (once per solve)
+int strip_pairs(lz_handle *h, int64_t n, const int64_t *rp, const uint64_t **out);
 // Pass 2: Wn <- Wn - Wcur*P2 (P2 = beta_j^-1 alpha_j, so Wcur*P2 = Q_j alpha_j);
 // slabs of Wn^T Wn.
 int fused_update16(lz_handle *h, int64_t n, double *Wn, const double *Wcur, const double *P2,
