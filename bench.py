@@ -101,6 +101,7 @@ def main():
     ap.add_argument("--cpu-iters", type=int, default=3)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--spmm-reps", type=int, default=20)
+    ap.add_argument("--c2-steps", type=int, default=200, help="single-vector Lanczos steps at BASELINE config 1 (0: skip)")
     ap.add_argument("--exchange", choices=["halo", "allgather"], default="halo",
                     help="multi-GPU Krylov-block exchange (N > 1, or with --dist at N = 1)")
     ap.add_argument("--dist", action="store_true",
@@ -216,6 +217,28 @@ def main():
                  "bytes_per_launch": spmm_bytes(n, A.nnz, b), "achieved_GBs": round(gbs, 1),
                  "frac_of_hbm_peak": round(gbs / HBM_PEAK_GBS, 4)}
 
+    # ---- BASELINE config 1 (single-vector Lanczos, n=1M, nnz=1e7): an extra line
+    c2 = None
+    if world == 1 and args.c2_steps > 0:
+        n2 = 1_000_000
+        A2 = lz.gen_banded(n2, 10.0, args.halfwidth, seed)
+        A2d = lz.CsrDevice.from_host(A2)
+        b2 = torch.from_numpy(lz.uniform_B(n2, 1, seed)[:, 0].copy()).cuda()
+        k2 = args.c2_steps
+        q2, al2, be2 = (torch.zeros(k2 + 1, **kw) for _ in range(3))
+        v0, v1, v2 = (torch.zeros(n2, **kw) for _ in range(3))
+        h.vector_lanczos(A2d, b2, k2, 84, q2, al2, be2, v0, v1, v2)  # warm
+        torch.cuda.synchronize()
+        t0c = time.perf_counter()
+        h.vector_lanczos(A2d, b2, k2, 84, q2, al2, be2, v0, v1, v2)
+        torch.cuda.synchronize()
+        dt2 = time.perf_counter() - t0c
+        c2 = {"workload": f"C2 single-vector Lanczos fp64, banded-random n={n2} nnz={A2.nnz}",
+              "iters_per_s": round(k2 / dt2, 1), "us_per_iter": round(dt2 / k2 * 1e6, 2),
+              "iteration_GBs": round((A2.nnz * 12 + (n2 + 1) * 8 + 5 * n2 * 8) / (dt2 / k2) / 1e9, 1),
+              "note": "A + 5 n s bytes per step (A, w read, q_{j-1} read, q_j written, w' written)"}
+        del A2d, v0, v1, v2
+
     # ---- CPU baseline: the oracle (C, OpenMP) on this operator, rank 0, N = 1
     cpu = None
     if world == 1 and rank == 0 and not args.no_cpu_baseline:
@@ -271,6 +294,7 @@ def main():
             "cpu_baseline": cpu,
             "extra": {
                 "plain_spmm": plain,
+                "c2_vector_lanczos": c2,
                 "kernel_ms_per_step": {"fused_spmm_pass": round(spmm_ms / K, 4),
                                        "update_pass": round(upd_ms / K, 4),
                                        "finish_sqrtm": round(small_ms / K, 4),
