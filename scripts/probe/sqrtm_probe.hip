@@ -43,11 +43,11 @@ static void run(double cond)
     hipMemcpy(dG, G.data(), B * B * 8, hipMemcpyHostToDevice);
     hipEvent_t e0, e1;
     hipEventCreate(&e0); hipEventCreate(&e1);
-    hipLaunchKernelGGL((lzprobe::k_sqrtm_b<double, B>), dim3(1), dim3(1024), 0, 0, dG, nullptr, 0, db, dbi, nullptr);
+    hipLaunchKernelGGL((lzprobe::k_sqrtm_b<double, B>), dim3(1), dim3(1024), 0, 0, dG, nullptr, 0, db, dbi, nullptr, nullptr, nullptr);
     hipEventRecord(e0);
     const int R = 20;
     for (int r = 0; r < R; ++r)
-        hipLaunchKernelGGL((lzprobe::k_sqrtm_b<double, B>), dim3(1), dim3(1024), 0, 0, dG, nullptr, 0, db, dbi, nullptr);
+        hipLaunchKernelGGL((lzprobe::k_sqrtm_b<double, B>), dim3(1), dim3(1024), 0, 0, dG, nullptr, 0, db, dbi, nullptr, nullptr, nullptr);
     hipEventRecord(e1);
     hipEventSynchronize(e1);
     float ms; hipEventElapsedTime(&ms, e0, e1);
