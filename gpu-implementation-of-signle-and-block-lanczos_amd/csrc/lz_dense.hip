@@ -167,6 +167,45 @@ __global__ __launch_bounds__(kRedThreads) void k_gram_finish(int b, const double
     }
 }
 
+// ------------------------------------------ b = 32 fp32 on v_mfma_f32_32x32x2_f32
+// (BASELINE config 5: block 32, fp32).  Lane l of a 32x32x2 MFMA supplies
+// A[i = l&31][k = l>>5] and B[k = l>>5][j = l&31]; C/D element (row
+// (v&3) + 8(v>>2) + 4(l>>5), col l&31) sits in register v of lane l.
+typedef float f16v_t __attribute__((ext_vector_type(16)));
+
+// G = X^T Y: k runs over rows, two per instruction; each wave walks 16-row
+// chunks, one accumulator (the 32x32x2 issue interval equals its dependent
+// latency, 64 cycles); per-block slabs of 32 x 32 doubles.
+template <bool SYM>
+__global__ __launch_bounds__(256) void k_gram32_f32(int64_t n, const float *__restrict__ X,
+                                                    const float *__restrict__ Y, double *__restrict__ part)
+{
+    __shared__ double red[4][1024];
+    const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+    f16v_t acc;
+#pragma unroll
+    for (int v = 0; v < 16; ++v) acc[v] = 0.0f;
+    XcdSched s(ceil_div(n, (int64_t)64));  // 64-row units: 16 rows per wave
+    for (int64_t u = s.begin; u < s.end; u += s.step) {
+        const int64_t r0 = u * 64 + 16 * w;
+        float a[8], bq[8];
+#pragma unroll
+        for (int t = 0; t < 8; ++t) {
+            const int64_t row = r0 + 2 * t + (lane >> 5);
+            a[t] = row < n ? X[row * 32 + (lane & 31)] : 0.0f;
+            if constexpr (!SYM) bq[t] = row < n ? Y[row * 32 + (lane & 31)] : 0.0f;
+        }
+#pragma unroll
+        for (int t = 0; t < 8; ++t) acc = __builtin_amdgcn_mfma_f32_32x32x2f32(a[t], SYM ? a[t] : bq[t], acc, 0, 0, 0);
+    }
+#pragma unroll
+    for (int v = 0; v < 16; ++v)
+        red[w][((v & 3) + 8 * (v >> 2) + 4 * (lane >> 5)) * 32 + (lane & 31)] = (double)acc[v];
+    __syncthreads();
+    for (int e = threadIdx.x; e < 1024; e += 256)
+        part[(int64_t)blockIdx.x * 1024 + e] = ((red[0][e] + red[1][e]) + red[2][e]) + red[3][e];
+}
+
 template <typename T>
 int gram_partials(lz_handle *h, int64_t n, int b, const T *X, const T *Y, int64_t ld, int *nparts)
 {
@@ -189,6 +228,21 @@ int gram_partials(lz_handle *h, int64_t n, int b, const T *X, const T *Y, int64_
                                    X, Y, h->partials);
                 prof_end(h, ev_);
                 }
+            LZ_LAUNCH_CHECK();
+            *nparts = grid;
+            return LZ_OK;
+        }
+    }
+    if constexpr (std::is_same<T, float>::value) {
+        if (b == 32 && ld == 32) {
+            const int grid = (int)std::max<int64_t>(1, std::min<int64_t>(ceil_div(n, (int64_t)64), h->n_cu * 2));
+            LZ_TRY(ensure_partials(h, (size_t)grid * 1024));
+            const int ev_ = prof_begin(h, PROF_GRAM);
+            if (X == Y)
+                hipLaunchKernelGGL(k_gram32_f32<true>, dim3(grid), dim3(256), 0, h->stream, n, X, Y, h->partials);
+            else
+                hipLaunchKernelGGL(k_gram32_f32<false>, dim3(grid), dim3(256), 0, h->stream, n, X, Y, h->partials);
+            prof_end(h, ev_);
             LZ_LAUNCH_CHECK();
             *nparts = grid;
             return LZ_OK;
@@ -602,6 +656,59 @@ __global__ __launch_bounds__(512) void k_tsmm16_f64(int64_t n, double sw, double
     }
 }
 
+// W = sw*W + sq*(Q S), computed transposed: D = S^T Q^T, so lane l's 16
+// accumulator registers are row l&31 of the 32-row tile, columns
+// 8g + 4(l>>5) + 0..3 in registers 4g..4g+3 -- four 16-B loads / stores per
+// lane.  The contraction is permuted (k = 16(l>>5) + s at step s) so the Q
+// operand of a lane is 64 contiguous bytes of its row (four 16-B loads).
+__global__ __launch_bounds__(256) void k_tsmm32_f32(int64_t n, float sw, float sq, const float *__restrict__ Q,
+                                                    const float *__restrict__ S, float *__restrict__ W)
+{
+    const int lane = threadIdx.x & 63, w = threadIdx.x >> 6, hh = lane >> 5, jr = lane & 31;
+    float sa[16];  // A[i = jr][k = 16 hh + s] = S[k][jr]
+#pragma unroll
+    for (int st = 0; st < 16; ++st) sa[st] = S[(16 * hh + st) * 32 + jr];
+    XcdSched s(ceil_div(n, (int64_t)128));  // 128-row units: 32 rows per wave
+    for (int64_t u = s.begin; u < s.end; u += s.step) {
+        const int64_t row = u * 128 + 32 * w + jr;
+        const bool ok = row < n;
+        float qb[16];
+#pragma unroll
+        for (int c4 = 0; c4 < 4; ++c4) {
+            float4 x = make_float4(0.f, 0.f, 0.f, 0.f);
+            if (ok) x = *reinterpret_cast<const float4 *>(Q + row * 32 + 16 * hh + 4 * c4);
+            qb[4 * c4] = x.x; qb[4 * c4 + 1] = x.y; qb[4 * c4 + 2] = x.z; qb[4 * c4 + 3] = x.w;
+        }
+        float4 wo[4];
+        if (sw != 0.0f) {
+#pragma unroll
+            for (int g = 0; g < 4; ++g)
+                wo[g] = ok ? *reinterpret_cast<const float4 *>(W + row * 32 + 8 * g + 4 * hh)
+                           : make_float4(0.f, 0.f, 0.f, 0.f);
+        }
+        f16v_t acc;
+#pragma unroll
+        for (int v = 0; v < 16; ++v) acc[v] = 0.0f;
+#pragma unroll
+        for (int st = 0; st < 16; ++st) acc = __builtin_amdgcn_mfma_f32_32x32x2f32(sa[st], qb[st], acc, 0, 0, 0);
+        if (ok) {
+#pragma unroll
+            for (int g = 0; g < 4; ++g) {
+                float4 o;
+                if (sw != 0.0f) {
+                    o.x = fmaf(sw, wo[g].x, sq * acc[4 * g]);
+                    o.y = fmaf(sw, wo[g].y, sq * acc[4 * g + 1]);
+                    o.z = fmaf(sw, wo[g].z, sq * acc[4 * g + 2]);
+                    o.w = fmaf(sw, wo[g].w, sq * acc[4 * g + 3]);
+                } else {
+                    o = make_float4(sq * acc[4 * g], sq * acc[4 * g + 1], sq * acc[4 * g + 2], sq * acc[4 * g + 3]);
+                }
+                *reinterpret_cast<float4 *>(W + row * 32 + 8 * g + 4 * hh) = o;
+            }
+        }
+    }
+}
+
 template <typename T>
 __global__ __launch_bounds__(256) void k_tsmm_gen(int64_t n, int b, T sw, T sq,
                                                   const T *__restrict__ Q, const T *__restrict__ S,
@@ -648,6 +755,16 @@ int tsmm(lz_handle *h, int64_t n, int b, T sw, T sq, const T *Q, const T *S, T *
                                W);
             prof_end(h, ev_);
             }
+            LZ_LAUNCH_CHECK();
+            return LZ_OK;
+        }
+    }
+    if constexpr (std::is_same<T, float>::value) {
+        if (b == 32 && ld == 32) {
+            const int grid = (int)std::max<int64_t>(1, std::min<int64_t>(ceil_div(n, (int64_t)128), h->n_cu * 4));
+            const int ev_ = prof_begin(h, PROF_TSMM);
+            hipLaunchKernelGGL(k_tsmm32_f32, dim3(grid), dim3(256), 0, h->stream, n, sw, sq, Q, S, W);
+            prof_end(h, ev_);
             LZ_LAUNCH_CHECK();
             return LZ_OK;
         }
