@@ -415,6 +415,7 @@ int lz_finalize(lz_handle *h)
     (void)hipSetDevice(h->device);
     halo_free(h);
     (void)hipFree(h->pairs);
+    (void)hipFree(h->longq);
     if (h->comm) ncclCommDestroy(comm_of(h));
     if (h->ev_pool) {
         for (int i = 0; i < h->ev_cap; ++i) (void)hipEventDestroy(h->ev_pool[i]);

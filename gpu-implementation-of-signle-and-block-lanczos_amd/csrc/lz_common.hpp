@@ -71,6 +71,8 @@ struct lz_handle {
     int nranks = 1, rank = 0;
     void *halo = nullptr;         // lz::HaloPlan when lz_halo_init was called
     uint64_t *pairs = nullptr;    // per-16-row-strip row order by length (k_strip_pairs)
+    int *longq = nullptr;         // k_spmm_seg long-tile queue: [0] count, [1..] tile ids
+    size_t longq_cap = 0;         // ints
     size_t pairs_cap = 0;         // entries
     // optional per-kernel-class timing with hipEvents on the handle's stream
     // (lz_prof_enable / lz_prof_read): events recorded around each launch of

@@ -521,13 +521,22 @@ __global__ __launch_bounds__(64 * (WS_NC + 1)) void k_spmm_ws(int64_t n, const i
 // first and last rows go to head/tail slots and are summed in a fixed order,
 // so results stay bitwise reproducible; the Y tile leaves with full-lane
 // coalesced stores.
-template <typename T, int B, int TR, int CAP, int UNR = 8, bool NT = false, int GAUX = 0>
+template <typename T, int B, int TR, int CAP, int UNR = 8, bool NT = false, int GAUX = 0, int MODE = 2>
 __global__ __launch_bounds__(256) void k_spmm_seg(int64_t n, const int64_t *__restrict__ rp,
                                                   const int32_t *__restrict__ col,
                                                   const T *__restrict__ val,
                                                   const T *__restrict__ X, int64_t ldx, int64_t nx,
-                                                  T *__restrict__ Y, int64_t ldy)
+                                                  T *__restrict__ Y, int64_t ldy, int *__restrict__ longq)
 {
+    // MODE 0: tiles whose run exceeds the stage are queued (longq[0] = count,
+    //         longq[1..] = tile ids) for MODE 1, so their code path costs the
+    //         main kernel no registers;
+    // MODE 1: persistent blocks over the queued tiles: CAP-sized chunks, each
+    //         split over the 32 groups; rows accumulate in the LDS Y tile
+    //         across chunks (chunk order, then group order: bitwise
+    //         reproducible).  A row-wise walk would leave one 8-lane group
+    //         serialising a 10^5-entry row (power-law degrees, config 5);
+    // MODE 2: long tiles walked row-wise in place (A/B, other tile heights).
     using S = SpmmShape<T, B>;
     constexpr int VEC = S::VEC, LPR = S::LPR, G = 256 / LPR;
     static_assert(TR <= 255, "row ids are bytes");
@@ -539,38 +548,137 @@ __global__ __launch_bounds__(256) void k_spmm_seg(int64_t n, const int64_t *__re
     __shared__ Vec<T, VEC> head[G][LPR];     // a group's piece of a row begun in an earlier slice
     const int tid = threadIdx.x;
     const int gi = tid / LPR, p = tid % LPR;
-    const int64_t r0 = xcd_remap(blockIdx.x, gridDim.x) * TR;
-    const int nrows = (int)((n - r0) < TR ? (n - r0) : TR);
-    const int64_t kA = rp[r0];
-    if (tid <= nrows) rel[tid] = (int)(rp[r0 + tid] - kA);
-    const int64_t N64 = rp[r0 + nrows] - kA;
     const __amdgpu_buffer_rsrc_t xr = lz_rsrc(X, (uint32_t)(nx * ldx * (int64_t)sizeof(T)));
     const uint32_t rowb = (uint32_t)(ldx * sizeof(T)), lane_off = p * VEC * sizeof(T);
     Vec<T, VEC> zero;
 #pragma unroll
     for (int i = 0; i < VEC; ++i) zero.v[i] = T(0);
-    if (N64 > CAP) {  // block-uniform: long rows -- row-wise straight from global
-        for (int r = gi; r < nrows; r += G) {
-            const int64_t a = rp[r0 + r], e = rp[r0 + r + 1];
-            Vec<T, VEC> acc = zero;
-            for (int64_t k = a; k < e; k += UNR) {
-                Vec<T, VEC> xs[UNR];
-                T vv[UNR];
-#pragma unroll
-                for (int t = 0; t < UNR; ++t) {
-                    const bool ok = k + t < e;
-                    vv[t] = ok ? val[k + t] : T(0);
-                    const uint32_t off = ok ? __umul24((unsigned)col[k + t], rowb) + lane_off : 0x80000000u;
-                    xs[t] = ldbuf<T, VEC>(xr, off);
+    if constexpr (MODE == 1) {
+        const int cnt = longq[0];
+        for (int qi = blockIdx.x; qi < cnt; qi += gridDim.x) {
+            const int64_t r0 = (int64_t)longq[1 + qi] * TR;
+            const int nrows = (int)((n - r0) < TR ? (n - r0) : TR);
+            const int64_t kA = rp[r0];
+            __syncthreads();  // the previous tile is done with rel / yt
+            if (tid <= nrows) rel[tid] = (int)(rp[r0 + tid] - kA);
+            const int64_t N64 = rp[r0 + nrows] - kA;
+        for (int idx = tid; idx < TR * LPR; idx += 256) yt[idx / LPR][idx % LPR] = zero;
+        for (int64_t c0 = kA; c0 < kA + N64; c0 += CAP) {
+            const int64_t c1 = (c0 + CAP < kA + N64) ? c0 + CAP : kA + N64;
+            const int Nc = (int)(c1 - c0), cb = (int)(c0 - kA);  // chunk length, offset in the run
+            __syncthreads();  // rel visible; the previous chunk is done with cs / vs / rid / head
+            for (int k = tid; k < Nc; k += 256) {
+                cs[k] = col[c0 + k];
+                vs[k] = val[c0 + k];
+                int lo = 0, hi = nrows - 1;  // the row holding entry cb + k: rel[r] <= cb + k < rel[r + 1]
+                while (lo < hi) {
+                    const int mid = (lo + hi + 1) >> 1;
+                    if (rel[mid] <= cb + k) lo = mid;
+                    else hi = mid - 1;
                 }
-#pragma unroll
-                for (int t = 0; t < UNR; ++t)
-#pragma unroll
-                    for (int i = 0; i < VEC; ++i) acc.v[i] = fma(vv[t], xs[t].v[i], acc.v[i]);
+                rid[k] = (uint8_t)lo;
             }
-            stv<T, VEC>(Y + (r0 + r) * ldy + p * VEC, acc);
+            if (tid < UNR) {
+                cs[Nc + tid] = 0;
+                vs[Nc + tid] = T(0);
+                rid[Nc + tid] = 255;
+            }
+            __syncthreads();
+            const int E = ((Nc + G - 1) / G + UNR - 1) / UNR * UNR;
+            const int start = gi * E, end = (start + E < Nc) ? start + E : Nc;
+            if (start < end) {  // group-uniform
+                int cur = rid[start];
+                bool open = (rel[cur] - cb > 0 ? rel[cur] - cb : 0) < start;
+                Vec<T, VEC> acc = zero;
+                auto flush = [&]() {
+                    if (open) {
+                        head[gi][p] = acc;
+                    } else {
+#pragma unroll
+                        for (int i2 = 0; i2 < VEC; ++i2) yt[cur][p].v[i2] += acc.v[i2];
+                    }
+                };
+                for (int s0 = start; s0 < end; s0 += UNR) {
+                    int32_t cc[UNR];
+                    T vv[UNR];
+                    int rr[UNR];
+#pragma unroll
+                    for (int t = 0; t < UNR; ++t) {
+                        cc[t] = cs[s0 + t];
+                        vv[t] = vs[s0 + t];
+                        rr[t] = rid[s0 + t];
+                    }
+                    Vec<T, VEC> xs[UNR];
+#pragma unroll
+                    for (int t = 0; t < UNR; ++t) {
+                        const uint32_t off =
+                            s0 + t < end ? __umul24((unsigned)cc[t], rowb) + lane_off : 0x80000000u;
+                        xs[t] = ldbuf<T, VEC, GAUX>(xr, off);
+                    }
+#pragma unroll
+                    for (int t = 0; t < UNR; ++t) {
+                        const int r = s0 + t < end ? rr[t] : cur;
+                        if (r != cur) {
+                            flush();
+                            acc = zero;
+                            cur = r;
+                            open = false;
+                        }
+#pragma unroll
+                        for (int i2 = 0; i2 < VEC; ++i2) acc.v[i2] = fma(vv[t], xs[t].v[i2], acc.v[i2]);
+                    }
+                }
+                flush();
+            }
+            __syncthreads();
+            for (int r = gi; r < nrows; r += G) {  // rows over several slices of this chunk
+                const int a = (rel[r] > cb ? rel[r] : cb) - cb, e = (rel[r + 1] < cb + Nc ? rel[r + 1] : cb + Nc) - cb;
+                if (a >= e) continue;
+                const int g1 = a / E, g2 = (e - 1) / E;
+                for (int g = g1 + 1; g <= g2; ++g) {
+#pragma unroll
+                    for (int i2 = 0; i2 < VEC; ++i2) yt[r][p].v[i2] += head[g][p].v[i2];
+                }
+            }
+        }
+        __syncthreads();
+        for (int idx = tid; idx < nrows * LPR; idx += 256)
+            stv<T, VEC>(Y + (r0 + idx / LPR) * ldy + (idx % LPR) * VEC, yt[idx / LPR][idx % LPR]);
         }
         return;
+    } else {
+    const int64_t r0 = xcd_remap(blockIdx.x, gridDim.x) * TR;
+    const int nrows = (int)((n - r0) < TR ? (n - r0) : TR);
+    const int64_t kA = rp[r0];
+    if (tid <= nrows) rel[tid] = (int)(rp[r0 + tid] - kA);
+    const int64_t N64 = rp[r0 + nrows] - kA;
+    if (N64 > CAP) {  // block-uniform
+        if constexpr (MODE == 0) {
+            if (tid == 0) longq[1 + atomicAdd(&longq[0], 1)] = (int)(r0 / TR);
+            return;
+        } else {
+        for (int r = gi; r < nrows; r += G) {
+                const int64_t a = rp[r0 + r], e = rp[r0 + r + 1];
+                Vec<T, VEC> acc = zero;
+                for (int64_t k = a; k < e; k += UNR) {
+                    Vec<T, VEC> xs[UNR];
+                    T vv[UNR];
+#pragma unroll
+                    for (int t = 0; t < UNR; ++t) {
+                        const bool ok = k + t < e;
+                        vv[t] = ok ? val[k + t] : T(0);
+                        const uint32_t off = ok ? __umul24((unsigned)col[k + t], rowb) + lane_off : 0x80000000u;
+                        xs[t] = ldbuf<T, VEC>(xr, off);
+                    }
+#pragma unroll
+                    for (int t = 0; t < UNR; ++t)
+#pragma unroll
+                        for (int i = 0; i < VEC; ++i) acc.v[i] = fma(vv[t], xs[t].v[i], acc.v[i]);
+                }
+                stv<T, VEC>(Y + (r0 + r) * ldy + p * VEC, acc);
+            }
+            return;
+        }
     }
     const int N = (int)N64;
     {  // stage the run with 16-B loads (aligned down; a piece reaching past nnz,
@@ -706,6 +814,7 @@ __global__ __launch_bounds__(256) void k_spmm_seg(int64_t n, const int64_t *__re
             stv<T, VEC>(dst, yt[idx / LPR][idx % LPR]);
         }
     }
+    }  // MODE 0 / 2
 }
 
 template <typename T, int B, int TR, int CAP>
@@ -951,7 +1060,7 @@ static int launch_spmm_rm(lz_handle *h, int64_t n, const int64_t *rp, const int3
         LZ_ARG_CHECK(st < (1LL << 31), "too many row tiles");
         auto go = [&](auto kern) {
             hipLaunchKernelGGL(kern, dim3((unsigned)st), dim3(256), 0, h->stream, n, rp, col, val, X, ldx, nx, Y,
-                               ldy);
+                               ldy, nullptr);
         };
         if (tr == 96)
             go(k_spmm_seg<T, B, 96, 1536, 8, true>);
@@ -959,8 +1068,25 @@ static int launch_spmm_rm(lz_handle *h, int64_t n, const int64_t *rp, const int3
             go(k_spmm_seg<T, B, 64, 1024, 8, true>);
         else if (tr == 32)
             go(k_spmm_seg<T, B, 32, 512, 8, true>);
-        else
-            go(k_spmm_seg<T, B, 48, 768, 8, true>);
+        else if (c == '5')  // A/B: long runs walked row-wise in place
+            go(k_spmm_seg<T, B, 48, 768, 8, true, 0, 2>);
+        else {
+            // long tiles (run > stage) queued by the main kernel, then chunked by a
+            // persistent second kernel (an empty queue costs one short launch)
+            if ((size_t)st + 1 > h->longq_cap) {
+                LZ_HIP_TRY(hipStreamSynchronize(h->stream));
+                (void)hipFree(h->longq);
+                h->longq = nullptr;
+                LZ_HIP_TRY(hipMalloc(&h->longq, sizeof(int) * ((size_t)st + 1)));
+                h->longq_cap = (size_t)st + 1;
+            }
+            LZ_HIP_TRY(hipMemsetAsync(h->longq, 0, sizeof(int), h->stream));
+            hipLaunchKernelGGL((k_spmm_seg<T, B, 48, 768, 8, true, 0, 0>), dim3((unsigned)st), dim3(256), 0, h->stream,
+                               n, rp, col, val, X, ldx, nx, Y, ldy, h->longq);
+            const int g2 = (int)std::max<int64_t>(1, std::min<int64_t>(st, (int64_t)h->n_cu * 4));
+            hipLaunchKernelGGL((k_spmm_seg<T, B, 48, 768, 8, true, 0, 1>), dim3(g2), dim3(256), 0, h->stream, n, rp,
+                               col, val, X, ldx, nx, Y, ldy, h->longq);
+        }
     } else if (buf_ok && variant && variant[0] == 'p') {  // first-touch prefetch round (A/B)
         hipLaunchKernelGGL((k_spmm_buf<T, B, 1024, 2, 8, 1, 4>), dim3((unsigned)tiles), dim3(256), 0,
                            h->stream, n, rp, col, val, X, ldx, nx, Y, ldy);
