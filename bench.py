@@ -102,6 +102,7 @@ def main():
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--spmm-reps", type=int, default=20)
     ap.add_argument("--c2-steps", type=int, default=200, help="single-vector Lanczos steps at BASELINE config 1 (0: skip)")
+    ap.add_argument("--c5-steps", type=int, default=10, help="block-32 fp32 power-law steps at BASELINE config 4 (0: skip)")
     ap.add_argument("--exchange", choices=["halo", "allgather"], default="halo",
                     help="multi-GPU Krylov-block exchange (N > 1, or with --dist at N = 1)")
     ap.add_argument("--dist", action="store_true",
@@ -239,6 +240,28 @@ def main():
               "note": "A + 5 n s bytes per step (A, w read, q_{j-1} read, q_j written, w' written)"}
         del A2d, v0, v1, v2
 
+    # ---- BASELINE config 4 (block Lanczos b=32 fp32, power-law rows): an extra line
+    c5 = None
+    if world == 1 and args.c5_steps > 0:
+        n5, k5 = args.n, args.c5_steps
+        A5 = lz.gen_powerlaw(n5, 10.0, 2.1, 100000, seed=seed, dtype=np.float32)
+        A5d = lz.CsrDevice.from_host(A5)
+        kw5 = dict(dtype=torch.float32, device="cuda")
+        B5 = torch.from_numpy(lz.uniform_B(n5, 32, seed=seed + 3, dtype=np.float32)).cuda()
+        q5, al5, be5 = torch.zeros(k5 * 32, **kw5), torch.zeros(k5, 32, 32, **kw5), torch.zeros(k5 + 1, 32, 32, **kw5)
+        P5 = [torch.zeros(n5, 32, **kw5) for _ in range(3)]
+        h.block_lanczos_blas(A5d, B5, 2, 84, q5, al5, be5, *P5)  # warm
+        torch.cuda.synchronize()
+        t0c = time.perf_counter()
+        h.block_lanczos_blas(A5d, B5, k5, 84, q5, al5, be5, *P5)
+        torch.cuda.synchronize()
+        dt5 = time.perf_counter() - t0c
+        c5 = {"workload": f"C5 block Lanczos b=32 fp32, power-law-degree CSR (alpha 2.1, cap 1e5) n={n5} "
+                          f"nnz={A5.nnz}, max row {int(np.diff(A5.row_ptr).max())}",
+              "iters_per_s": round(k5 / dt5, 2), "ms_per_iter": round(dt5 / k5 * 1e3, 3),
+              "finite": bool(torch.isfinite(al5).all())}
+        del A5d, B5, P5
+
     # ---- CPU baseline: the oracle (C, OpenMP) on this operator, rank 0, N = 1
     cpu = None
     if world == 1 and rank == 0 and not args.no_cpu_baseline:
@@ -295,6 +318,7 @@ def main():
             "extra": {
                 "plain_spmm": plain,
                 "c2_vector_lanczos": c2,
+                "c5_block32_f32_powerlaw": c5,
                 "kernel_ms_per_step": {"fused_spmm_pass": round(spmm_ms / K, 4),
                                        "update_pass": round(upd_ms / K, 4),
                                        "finish_sqrtm": round(small_ms / K, 4),
