@@ -149,7 +149,9 @@ int lz_vector_lanczos(lz_handle *h, int64_t n, int64_t nnz, const int64_t *row_p
 
 /* Forward-Euler validation run U += dt*A*U, Nsteps times, then out[c] = U(lc,c).
  * Replaces ftdt_block (methods/fdtd.hpp:33-56).  U0 n x b row-major; U, D are
- * n x b workspaces. */
+ * n x b buffers (U receives the final state, D is scratch).  Up to 2^18 rows each
+ * step is one fused kernel (U and D ping-pong); the step loop is replayed from a
+ * captured hipGraph of 256 steps (LZ_FDTD_GRAPH=0: launch every step). */
 int lz_fdtd_block(lz_handle *h, int64_t n, int64_t nnz, const int64_t *row_ptr,
                   const int32_t *col, const void *val, lz_dtype dtype, int b, const void *U0,
                   int64_t steps, double T_end, int64_t lc, void *U, void *D, void *out);

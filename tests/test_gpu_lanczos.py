@@ -144,6 +144,24 @@ def test_fdtd_block(lz, orc, handle, torch_cuda, golden):
     assert np.allclose(out.cpu().numpy(), orc.fdtd_block(A, B, 2000, 1.0, lc), rtol=1e-12)
 
 
+@pytest.mark.parametrize("n,b,steps", [(3001, 3, 1001), (3001, 16, 513), ((1 << 18) + 1, 4, 3)])
+def test_fdtd_block_shapes(lz, orc, handle, torch_cuda, n, b, steps):
+    """Odd step counts (final state in the ping-pong buffer), b not a power of
+    two, a graph replay count with eager remainder, and the unfused large-n path."""
+    torch = torch_cuda
+    A = lz.gen_banded(n, 6.0, 200, seed=n)
+    A = lz.CsrHost(A.n, A.row_ptr, A.col, A.val * 0.05)
+    B = lz.uniform_B(n, b, seed=7)
+    lc = n // 3
+    kw = dict(dtype=torch.float64, device="cuda")
+    U = torch.empty(n, b, **kw)
+    out = torch.empty(b, **kw)
+    handle.ftdt_block(lz.CsrDevice.from_host(A), torch.from_numpy(B).cuda(), steps, 1.0, lc,
+                      U, torch.empty(n, b, **kw), out)
+    ref = orc.fdtd_block(A, B, steps, 1.0, lc)
+    assert np.allclose(out.cpu().numpy(), ref, rtol=1e-12, atol=1e-14)
+
+
 def test_block_large_properties(lz, orc, handle, torch_cuda):
     """n = 2M, b = 16: fused == unfused (two GPU paths), bitwise run-to-run
     determinism, and the oracle (OpenMP) on the same input."""
