@@ -17,6 +17,7 @@
 // place (row r is read and written by the same wave), the residual alternates
 // between the W and Q1 buffers.  All epilogue products run on
 // v_mfma_f64_16x16x4_f64 (see lz_dense.hip for the operand layouts).
+#include <cstring>
 #include "lz_common.hpp"
 #include "lz_internal.hpp"
 #include "lz_kernels.hpp"
@@ -1908,6 +1909,257 @@ __global__ __launch_bounds__(kVlThreads) void k_vl_spmv(
     block_store_slab(dot, red, part_out);
 }
 
+// CSR-stream form of k_vl_spmv (same outputs).  A tile of R rows is one
+// contiguous run of the CSR arrays: each thread loads whole 4-entry quads of it
+// (one 16-B col load, two 16-B val loads), gathers the four w values, and parks
+// the products in LDS; then thread t sums row t's products in CSR order and
+// runs the row epilogue.  Against the lanes-per-row kernel this issues ~4x fewer
+// vector-memory instructions per row (col/val vectorised, the epilogue on every
+// lane instead of one in LV), which is what a 10-nnz-per-row SpMV spends.
+// A run longer than NQ quads per thread (a heavy tile) takes a wave per row.
+// The row sum adds rounded products left to right, the oracle's arithmetic.
+template <int NT, int NQ>
+__global__ __launch_bounds__(NT) void k_vl_spmv_cs(
+    int64_t n, int64_t nnz, const int64_t *__restrict__ rp, const int32_t *__restrict__ col,
+    const double *__restrict__ val, const double *__restrict__ w, double *__restrict__ qbuf,
+    double *__restrict__ wn, const double *__restrict__ part_in, int P, int has_prev, int64_t lc,
+    double *__restrict__ qrow, double *__restrict__ beta_out, double *__restrict__ part_out)
+{
+    constexpr int R = NT, CAPQ = NQ * NT;
+    __shared__ double red[NT];
+    __shared__ double prod[4 * CAPQ];
+    __shared__ double yrow[R];
+    __shared__ int64_t srp[R + 1];
+    const double bsq = block_sum_slabs(part_in, P, red);
+    const double beta = sqrt(bsq), rbeta = 1.0 / beta;
+    if (blockIdx.x == 0 && threadIdx.x == 0) *beta_out = beta;
+    const int t = threadIdx.x, lane = t & 63, wv = t >> 6;
+    double dot = 0.0;
+    XcdSched sch(ceil_div(n, R));
+    for (int64_t u = sch.begin; u < sch.end; u += sch.step) {
+        const int64_t r0 = u * R;
+        const int rows = (int)(n - r0 < R ? n - r0 : R);
+        for (int i = t; i <= rows; i += NT) srp[i] = rp[r0 + i];
+        __syncthreads();
+        const int64_t k0 = srp[0], k1 = srp[rows];
+        double acc = 0.0;
+        if (((k1 + 3) >> 2) - (k0 >> 2) <= CAPQ) {  // block-uniform
+            const int64_t qb = k0 >> 2, qe = (k1 + 3) >> 2;
+            int c[NQ][4];
+            double v[NQ][4], x[NQ][4];
+#pragma unroll
+            for (int i = 0; i < NQ; ++i) {
+                const int64_t q = qb + t + (int64_t)NT * i;
+#pragma unroll
+                for (int j = 0; j < 4; ++j) { c[i][j] = 0; v[i][j] = 0.0; }
+                if (q < qe) {
+                    if (4 * q + 4 <= nnz) {
+                        const int4 c4 = *reinterpret_cast<const int4 *>(col + 4 * q);
+                        const double2 va = *reinterpret_cast<const double2 *>(val + 4 * q);
+                        const double2 vb = *reinterpret_cast<const double2 *>(val + 4 * q + 2);
+                        c[i][0] = c4.x; c[i][1] = c4.y; c[i][2] = c4.z; c[i][3] = c4.w;
+                        v[i][0] = va.x; v[i][1] = va.y; v[i][2] = vb.x; v[i][3] = vb.y;
+                    } else {
+#pragma unroll
+                        for (int j = 0; j < 4; ++j)
+                            if (4 * q + j < nnz) { c[i][j] = col[4 * q + j]; v[i][j] = val[4 * q + j]; }
+                    }
+                }
+            }
+#pragma unroll
+            for (int i = 0; i < NQ; ++i) {
+                const int64_t q = qb + t + (int64_t)NT * i;
+#pragma unroll
+                for (int j = 0; j < 4; ++j) {
+                    const int64_t e = 4 * q + j;
+                    x[i][j] = (q < qe && e >= k0 && e < k1) ? w[c[i][j]] : 0.0;
+                }
+            }
+#pragma unroll
+            for (int i = 0; i < NQ; ++i) {
+                const int64_t q = qb + t + (int64_t)NT * i;
+#pragma unroll
+                for (int j = 0; j < 4; ++j) {
+                    const int64_t e = 4 * q + j;
+                    if (q < qe && e >= k0 && e < k1) {
+#pragma clang fp contract(off)
+                        prod[e - k0] = v[i][j] * x[i][j];
+                    }
+                }
+            }
+            __syncthreads();
+            if (t < rows)
+                for (int64_t k = srp[t] - k0, e = srp[t + 1] - k0; k < e; ++k) acc += prod[k];
+        } else {  // heavy tile: a wave per row, lanes strided, fixed-shape shuffle tree
+            for (int r = wv; r < rows; r += NT / 64) {
+                double a = 0.0;
+                for (int64_t k = srp[r] + lane; k < srp[r + 1]; k += 64) a = fma(val[k], w[col[k]], a);
+#pragma unroll
+                for (int off = 32; off > 0; off >>= 1) a += __shfl_xor(a, off, 64);
+                if (lane == 0) yrow[r] = a;
+            }
+            __syncthreads();
+            if (t < rows) acc = yrow[t];
+        }
+        if (t < rows) {
+            const int64_t row = r0 + t;
+            const double qj = w[row] * rbeta;
+            double wvv = acc * rbeta;
+            if (has_prev) wvv = fma(-beta, qbuf[row], wvv);
+            qbuf[row] = qj;
+            wn[row] = wvv;
+            dot = fma(wvv, qj, dot);
+            if (row == lc) *qrow = qj;
+        }
+        __syncthreads();  // srp / prod / yrow reused by the next tile
+    }
+    block_store_slab(dot, red, part_out);
+}
+
+// Half band width max_k |col[k] - row(k)| of the operator (once per solve);
+// band[0] must be zero on entry.
+__global__ __launch_bounds__(256) void k_vl_band(int64_t n, const int64_t *__restrict__ rp,
+                                                 const int32_t *__restrict__ col,
+                                                 unsigned long long *__restrict__ band)
+{
+    unsigned long long m = 0;
+    for (int64_t r = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; r < n;
+         r += (int64_t)gridDim.x * blockDim.x)
+        for (int64_t k = rp[r], e = rp[r + 1]; k < e; ++k) {
+            const int64_t d = (int64_t)col[k] - r;
+            const unsigned long long a = (unsigned long long)(d < 0 ? -d : d);
+            m = a > m ? a : m;
+        }
+#pragma unroll
+    for (int off = 32; off > 0; off >>= 1) {
+        const unsigned long long o = __shfl_xor(m, off, 64);
+        m = o > m ? o : m;
+    }
+    if ((threadIdx.x & 63) == 0 && m) atomicMax(band, m);
+}
+
+// Band-window form of k_vl_spmv (same outputs, same per-row arithmetic: LV
+// lanes per row, strided, fixed xor tree).  Block g owns the contiguous rows
+// [n g / G, n (g+1) / G) and walks them in tiles of R; the gathered vector
+// lives in an LDS ring holding w[r0 - H, r0 + R + H) for the current tile
+// (H = the operator's half band width) while the next tile's R-element slab
+// arrives from registers.  A banded operator's 10 gathers per row then cost
+// LDS reads instead of ~10 L2 requests each holding a texture-path miss slot
+// (PMC on C2: ~1e7 L2 requests per SpMV, the whole bound of the gather kernels).
+// Operators with 2H + 2R > the ring gather from global memory (same kernel).
+constexpr int kWinThreads = 1024, kWinRows = 1024, kWinRing = 16384;
+
+// Tile loop of k_vl_spmv_win; WIN selects LDS-ring or global gathers at
+// compile time (a runtime select would make every gather a flat load).
+template <int LV, bool WIN>
+__device__ __forceinline__ double vl_win_tiles(int64_t n, int64_t c0, int64_t c1, int64_t H,
+                                               const int64_t *__restrict__ rp,
+                                               const int32_t *__restrict__ col,
+                                               const double *__restrict__ val,
+                                               const double *__restrict__ w, double *__restrict__ qbuf,
+                                               double *__restrict__ wn, int has_prev, int64_t lc,
+                                               double *__restrict__ qrow, double beta, double rbeta,
+                                               double *ring, double *yrow)
+{
+    constexpr int NT = kWinThreads, R = kWinRows, M = kWinRing - 1;
+    constexpr int RPP = NT / LV, PASSES = R / RPP;  // rows per pass, passes per tile
+    const int t = threadIdx.x, g = t / LV, p = t % LV;
+    auto wat = [&](int64_t i) -> double { return WIN ? ring[i & M] : w[i]; };
+    double dot = 0.0;
+    for (int64_t r0 = c0; r0 < c1; r0 += R) {
+        const int rows = (int)(c1 - r0 < R ? c1 - r0 : R);
+        // next tile's slab and this thread's epilogue row, issued first
+        const int64_t si = r0 + R + H + t;
+        const double slab = (WIN && si < n) ? w[si] : 0.0;
+        const int64_t erow = r0 + t;
+        const double qprev = (t < rows && has_prev) ? qbuf[erow] : 0.0;
+        // CSR offsets relative to the tile's first entry (a tile's run < 2^31)
+        const int64_t kb = rp[r0];
+        const int32_t *cb = col + kb;
+        const double *vb = val + kb;
+        int ks[PASSES], ke[PASSES];
+#pragma unroll
+        for (int s = 0; s < PASSES; ++s) {
+            const int lr = s * RPP + g;
+            ks[s] = lr < rows ? (int)(rp[r0 + lr] - kb) : 0;
+            ke[s] = lr < rows ? (int)(rp[r0 + lr + 1] - kb) : 0;
+        }
+        int c[PASSES][2];
+        double v[PASSES][2];
+#pragma unroll
+        for (int s = 0; s < PASSES; ++s)
+#pragma unroll
+            for (int h2 = 0; h2 < 2; ++h2) {
+                const int k = ks[s] + p + h2 * LV;
+                c[s][h2] = k < ke[s] ? cb[k] : -1;
+                v[s][h2] = k < ke[s] ? vb[k] : 0.0;
+            }
+#pragma unroll
+        for (int s = 0; s < PASSES; ++s) {
+            double acc = 0.0;
+#pragma unroll
+            for (int h2 = 0; h2 < 2; ++h2)
+                if (c[s][h2] >= 0) acc = fma(v[s][h2], wat(c[s][h2]), acc);
+            for (int k = ks[s] + p + 2 * LV; k < ke[s]; k += LV) acc = fma(vb[k], wat(cb[k]), acc);
+#pragma unroll
+            for (int off = LV / 2; off > 0; off >>= 1) acc += __shfl_xor(acc, off, 64);
+            if (p == 0) yrow[s * RPP + g] = acc;
+        }
+        __syncthreads();
+        if (t < rows) {
+            const double qj = wat(erow) * rbeta;
+            double wv = yrow[t] * rbeta;
+            if (has_prev) wv = fma(-beta, qprev, wv);
+            qbuf[erow] = qj;
+            wn[erow] = wv;
+            dot = fma(wv, qj, dot);
+            if (erow == lc) *qrow = qj;
+        }
+        if (WIN && si < n) ring[si & M] = slab;  // disjoint from this tile's window (2H + 2R <= ring)
+        __syncthreads();
+    }
+    return dot;
+}
+
+template <int LV>
+__global__ __launch_bounds__(kWinThreads) void k_vl_spmv_win(
+    int64_t n, const int64_t *__restrict__ rp, const int32_t *__restrict__ col,
+    const double *__restrict__ val, const double *__restrict__ w, double *__restrict__ qbuf,
+    double *__restrict__ wn, const double *__restrict__ part_in, int P, int has_prev, int64_t lc,
+    double *__restrict__ qrow, double *__restrict__ beta_out, double *__restrict__ part_out,
+    const unsigned long long *__restrict__ band)
+{
+    constexpr int NT = kWinThreads, R = kWinRows, M = kWinRing - 1, NI = kWinRing / NT;
+    __shared__ double ring[kWinRing];
+    __shared__ double yrow[R];  // also the slab reduction scratch
+    const int t = threadIdx.x;
+    const int64_t H = (int64_t)*band;
+    const bool win = 2 * H + 2 * R <= kWinRing;  // block-uniform
+    const int64_t c0 = n * blockIdx.x / gridDim.x, c1 = n * (blockIdx.x + 1) / gridDim.x;
+    // first window w[c0 - H, c0 + R + H): all loads in flight, then the slab sum
+    double wi[NI];
+    const int64_t lo = c0 - H < 0 ? 0 : c0 - H, hi = c0 + R + H < n ? c0 + R + H : n;
+#pragma unroll
+    for (int k = 0; k < NI; ++k) {
+        const int64_t i = lo + t + (int64_t)k * NT;
+        wi[k] = (win && i < hi) ? w[i] : 0.0;
+    }
+    const double bsq = block_sum_slabs(part_in, P, yrow);
+    const double beta = sqrt(bsq), rbeta = 1.0 / beta;
+    if (blockIdx.x == 0 && t == 0) *beta_out = beta;
+#pragma unroll
+    for (int k = 0; k < NI; ++k) {
+        const int64_t i = lo + t + (int64_t)k * NT;
+        if (win && i < hi) ring[i & M] = wi[k];
+    }
+    __syncthreads();
+    const double dot = win ? vl_win_tiles<LV, true>(n, c0, c1, H, rp, col, val, w, qbuf, wn, has_prev, lc,
+                                                    qrow, beta, rbeta, ring, yrow)
+                           : vl_win_tiles<LV, false>(n, c0, c1, H, rp, col, val, w, qbuf, wn, has_prev, lc,
+                                                     qrow, beta, rbeta, ring, yrow);
+    block_store_slab(dot, yrow, part_out);
+}
+
 __global__ __launch_bounds__(kVlThreads) void k_vl_update(int64_t n, double *__restrict__ wn,
                                                           const double *__restrict__ q,
                                                           const double *__restrict__ part_in,
@@ -1933,8 +2185,18 @@ int vector_lanczos_dev(lz_handle *h, int64_t n, int64_t nnz, const int64_t *rp, 
 {
     const double mean = n > 0 ? (double)nnz / (double)n : 10.0;
     const int lv = mean <= 5 ? 4 : mean <= 12 ? 8 : mean <= 28 ? 16 : mean <= 60 ? 32 : 64;
-    const int grid = (int)std::max<int64_t>(
-        8, std::min<int64_t>(ceil_div(n, kVlThreads / lv), (int64_t)h->n_cu * 4));
+    // LZ_VL_KERNEL=cs / cs2: the CSR-stream kernel, 512 / 256-row tiles (needs
+    // 16-B aligned col/val).  Default: lanes-per-row.
+    const char *vk = getenv("LZ_VL_KERNEL");
+    const bool al16 = ((uintptr_t)col & 15) == 0 && ((uintptr_t)val & 15) == 0;
+    const int cs = !(vk && al16) ? 0 : !strcmp(vk, "cs") ? 1 : !strcmp(vk, "cs2") ? 2 : 0;
+    // default: the band-window kernel (any operator; the window pays for banded ones)
+    const bool win = !cs && lv <= 8 && !(vk && !strcmp(vk, "row"));
+    const int grid = win       ? (int)std::max<int64_t>(1, std::min<int64_t>(ceil_div(n, kWinRows), (int64_t)h->n_cu))
+                     : cs == 1 ? (int)std::max<int64_t>(8, std::min<int64_t>(ceil_div(n, 512), (int64_t)h->n_cu * 2))
+                     : cs == 2 ? (int)std::max<int64_t>(8, std::min<int64_t>(ceil_div(n, 256), (int64_t)h->n_cu * 5))
+                               : (int)std::max<int64_t>(
+                              8, std::min<int64_t>(ceil_div(n, kVlThreads / lv), (int64_t)h->n_cu * 4));
     const int gridu = (int)std::max<int64_t>(
         8, std::min<int64_t>(ceil_div(n, kVlThreads), (int64_t)h->n_cu * 4));
     // slabs: two alternating regions of h->partials
@@ -1943,6 +2205,13 @@ int vector_lanczos_dev(lz_handle *h, int64_t n, int64_t nnz, const int64_t *rp, 
     hipLaunchKernelGGL(k_vl_sq, dim3(gsq), dim3(kVlThreads), 0, h->stream, n, b, pa);
     LZ_LAUNCH_CHECK();
     int P = gsq;
+    unsigned long long *band = reinterpret_cast<unsigned long long *>(h->partials + 8192);
+    if (win) {
+        LZ_HIP_TRY(hipMemsetAsync(band, 0, sizeof(*band), h->stream));
+        hipLaunchKernelGGL(k_vl_band, dim3((unsigned)std::max<int64_t>(1, std::min<int64_t>(ceil_div(n, 256), h->n_cu * 4))),
+                           dim3(256), 0, h->stream, n, rp, col, band);
+        LZ_LAUNCH_CHECK();
+    }
     const double *wcur = b;
     double *wbuf[2] = {w, q1};
     int wi = 0;
@@ -1954,12 +2223,27 @@ int vector_lanczos_dev(lz_handle *h, int64_t n, int64_t nnz, const int64_t *rp, 
                            col, val, wcur, q0, wnext, pa, P, j > 0 ? 1 : 0, lc, q + j, beta + j, \
                            pb);                                                                 \
         break;
-        switch (lv) {
-            LZ_VL_CASE(4)
-            LZ_VL_CASE(8)
-            LZ_VL_CASE(16)
-            LZ_VL_CASE(32)
-            LZ_VL_CASE(64)
+        if (win) {
+            if (lv == 4)
+                hipLaunchKernelGGL((k_vl_spmv_win<4>), dim3(grid), dim3(kWinThreads), 0, h->stream, n, rp, col, val,
+                                   wcur, q0, wnext, pa, P, j > 0 ? 1 : 0, lc, q + j, beta + j, pb, band);
+            else
+                hipLaunchKernelGGL((k_vl_spmv_win<8>), dim3(grid), dim3(kWinThreads), 0, h->stream, n, rp, col, val,
+                                   wcur, q0, wnext, pa, P, j > 0 ? 1 : 0, lc, q + j, beta + j, pb, band);
+        } else if (cs == 1) {
+            hipLaunchKernelGGL((k_vl_spmv_cs<512, 3>), dim3(grid), dim3(512), 0, h->stream, n, nnz, rp,
+                               col, val, wcur, q0, wnext, pa, P, j > 0 ? 1 : 0, lc, q + j, beta + j, pb);
+        } else if (cs == 2) {
+            hipLaunchKernelGGL((k_vl_spmv_cs<256, 3>), dim3(grid), dim3(256), 0, h->stream, n, nnz, rp,
+                               col, val, wcur, q0, wnext, pa, P, j > 0 ? 1 : 0, lc, q + j, beta + j, pb);
+        } else {
+            switch (lv) {
+                LZ_VL_CASE(4)
+                LZ_VL_CASE(8)
+                LZ_VL_CASE(16)
+                LZ_VL_CASE(32)
+                LZ_VL_CASE(64)
+            }
         }
 #undef LZ_VL_CASE
         LZ_LAUNCH_CHECK();

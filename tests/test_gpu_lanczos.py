@@ -119,6 +119,29 @@ def test_vector_lanczos(lz, orc, handle, torch_cuda, golden):
         assert np.max(np.abs(r - ro)) <= RITZ_TOL
 
 
+@pytest.mark.parametrize("kernel", ["win", "row", "cs", "cs2"])
+def test_vector_lanczos_heavy_tiles(lz, orc, handle, torch_cuda, monkeypatch, kernel):
+    """Power-law rows, every SpMV kernel (LZ_VL_KERNEL): tiles whose CSR run
+    exceeds the CSR-stream kernels' LDS capacity take their wave-per-row path;
+    nnz not a multiple of 4 (tail quad)."""
+    torch = torch_cuda
+    if kernel == "win":  # default: band-window kernel; this operator's band exceeds the ring
+        monkeypatch.delenv("LZ_VL_KERNEL", raising=False)
+    else:
+        monkeypatch.setenv("LZ_VL_KERNEL", kernel)
+    A = lz.gen_powerlaw(60001, 10.0, 1.8, 30000, seed=9, dtype=np.float64)
+    m, lc = 10, 4321
+    bv = lz.uniform_B(A.n, 1, seed=4)[:, 0].copy()
+    kw = dict(dtype=torch.float64, device="cuda")
+    q, al, be = torch.zeros(m, **kw), torch.zeros(m, **kw), torch.zeros(m, **kw)
+    ws = [torch.empty(A.n, **kw) for _ in range(3)]
+    handle.vector_lanczos(lz.CsrDevice.from_host(A), torch.from_numpy(bv).cuda(), m, lc, q, al, be, *ws)
+    qo, ao, bo = orc.vector_lanczos(A, bv, m, lc)
+    assert np.allclose(al.cpu().numpy(), ao, rtol=1e-9, atol=1e-12)
+    assert np.allclose(be.cpu().numpy(), bo, rtol=1e-9)
+    assert np.allclose(q.cpu().numpy(), qo, rtol=1e-9, atol=1e-14)
+
+
 def test_vector_lanczos_golden(lz, handle, torch_cuda, golden):
     torch = torch_cuda
     A = golden_csr(lz, golden, 10)
