@@ -2047,11 +2047,13 @@ __global__ __launch_bounds__(256) void k_vl_band(int64_t n, const int64_t *__res
 // LDS reads instead of ~10 L2 requests each holding a texture-path miss slot
 // (PMC on C2: ~1e7 L2 requests per SpMV, the whole bound of the gather kernels).
 // Operators with 2H + 2R > the ring gather from global memory (same kernel).
-constexpr int kWinThreads = 1024, kWinRows = 1024, kWinRing = 16384;
+// Shapes <threads = tile rows, ring doubles>: <1024, 16384>, one block per CU,
+// for half bands up to 7168; <512, 9216>, two blocks per CU (one block's loads
+// overlap the other's row phase), for half bands up to 4096.
 
 // Tile loop of k_vl_spmv_win; WIN selects LDS-ring or global gathers at
 // compile time (a runtime select would make every gather a flat load).
-template <int LV, bool WIN>
+template <int LV, int NT, int RING, bool WIN>
 __device__ __forceinline__ double vl_win_tiles(int64_t n, int64_t c0, int64_t c1, int64_t H,
                                                const int64_t *__restrict__ rp,
                                                const int32_t *__restrict__ col,
@@ -2061,10 +2063,12 @@ __device__ __forceinline__ double vl_win_tiles(int64_t n, int64_t c0, int64_t c1
                                                double *__restrict__ qrow, double beta, double rbeta,
                                                double *ring, double *yrow)
 {
-    constexpr int NT = kWinThreads, R = kWinRows, M = kWinRing - 1;
+    constexpr int R = NT;
     constexpr int RPP = NT / LV, PASSES = R / RPP;  // rows per pass, passes per tile
     const int t = threadIdx.x, g = t / LV, p = t % LV;
-    auto wat = [&](int64_t i) -> double { return WIN ? ring[i & M] : w[i]; };
+    const int64_t base = c0 - H;  // ring slot of w[i]: (i - base) mod RING
+    auto slot = [&](int64_t i) -> int { return (int)((uint32_t)(i - base) % (uint32_t)RING); };
+    auto wat = [&](int64_t i) -> double { return WIN ? ring[slot(i)] : w[i]; };
     double dot = 0.0;
     for (int64_t r0 = c0; r0 < c1; r0 += R) {
         const int rows = (int)(c1 - r0 < R ? c1 - r0 : R);
@@ -2115,26 +2119,26 @@ __device__ __forceinline__ double vl_win_tiles(int64_t n, int64_t c0, int64_t c1
             dot = fma(wv, qj, dot);
             if (erow == lc) *qrow = qj;
         }
-        if (WIN && si < n) ring[si & M] = slab;  // disjoint from this tile's window (2H + 2R <= ring)
+        if (WIN && si < n) ring[slot(si)] = slab;  // disjoint from this tile's window (2H + 2R <= ring)
         __syncthreads();
     }
     return dot;
 }
 
-template <int LV>
-__global__ __launch_bounds__(kWinThreads) void k_vl_spmv_win(
+template <int LV, int NT, int RING>
+__global__ __launch_bounds__(NT) void k_vl_spmv_win(
     int64_t n, const int64_t *__restrict__ rp, const int32_t *__restrict__ col,
     const double *__restrict__ val, const double *__restrict__ w, double *__restrict__ qbuf,
     double *__restrict__ wn, const double *__restrict__ part_in, int P, int has_prev, int64_t lc,
     double *__restrict__ qrow, double *__restrict__ beta_out, double *__restrict__ part_out,
     const unsigned long long *__restrict__ band)
 {
-    constexpr int NT = kWinThreads, R = kWinRows, M = kWinRing - 1, NI = kWinRing / NT;
-    __shared__ double ring[kWinRing];
+    constexpr int R = NT, NI = (RING + NT - 1) / NT;
+    __shared__ double ring[RING];
     __shared__ double yrow[R];  // also the slab reduction scratch
     const int t = threadIdx.x;
     const int64_t H = (int64_t)*band;
-    const bool win = 2 * H + 2 * R <= kWinRing;  // block-uniform
+    const bool win = 2 * H + 2 * R <= RING;  // block-uniform
     const int64_t c0 = n * blockIdx.x / gridDim.x, c1 = n * (blockIdx.x + 1) / gridDim.x;
     // first window w[c0 - H, c0 + R + H): all loads in flight, then the slab sum
     double wi[NI];
@@ -2150,13 +2154,13 @@ __global__ __launch_bounds__(kWinThreads) void k_vl_spmv_win(
 #pragma unroll
     for (int k = 0; k < NI; ++k) {
         const int64_t i = lo + t + (int64_t)k * NT;
-        if (win && i < hi) ring[i & M] = wi[k];
+        if (win && i < hi) ring[(int)((uint32_t)(i - (c0 - H)) % (uint32_t)RING)] = wi[k];
     }
     __syncthreads();
-    const double dot = win ? vl_win_tiles<LV, true>(n, c0, c1, H, rp, col, val, w, qbuf, wn, has_prev, lc,
-                                                    qrow, beta, rbeta, ring, yrow)
-                           : vl_win_tiles<LV, false>(n, c0, c1, H, rp, col, val, w, qbuf, wn, has_prev, lc,
-                                                     qrow, beta, rbeta, ring, yrow);
+    const double dot = win ? vl_win_tiles<LV, NT, RING, true>(n, c0, c1, H, rp, col, val, w, qbuf, wn, has_prev,
+                                                              lc, qrow, beta, rbeta, ring, yrow)
+                           : vl_win_tiles<LV, NT, RING, false>(n, c0, c1, H, rp, col, val, w, qbuf, wn, has_prev,
+                                                               lc, qrow, beta, rbeta, ring, yrow);
     block_store_slab(dot, yrow, part_out);
 }
 
@@ -2186,13 +2190,29 @@ int vector_lanczos_dev(lz_handle *h, int64_t n, int64_t nnz, const int64_t *rp, 
     const double mean = n > 0 ? (double)nnz / (double)n : 10.0;
     const int lv = mean <= 5 ? 4 : mean <= 12 ? 8 : mean <= 28 ? 16 : mean <= 60 ? 32 : 64;
     // LZ_VL_KERNEL=cs / cs2: the CSR-stream kernel, 512 / 256-row tiles (needs
-    // 16-B aligned col/val).  Default: lanes-per-row.
+    // 16-B aligned col/val); row: lanes-per-row; win512 / win1024: one band-window
+    // shape.  Default: the band window whose ring holds the operator's half band
+    // (measured once per solve: one host sync), else lanes-per-row.
     const char *vk = getenv("LZ_VL_KERNEL");
     const bool al16 = ((uintptr_t)col & 15) == 0 && ((uintptr_t)val & 15) == 0;
     const int cs = !(vk && al16) ? 0 : !strcmp(vk, "cs") ? 1 : !strcmp(vk, "cs2") ? 2 : 0;
-    // default: the band-window kernel (any operator; the window pays for banded ones)
-    const bool win = !cs && lv <= 8 && !(vk && !strcmp(vk, "row"));
-    const int grid = win       ? (int)std::max<int64_t>(1, std::min<int64_t>(ceil_div(n, kWinRows), (int64_t)h->n_cu))
+    unsigned long long *band = reinterpret_cast<unsigned long long *>(h->partials + 8192);
+    int win = 0;  // 1: <512, 9216>, 2: <1024, 16384>
+    if (!cs && lv <= 8 && !(vk && !strcmp(vk, "row"))) {
+        LZ_HIP_TRY(hipMemsetAsync(band, 0, sizeof(*band), h->stream));
+        hipLaunchKernelGGL(k_vl_band, dim3((unsigned)std::max<int64_t>(1, std::min<int64_t>(ceil_div(n, 256), h->n_cu * 4))),
+                           dim3(256), 0, h->stream, n, rp, col, band);
+        LZ_LAUNCH_CHECK();
+        unsigned long long H = 0;
+        LZ_HIP_TRY(hipMemcpyAsync(&H, band, sizeof(H), hipMemcpyDeviceToHost, h->stream));
+        LZ_HIP_TRY(hipStreamSynchronize(h->stream));
+        win = (vk && !strcmp(vk, "win512")) ? 1 : (vk && !strcmp(vk, "win1024")) ? 2
+              : 2 * H + 2 * 512 <= 9216     ? 1
+              : 2 * H + 2 * 1024 <= 16384   ? 2
+                                            : 0;
+    }
+    const int grid = win == 1  ? (int)std::max<int64_t>(1, std::min<int64_t>(ceil_div(n, 512), (int64_t)h->n_cu * 2))
+                     : win == 2 ? (int)std::max<int64_t>(1, std::min<int64_t>(ceil_div(n, 1024), (int64_t)h->n_cu))
                      : cs == 1 ? (int)std::max<int64_t>(8, std::min<int64_t>(ceil_div(n, 512), (int64_t)h->n_cu * 2))
                      : cs == 2 ? (int)std::max<int64_t>(8, std::min<int64_t>(ceil_div(n, 256), (int64_t)h->n_cu * 5))
                                : (int)std::max<int64_t>(
@@ -2205,13 +2225,6 @@ int vector_lanczos_dev(lz_handle *h, int64_t n, int64_t nnz, const int64_t *rp, 
     hipLaunchKernelGGL(k_vl_sq, dim3(gsq), dim3(kVlThreads), 0, h->stream, n, b, pa);
     LZ_LAUNCH_CHECK();
     int P = gsq;
-    unsigned long long *band = reinterpret_cast<unsigned long long *>(h->partials + 8192);
-    if (win) {
-        LZ_HIP_TRY(hipMemsetAsync(band, 0, sizeof(*band), h->stream));
-        hipLaunchKernelGGL(k_vl_band, dim3((unsigned)std::max<int64_t>(1, std::min<int64_t>(ceil_div(n, 256), h->n_cu * 4))),
-                           dim3(256), 0, h->stream, n, rp, col, band);
-        LZ_LAUNCH_CHECK();
-    }
     const double *wcur = b;
     double *wbuf[2] = {w, q1};
     int wi = 0;
@@ -2224,12 +2237,15 @@ int vector_lanczos_dev(lz_handle *h, int64_t n, int64_t nnz, const int64_t *rp, 
                            pb);                                                                 \
         break;
         if (win) {
-            if (lv == 4)
-                hipLaunchKernelGGL((k_vl_spmv_win<4>), dim3(grid), dim3(kWinThreads), 0, h->stream, n, rp, col, val,
-                                   wcur, q0, wnext, pa, P, j > 0 ? 1 : 0, lc, q + j, beta + j, pb, band);
-            else
-                hipLaunchKernelGGL((k_vl_spmv_win<8>), dim3(grid), dim3(kWinThreads), 0, h->stream, n, rp, col, val,
-                                   wcur, q0, wnext, pa, P, j > 0 ? 1 : 0, lc, q + j, beta + j, pb, band);
+#define LZ_VL_WIN(LV, NT, RING)                                                                            \
+    hipLaunchKernelGGL((k_vl_spmv_win<LV, NT, RING>), dim3(grid), dim3(NT), 0, h->stream, n, rp, col, val, \
+                       wcur, q0, wnext, pa, P, j > 0 ? 1 : 0, lc, q + j, beta + j, pb, band)
+            if (win == 1) {
+                if (lv == 4) LZ_VL_WIN(4, 512, 9216); else LZ_VL_WIN(8, 512, 9216);
+            } else {
+                if (lv == 4) LZ_VL_WIN(4, 1024, 16384); else LZ_VL_WIN(8, 1024, 16384);
+            }
+#undef LZ_VL_WIN
         } else if (cs == 1) {
             hipLaunchKernelGGL((k_vl_spmv_cs<512, 3>), dim3(grid), dim3(512), 0, h->stream, n, nnz, rp,
                                col, val, wcur, q0, wnext, pa, P, j > 0 ? 1 : 0, lc, q + j, beta + j, pb);

@@ -142,6 +142,39 @@ def test_vector_lanczos_heavy_tiles(lz, orc, handle, torch_cuda, monkeypatch, ke
     assert np.allclose(q.cpu().numpy(), qo, rtol=1e-9, atol=1e-14)
 
 
+@pytest.mark.parametrize("n,H,kernel", [(600013, 4096, None), (600013, 4097, None), (600013, 7168, None),
+                                        (600013, 7169, None), (60013, 7168, None), (60013, 7168, "win512")])
+def test_vector_lanczos_band_window_edge(lz, orc, handle, torch_cuda, monkeypatch, n, H, kernel):
+    """Half bands at each band-window shape's limit (2H + 2R <= ring: 4096 for
+    <512, 9216>, 7168 for <1024, 16384>) and one past it; several tiles per
+    block and blocks with a single partial tile; a forced shape whose ring is
+    too small (the kernel's global-gather instantiation)."""
+    import scipy.sparse as sp
+    torch = torch_cuda
+    if kernel:
+        monkeypatch.setenv("LZ_VL_KERNEL", kernel)
+    else:
+        monkeypatch.delenv("LZ_VL_KERNEL", raising=False)
+    A0 = lz.gen_banded(n, 8.0, 3000, seed=H)
+    M = sp.csr_matrix((A0.val, A0.col, A0.row_ptr), shape=(n, n))
+    r = np.array([17, n - 1 - H, n // 2])
+    E = sp.coo_matrix((np.full(6, 0.01), (np.r_[r, r + H], np.r_[r + H, r])), shape=(n, n))
+    M = (M + E).tocsr()
+    M.sort_indices()
+    A = lz.CsrHost(n, M.indptr.astype(np.int64), M.indices.astype(np.int32), M.data.astype(np.float64))
+    assert np.max(np.abs(M.indices - np.repeat(np.arange(n), np.diff(M.indptr)))) == H
+    m, lc = 10, n // 3
+    bv = lz.uniform_B(n, 1, seed=5)[:, 0].copy()
+    kw = dict(dtype=torch.float64, device="cuda")
+    q, al, be = torch.zeros(m, **kw), torch.zeros(m, **kw), torch.zeros(m, **kw)
+    ws = [torch.empty(n, **kw) for _ in range(3)]
+    handle.vector_lanczos(lz.CsrDevice.from_host(A), torch.from_numpy(bv).cuda(), m, lc, q, al, be, *ws)
+    qo, ao, bo = orc.vector_lanczos(A, bv, m, lc)
+    assert np.allclose(al.cpu().numpy(), ao, rtol=1e-9, atol=1e-12)
+    assert np.allclose(be.cpu().numpy(), bo, rtol=1e-9)
+    assert np.allclose(q.cpu().numpy(), qo, rtol=1e-9, atol=1e-14)
+
+
 def test_vector_lanczos_golden(lz, handle, torch_cuda, golden):
     torch = torch_cuda
     A = golden_csr(lz, golden, 10)
