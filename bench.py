@@ -103,6 +103,8 @@ def main():
     ap.add_argument("--spmm-reps", type=int, default=20)
     ap.add_argument("--c2-steps", type=int, default=200, help="single-vector Lanczos steps at BASELINE config 1 (0: skip)")
     ap.add_argument("--c5-steps", type=int, default=10, help="block-32 fp32 power-law steps at BASELINE config 4 (0: skip)")
+    ap.add_argument("--rand-steps", type=int, default=10,
+                    help="block-Lanczos steps on the C3 uniform-random-column stress operator (0: skip)")
     ap.add_argument("--exchange", choices=["halo", "allgather"], default="halo",
                     help="multi-GPU Krylov-block exchange (N > 1, or with --dist at N = 1)")
     ap.add_argument("--dist", action="store_true",
@@ -262,6 +264,37 @@ def main():
               "finite": bool(torch.isfinite(al5).all())}
         del A5d, B5, P5
 
+    # ---- C3 stress case: uniform-random columns (half width = n), same n, nnz/row, b
+    c3r = None
+    if world == 1 and not dist_path and args.rand_steps > 0:
+        kr = args.rand_steps
+        Ar = lz.gen_banded(n, args.nnz_per_row, n, seed + 7)
+        Ard = lz.CsrDevice.from_host(Ar)
+        Yr = torch.empty(n, b, **kw)
+        h.spmm(Ard, Bd, Yr)
+        torch.cuda.synchronize()
+        h.prof_enable(True)
+        for _ in range(5):
+            h.spmm(Ard, Bd, Yr)
+        torch.cuda.synchronize()
+        ms_r, cnt_r = h.prof_read(h.PROF_SPMM)
+        h.prof_enable(False)
+        qr, alr, ber = torch.zeros(kr * b, **kw), torch.zeros(kr, b, b, **kw), torch.zeros(kr + 1, b, b, **kw)
+        h.block_lanczos_blas(Ard, Bd, 2, 84, qr, alr, ber, Q0, Q1, W)  # warm
+        torch.cuda.synchronize()
+        t0c = time.perf_counter()
+        h.block_lanczos_blas(Ard, Bd, kr, 84, qr, alr, ber, Q0, Q1, W)
+        torch.cuda.synchronize()
+        dtr = time.perf_counter() - t0c
+        t_sp = ms_r / cnt_r * 1e-3
+        c3r = {"workload": f"C3 stress: uniform-random columns (half width n), b={b} fp64, n={n} nnz={Ar.nnz}",
+               "iters_per_s": round(kr / dtr, 2), "ms_per_iter": round(dtr / kr * 1e3, 3),
+               "spmm_ms": round(t_sp * 1e3, 4),
+               "spmm_GBs": round(spmm_bytes(n, Ar.nnz, b) / t_sp / 1e9, 1),
+               "spmm_frac_of_hbm_peak": round(spmm_bytes(n, Ar.nnz, b) / t_sp / 1e9 / HBM_PEAK_GBS, 4),
+               "finite": bool(torch.isfinite(alr).all())}
+        del Ard, Yr
+
     # ---- CPU baseline: the oracle (C, OpenMP) on this operator, rank 0, N = 1
     cpu = None
     if world == 1 and rank == 0 and not args.no_cpu_baseline:
@@ -319,6 +352,7 @@ def main():
                 "plain_spmm": plain,
                 "c2_vector_lanczos": c2,
                 "c5_block32_f32_powerlaw": c5,
+                "c3_random_columns_stress": c3r,
                 "kernel_ms_per_step": {"fused_spmm_pass": round(spmm_ms / K, 4),
                                        "update_pass": round(upd_ms / K, 4),
                                        "finish_sqrtm": round(small_ms / K, 4),
