@@ -24,9 +24,11 @@
 namespace lz {
 
 // ============================================================== Gram slabs
-template <bool SAME>
-__global__ __launch_bounds__(512) void k_gram16_f64(int64_t n, const double *__restrict__ X,
-                                                    const double *__restrict__ Y,
+// b = 16 Gram slabs on v_mfma_f64_16x16x4f64; T = double or float (fp32 blocks
+// are widened on load and accumulated in fp64, as every other fp32 reduction here).
+template <typename T, bool SAME>
+__global__ __launch_bounds__(512) void k_gram16_f64(int64_t n, const T *__restrict__ X,
+                                                    const T *__restrict__ Y,
                                                     double *__restrict__ part)
 {
     __shared__ double red[8][256];
@@ -43,8 +45,8 @@ __global__ __launch_bounds__(512) void k_gram16_f64(int64_t n, const double *__r
             const int64_t uu = u + t * s.step;
             const int64_t e = (uu * 8 + w) * 64 + lane;
             const bool ok = (uu < s.end) && (e < nel);
-            xa[t] = ok ? X[e] : 0.0;
-            ya[t] = SAME ? xa[t] : (ok ? Y[e] : 0.0);
+            xa[t] = ok ? (double)X[e] : 0.0;
+            ya[t] = SAME ? xa[t] : (ok ? (double)Y[e] : 0.0);
         }
 #pragma unroll
         for (int t = 0; t < U; ++t) acc = mfma16(xa[t], ya[t], acc);
@@ -210,28 +212,18 @@ template <typename T>
 int gram_partials(lz_handle *h, int64_t n, int b, const T *X, const T *Y, int64_t ld, int *nparts)
 {
     LZ_ARG_CHECK(b >= 1 && b <= kMaxB, "b out of range");
-    if constexpr (std::is_same<T, double>::value) {
-        if (b == 16 && ld == 16) {
-            const int64_t units = ceil_div(ceil_div(n, 4), 8);
-            const int grid = (int)std::max<int64_t>(1, std::min<int64_t>(units, h->n_cu));
-            if (X == Y)
-                {
-                const int ev_ = prof_begin(h, PROF_GRAM);
-                hipLaunchKernelGGL((k_gram16_f64<true>), dim3(grid), dim3(512), 0, h->stream, n, X,
-                                   Y, h->partials);
-                prof_end(h, ev_);
-                }
-            else
-                {
-                const int ev_ = prof_begin(h, PROF_GRAM);
-                hipLaunchKernelGGL((k_gram16_f64<false>), dim3(grid), dim3(512), 0, h->stream, n,
-                                   X, Y, h->partials);
-                prof_end(h, ev_);
-                }
-            LZ_LAUNCH_CHECK();
-            *nparts = grid;
-            return LZ_OK;
-        }
+    if (b == 16 && ld == 16) {  // fp64 and fp32
+        const int64_t units = ceil_div(ceil_div(n, 4), 8);
+        const int grid = (int)std::max<int64_t>(1, std::min<int64_t>(units, h->n_cu));
+        const int ev_ = prof_begin(h, PROF_GRAM);
+        if (X == Y)
+            hipLaunchKernelGGL((k_gram16_f64<T, true>), dim3(grid), dim3(512), 0, h->stream, n, X, Y, h->partials);
+        else
+            hipLaunchKernelGGL((k_gram16_f64<T, false>), dim3(grid), dim3(512), 0, h->stream, n, X, Y, h->partials);
+        prof_end(h, ev_);
+        LZ_LAUNCH_CHECK();
+        *nparts = grid;
+        return LZ_OK;
     }
     if constexpr (std::is_same<T, float>::value) {
         if (b == 32 && ld == 32) {
@@ -610,17 +602,20 @@ int sqrtm_pair(lz_handle *h, int b, const T *G, int nparts, T *beta, T *beta_inv
 }
 
 // ==================================================================== Q * S
+// W = sw W + sq Q S at b = 16 on v_mfma_f64_16x16x4f64; T = double or float
+// (fp32 operands widened on load, the result rounded once on store).
+template <typename T>
 __global__ __launch_bounds__(512) void k_tsmm16_f64(int64_t n, double sw, double sq,
-                                                    const double *__restrict__ Q,
-                                                    const double *__restrict__ S,
-                                                    double *__restrict__ W)
+                                                    const T *__restrict__ Q,
+                                                    const T *__restrict__ S,
+                                                    T *__restrict__ W)
 {
     __shared__ double tile[8][16 * 17];
     const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
-    double *T = tile[w];
+    double *tl = tile[w];
     double sb[4];
 #pragma unroll
-    for (int kc = 0; kc < 4; ++kc) sb[kc] = sq * S[(4 * kc + (lane >> 4)) * 16 + (lane & 15)];
+    for (int kc = 0; kc < 4; ++kc) sb[kc] = sq * (double)S[(4 * kc + (lane >> 4)) * 16 + (lane & 15)];
     const int64_t ntile = ceil_div(n, 16);
     XcdSched s(ceil_div(ntile, 8));
     for (int64_t u = s.begin; u < s.end; u += s.step) {
@@ -629,29 +624,34 @@ __global__ __launch_bounds__(512) void k_tsmm16_f64(int64_t n, double sw, double
         const int64_t qrow = r0 + (lane >> 2);
         double qv[4] = {0.0, 0.0, 0.0, 0.0};
         if (qrow < n) {
-            const double2 *src = reinterpret_cast<const double2 *>(Q + qrow * 16 + 4 * (lane & 3));
-            const double2 a = src[0], b2 = src[1];
-            qv[0] = a.x; qv[1] = a.y; qv[2] = b2.x; qv[3] = b2.y;
+            if constexpr (std::is_same<T, double>::value) {
+                const double2 *src = reinterpret_cast<const double2 *>(Q + qrow * 16 + 4 * (lane & 3));
+                const double2 a = src[0], b2 = src[1];
+                qv[0] = a.x; qv[1] = a.y; qv[2] = b2.x; qv[3] = b2.y;
+            } else {
+                const float4 a = *reinterpret_cast<const float4 *>(Q + qrow * 16 + 4 * (lane & 3));
+                qv[0] = a.x; qv[1] = a.y; qv[2] = a.z; qv[3] = a.w;
+            }
         }
         d4_t acc;
 #pragma unroll
         for (int r = 0; r < 4; ++r) {
             const int64_t row = r0 + (lane >> 4) + 4 * r;
-            acc[r] = (sw != 0.0 && row < n) ? sw * W[r0 * 16 + 64 * r + lane] : 0.0;
+            acc[r] = (sw != 0.0 && row < n) ? sw * (double)W[r0 * 16 + 64 * r + lane] : 0.0;
         }
 #pragma unroll
-        for (int i = 0; i < 4; ++i) T[(lane >> 2) * 17 + 4 * (lane & 3) + i] = qv[i];
+        for (int i = 0; i < 4; ++i) tl[(lane >> 2) * 17 + 4 * (lane & 3) + i] = qv[i];
         wave_lds_sync();
         double a[4];
 #pragma unroll
-        for (int kc = 0; kc < 4; ++kc) a[kc] = T[(lane & 15) * 17 + 4 * kc + (lane >> 4)];
+        for (int kc = 0; kc < 4; ++kc) a[kc] = tl[(lane & 15) * 17 + 4 * kc + (lane >> 4)];
         wave_lds_sync();
 #pragma unroll
         for (int kc = 0; kc < 4; ++kc) acc = mfma16(a[kc], sb[kc], acc);
 #pragma unroll
         for (int r = 0; r < 4; ++r) {
             const int64_t row = r0 + (lane >> 4) + 4 * r;
-            if (row < n) W[r0 * 16 + 64 * r + lane] = acc[r];
+            if (row < n) W[r0 * 16 + 64 * r + lane] = (T)acc[r];
         }
     }
 }
@@ -745,19 +745,15 @@ int tsmm(lz_handle *h, int64_t n, int b, T sw, T sq, const T *Q, const T *S, T *
 {
     LZ_ARG_CHECK(b >= 1 && b <= kMaxB && ld >= b, "tsmm shape");
     if (n <= 0) return LZ_OK;
-    if constexpr (std::is_same<T, double>::value) {
-        if (b == 16 && ld == 16) {
-            const int64_t units = ceil_div(ceil_div(n, 16), 8);
-            const int grid = (int)std::max<int64_t>(1, std::min<int64_t>(units, h->n_cu * 2));
-            {
-            const int ev_ = prof_begin(h, PROF_TSMM);
-            hipLaunchKernelGGL(k_tsmm16_f64, dim3(grid), dim3(512), 0, h->stream, n, sw, sq, Q, S,
-                               W);
-            prof_end(h, ev_);
-            }
-            LZ_LAUNCH_CHECK();
-            return LZ_OK;
-        }
+    if (b == 16 && ld == 16) {  // fp64 and fp32
+        const int64_t units = ceil_div(ceil_div(n, 16), 8);
+        const int grid = (int)std::max<int64_t>(1, std::min<int64_t>(units, h->n_cu * 2));
+        const int ev_ = prof_begin(h, PROF_TSMM);
+        hipLaunchKernelGGL((k_tsmm16_f64<T>), dim3(grid), dim3(512), 0, h->stream, n, (double)sw, (double)sq, Q, S,
+                           W);
+        prof_end(h, ev_);
+        LZ_LAUNCH_CHECK();
+        return LZ_OK;
     }
     if constexpr (std::is_same<T, float>::value) {
         if (b == 32 && ld == 32) {

@@ -150,15 +150,17 @@ def test_tsmm(lz, handle, torch_cuda, b, n, sw):
     assert np.all(np.abs(Wd.cpu().numpy() - ref) <= 64 * EPS[np.float64] * bound)
 
 
+@pytest.mark.parametrize("b", [16, 32])
 @pytest.mark.parametrize("n", [5000, 131, 128])
 @pytest.mark.parametrize("sw", [0.0, 1.0])
-def test_tsmm_f32(lz, handle, torch_cuda, n, sw):
-    """b = 32 fp32: the 32x32x2 MFMA kernel (transposed product, 16-B row pieces)."""
+def test_tsmm_f32(lz, handle, torch_cuda, b, n, sw):
+    """fp32: b = 32 on the 32x32x2 MFMA kernel (transposed product, 16-B row
+    pieces); b = 16 on the f64 16x16x4 kernel (operands widened on load)."""
     torch = torch_cuda
-    rng = np.random.default_rng(3 + n)
-    Q = rng.uniform(-1, 1, (n, 32)).astype(np.float32)
-    S = rng.uniform(-1, 1, (32, 32)).astype(np.float32)
-    W0 = rng.uniform(-1, 1, (n, 32)).astype(np.float32)
+    rng = np.random.default_rng(3 + n + b)
+    Q = rng.uniform(-1, 1, (n, b)).astype(np.float32)
+    S = rng.uniform(-1, 1, (b, b)).astype(np.float32)
+    W0 = rng.uniform(-1, 1, (n, b)).astype(np.float32)
     W = torch.from_numpy(W0.copy()).cuda()
     handle.mm_ts(sw, -0.5, torch.from_numpy(Q).cuda(), torch.from_numpy(S).cuda(), W)
     ref = sw * W0.astype(np.float64) - 0.5 * (Q.astype(np.float64) @ S.astype(np.float64))
@@ -166,15 +168,17 @@ def test_tsmm_f32(lz, handle, torch_cuda, n, sw):
     assert np.all(np.abs(W.cpu().numpy() - ref) <= 64 * EPS[np.float32] * bound)
 
 
+@pytest.mark.parametrize("b", [16, 32])
 @pytest.mark.parametrize("n", [100003, 77])
-def test_gram_f32_b32(lz, handle, torch_cuda, n):
-    """b = 32 fp32 Gram and symmetric cross-Gram on the 32x32x2 MFMA kernel."""
+def test_gram_f32(lz, handle, torch_cuda, b, n):
+    """fp32 Gram and symmetric cross-Gram: b = 32 on the 32x32x2 MFMA kernel,
+    b = 16 on the f64 16x16x4 kernel."""
     torch = torch_cuda
-    rng = np.random.default_rng(n)
-    W = rng.uniform(-1, 1, (n, 32)).astype(np.float32)
-    Q = rng.uniform(-1, 1, (n, 32)).astype(np.float32)
+    rng = np.random.default_rng(n + b)
+    W = rng.uniform(-1, 1, (n, b)).astype(np.float32)
+    Q = rng.uniform(-1, 1, (n, b)).astype(np.float32)
     W64, Q64 = W.astype(np.float64), Q.astype(np.float64)
-    R = torch.empty(32, 32, dtype=torch.float32, device="cuda")
+    R = torch.empty(b, b, dtype=torch.float32, device="cuda")
     handle.mm_tt(torch.from_numpy(W).cuda(), R)
     bound = np.abs(W64).T @ np.abs(W64)
     assert np.all(np.abs(R.cpu().numpy() - W64.T @ W64) <= 64 * EPS[np.float32] * bound)
