@@ -57,6 +57,7 @@ HIP_SYMBOLS = [
     ("lz_version", ctypes.c_char_p, []),
     ("lz_device_ok", _c_int, [_c_int]),
     ("lz_device_error", _c_int, [_c_vp, ctypes.POINTER(_c_int)]),
+    ("lz_debug_poison_lds", _c_int, [_c_vp, ctypes.c_uint32]),
     ("lz_prof_enable", _c_int, [_c_vp, _c_int]),
     ("lz_prof_read", _c_int, [_c_vp, _c_int, ctypes.POINTER(_c_dbl), ctypes.POINTER(_c_int)]),
     ("lz_csr_spmm", _c_int, [_c_vp, _c_i64, _c_i64, _c_i64, _c_vp, _c_vp, _c_vp, _c_int, _c_int,
@@ -534,6 +535,10 @@ class Handle:
         c = _c_int()
         _check(self.L.lz_device_error(self._h, ctypes.byref(c)), "lz_device_error")
         return c.value
+
+    def debug_poison_lds(self, pattern: int = 0xFFFFFFFF):
+        """Fill every CU's LDS with `pattern` (test support: stale-LDS reads show as NaN)."""
+        _check(self.L.lz_debug_poison_lds(self._h, pattern), "lz_debug_poison_lds")
 
     def prof_enable(self, on: bool = True):
         _check(self.L.lz_prof_enable(self._h, int(on)), "lz_prof_enable")

@@ -525,6 +525,22 @@ int lz_device_error(lz_handle *h, int *code)
     return LZ_OK;
 }
 
+__global__ __launch_bounds__(1024) void k_poison_lds(uint32_t pattern)
+{
+    constexpr int kWords = 160 * 1024 / 4;
+    __shared__ uint32_t lds[kWords];
+    volatile uint32_t *v = lds;
+    for (int i = threadIdx.x; i < kWords; i += blockDim.x) v[i] = pattern;
+}
+
+int lz_debug_poison_lds(lz_handle *h, uint32_t pattern)
+{
+    LZ_HANDLE_CHECK(h);
+    hipLaunchKernelGGL(k_poison_lds, dim3(h->n_cu * 4), dim3(1024), 0, h->stream, pattern);
+    LZ_LAUNCH_CHECK();
+    return LZ_OK;
+}
+
 int lz_prof_enable(lz_handle *h, int on)
 {
     LZ_HANDLE_CHECK(h);

@@ -937,9 +937,13 @@ __global__ __launch_bounds__(64 * (NC + NL)) void k_fused_pp16(
     // epilogue of the pending strip: Y parked in S0 (swizzled), W/Q rows in wv/qv
     auto epilogue = [&]() {
         const int ar = lane & 15;
+        // rows past n: the parked tile holds whatever the LDS held (a strip
+        // past the end has no row order, so only its row 0 is written); they
+        // must not reach the slab accumulation as NaN * 0
+        const bool live_row = s0p + ar < n;
         double ya[4];
 #pragma unroll
-        for (int kc = 0; kc < 4; ++kc) ya[kc] = S0[fw_sw(ar, 4 * (lane >> 4) + kc)];
+        for (int kc = 0; kc < 4; ++kc) ya[kc] = live_row ? S0[fw_sw(ar, 4 * (lane >> 4) + kc)] : 0.0;
         d4_t q1 = {0.0, 0.0, 0.0, 0.0}, wn = {0.0, 0.0, 0.0, 0.0};
 #pragma unroll
         for (int kc = 0; kc < 4; ++kc) q1 = mfma16(wa[kc], ops[0][64 * kc + lane], q1);

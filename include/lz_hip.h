@@ -63,6 +63,11 @@ int lz_device_ok(int device);
  * results are then invalid).  0 in normal operation. */
 int lz_device_error(lz_handle *h, int *code);
 
+/* Test support: fills the LDS of every CU with a 32-bit pattern (0xFFFFFFFF
+ * reads back as a double NaN) on the handle's stream, so a kernel that reads
+ * LDS it did not write shows it deterministically instead of by chance. */
+int lz_debug_poison_lds(lz_handle *h, uint32_t pattern);
+
 int lz_prof_enable(lz_handle *h, int on);
 int lz_prof_read(lz_handle *h, int kernel_class, double *ms_total, int *count);
 

@@ -48,3 +48,15 @@ def torch_cuda():
 def golden_csr(lz, g, N, bug=False):
     tag = "_bug" if bug else ""
     return lz.CsrHost(int(g[f"N{N}_n"]), g[f"N{N}{tag}_row_ptr"], g[f"N{N}{tag}_col"], g[f"N{N}{tag}_val"])
+
+
+@pytest.fixture(autouse=True)
+def _poison_lds(request):
+    """Before every GPU test, fill each CU's LDS with NaN bit patterns
+    (lz_debug_poison_lds), so a kernel that reads LDS it never wrote fails
+    deterministically rather than when the previous kernel left garbage."""
+    if request.node.get_closest_marker("gpu") is not None:
+        h = request.getfixturevalue("handle")
+        request.getfixturevalue("torch_cuda")
+        h.debug_poison_lds()
+    yield

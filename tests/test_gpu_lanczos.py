@@ -48,6 +48,24 @@ def test_block_b16_banded(lz, orc, handle, torch_cuda, fused, m):
     assert np.allclose(got[2][m], ref[2][m], rtol=1e-9, atol=1e-12)
 
 
+@pytest.mark.parametrize("n", [50021, 1000 * 16 + 11, 224 * 40 + 16 * 3 + 5])
+def test_block_b16_stale_lds(lz, orc, handle, torch_cuda, n):
+    """Every CU's LDS filled with NaN bit patterns before each fused pass: a
+    last tile whose trailing strips lie past n (no row order staged for them)
+    must not carry unwritten LDS into the slabs (it once made alpha NaN by chance)."""
+    A = lz.gen_banded(n, 10.0, 512, seed=n)
+    B = lz.uniform_B(A.n, 16, seed=6)
+    m, lc = 4, n // 2
+    Ad = lz.CsrDevice.from_host(A)
+    handle.debug_poison_lds()
+    torch_cuda.cuda.synchronize()
+    q, al, be = lz.run_block_lanczos(handle, Ad, torch_cuda.from_numpy(B).cuda(), m, lc)
+    torch_cuda.cuda.synchronize()
+    got = (q.cpu().numpy(), al.cpu().numpy(), be.cpu().numpy())
+    assert np.isfinite(got[1]).all() and np.isfinite(got[2]).all()
+    assert_close_run(lz, m, 16, got, orc.block_lanczos(A, B, m, lc))
+
+
 def test_block_b16_tail_rows(lz, orc, handle, torch_cuda):
     """n not a multiple of the 16-row tiles, lc in the last partial tile."""
     A = lz.gen_banded(1000 * 16 + 11, 7.0, 64, seed=2)
