@@ -538,6 +538,11 @@ int lz_debug_poison_lds(lz_handle *h, uint32_t pattern)
     LZ_HANDLE_CHECK(h);
     hipLaunchKernelGGL(k_poison_lds, dim3(h->n_cu * 4), dim3(1024), 0, h->stream, pattern);
     LZ_LAUNCH_CHECK();
+    // and the handle's slab / scratch workspaces (nothing may read them before writing)
+    const int byte = (int)(pattern & 0xFF);
+    LZ_HIP_TRY(hipMemsetAsync(h->partials, byte, sizeof(double) * h->partials_cap, h->stream));
+    LZ_HIP_TRY(hipMemsetAsync(h->partials2, byte, sizeof(double) * (256 * kMaxB * kMaxB + 4096 * 256), h->stream));
+    LZ_HIP_TRY(hipMemsetAsync(h->scratch, byte, sizeof(double) * 8 * kMaxB * kMaxB, h->stream));
     return LZ_OK;
 }
 

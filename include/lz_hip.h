@@ -64,8 +64,9 @@ int lz_device_ok(int device);
 int lz_device_error(lz_handle *h, int *code);
 
 /* Test support: fills the LDS of every CU with a 32-bit pattern (0xFFFFFFFF
- * reads back as a double NaN) on the handle's stream, so a kernel that reads
- * LDS it did not write shows it deterministically instead of by chance. */
+ * reads back as a double NaN), and the handle's slab and scratch workspaces
+ * with its low byte, on the handle's stream, so a kernel that reads LDS or
+ * workspace it did not write shows it deterministically instead of by chance. */
 int lz_debug_poison_lds(lz_handle *h, uint32_t pattern);
 
 int lz_prof_enable(lz_handle *h, int on);
