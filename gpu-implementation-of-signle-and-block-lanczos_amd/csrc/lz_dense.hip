@@ -26,6 +26,63 @@ namespace lz {
 // ============================================================== Gram slabs
 // b = 16 Gram slabs on v_mfma_f64_16x16x4f64; T = double or float (fp32 blocks
 // are widened on load and accumulated in fp64, as every other fp32 reduction here).
+// fp32 b = 16 Gram slabs: a lane loads 16 B (4 columns of one row), so one
+// wave-instruction brings a whole 16-row tile (4x fewer loads than one element
+// per lane); the tile goes through the wave's LDS and comes back in MFMA operand
+// order.  MFMA step st contracts over rows {4k + st}: lane l supplies row
+// 4 (l >> 4) + st, column l & 15, for both operands.  fp64 accumulation.
+template <bool SAME>
+__global__ __launch_bounds__(512) void k_gram16_f32(int64_t n, const float *__restrict__ X,
+                                                    const float *__restrict__ Y,
+                                                    double *__restrict__ part)
+{
+    constexpr int U = 4;  // tiles in flight per wave
+    __shared__ float tx[8][U][256];
+    __shared__ float ty[SAME ? 1 : 8][U][256];
+    __shared__ double red[8][256];
+    const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+    const int64_t ntl = ceil_div(n, 16);
+    XcdSched s(ceil_div(ntl, 8));
+    d4_t acc = {0.0, 0.0, 0.0, 0.0};
+    const float4 zero = {0.f, 0.f, 0.f, 0.f};
+    for (int64_t u = s.begin; u < s.end; u += U * s.step) {
+        float4 xv[U], yv[U];
+#pragma unroll
+        for (int t = 0; t < U; ++t) {
+            const int64_t uu = u + t * s.step;
+            const int64_t row = (uu * 8 + w) * 16 + (lane >> 2);
+            const bool ok = uu < s.end && row < n;
+            xv[t] = ok ? *reinterpret_cast<const float4 *>(X + row * 16 + 4 * (lane & 3)) : zero;
+            if constexpr (!SAME) yv[t] = ok ? *reinterpret_cast<const float4 *>(Y + row * 16 + 4 * (lane & 3)) : zero;
+        }
+#pragma unroll
+        for (int t = 0; t < U; ++t) {
+            *reinterpret_cast<float4 *>(&tx[w][t][4 * lane]) = xv[t];
+            if constexpr (!SAME) *reinterpret_cast<float4 *>(&ty[w][t][4 * lane]) = yv[t];
+        }
+        wave_lds_sync();
+#pragma unroll
+        for (int t = 0; t < U; ++t)
+#pragma unroll
+            for (int st = 0; st < 4; ++st) {
+                const int e = (4 * (lane >> 4) + st) * 16 + (lane & 15);
+                const double a = (double)tx[w][t][e];
+                const double b = SAME ? a : (double)ty[w][t][e];
+                acc = mfma16(a, b, acc);
+            }
+        wave_lds_sync();
+    }
+#pragma unroll
+    for (int r = 0; r < 4; ++r) red[w][((lane >> 4) + 4 * r) * 16 + (lane & 15)] = acc[r];
+    __syncthreads();
+    if (threadIdx.x < 256) {
+        double sum = 0.0;
+#pragma unroll
+        for (int ww = 0; ww < 8; ++ww) sum += red[ww][threadIdx.x];
+        part[(int64_t)blockIdx.x * 256 + threadIdx.x] = sum;
+    }
+}
+
 template <typename T, bool SAME>
 __global__ __launch_bounds__(512) void k_gram16_f64(int64_t n, const T *__restrict__ X,
                                                     const T *__restrict__ Y,
@@ -213,13 +270,20 @@ int gram_partials(lz_handle *h, int64_t n, int b, const T *X, const T *Y, int64_
 {
     LZ_ARG_CHECK(b >= 1 && b <= kMaxB, "b out of range");
     if (b == 16 && ld == 16) {  // fp64 and fp32
-        const int64_t units = ceil_div(ceil_div(n, 4), 8);
-        const int grid = (int)std::max<int64_t>(1, std::min<int64_t>(units, h->n_cu));
+        const bool f32 = std::is_same<T, float>::value;
+        const int64_t units = f32 ? ceil_div(ceil_div(n, 16), 8) : ceil_div(ceil_div(n, 4), 8);
+        const int grid = (int)std::max<int64_t>(1, std::min<int64_t>(units, f32 ? h->n_cu * 2 : h->n_cu));
         const int ev_ = prof_begin(h, PROF_GRAM);
-        if (X == Y)
+        if constexpr (std::is_same<T, float>::value) {
+            if (X == Y)
+                hipLaunchKernelGGL((k_gram16_f32<true>), dim3(grid), dim3(512), 0, h->stream, n, X, Y, h->partials);
+            else
+                hipLaunchKernelGGL((k_gram16_f32<false>), dim3(grid), dim3(512), 0, h->stream, n, X, Y, h->partials);
+        } else if (X == Y) {
             hipLaunchKernelGGL((k_gram16_f64<T, true>), dim3(grid), dim3(512), 0, h->stream, n, X, Y, h->partials);
-        else
+        } else {
             hipLaunchKernelGGL((k_gram16_f64<T, false>), dim3(grid), dim3(512), 0, h->stream, n, X, Y, h->partials);
+        }
         prof_end(h, ev_);
         LZ_LAUNCH_CHECK();
         *nparts = grid;
