@@ -452,10 +452,15 @@ struct FwCfg {
 // lane group's two-row list is a long row plus a short one.  (C3 rows: 10 +-
 // 2.2 nnz; a wave steps as long as its longest list: 3.48 steps per strip for
 // the rows (g, g+8), 3.03 for the ranked pairs, 3.00 ideal.)
+constexpr int64_t kPairPad = 16;  // >= strips per pass-1 tile (14)
+
 __global__ __launch_bounds__(256) void k_strip_pairs(int64_t n, const int64_t *__restrict__ rp,
                                                      uint64_t *__restrict__ out)
 {
-    const int64_t ns = (n + 15) / 16;
+    // kPairPad strips past the last one get the order of 16 empty rows (the
+    // identity): the last tile's trailing strips lie past n, and a consumer
+    // must still write every row of its parked Y tile (rows of length 0)
+    const int64_t ns = (n + 15) / 16 + kPairPad;
     for (int64_t st = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; st < ns;
          st += (int64_t)gridDim.x * blockDim.x) {
         uint32_t key[16];
@@ -483,7 +488,7 @@ __global__ __launch_bounds__(256) void k_strip_pairs(int64_t n, const int64_t *_
 
 int strip_pairs(lz_handle *h, int64_t n, const int64_t *rp, const uint64_t **out)
 {
-    const int64_t ns = ceil_div(n, (int64_t)16);
+    const int64_t ns = ceil_div(n, (int64_t)16) + kPairPad;
     if ((size_t)ns > h->pairs_cap) {
         LZ_HIP_TRY(hipStreamSynchronize(h->stream));
         (void)hipFree(h->pairs);
@@ -881,8 +886,8 @@ __global__ __launch_bounds__(64 * (NC + NL)) void k_fused_pp16(
             ws_dma(rr, st[s].rp, C::RP_PIECES, lane);
             ws_dma(cr, st[s].col, C::COL_PIECES, lane);
             ws_dma(vr, st[s].val, C::VAL_PIECES, lane);
-            if constexpr (BP) {  // the tile's strips' row orders (past the last strip: zeros)
-                const int64_t s0i = r0 / 16, ns = (n + 15) / 16;
+            if constexpr (BP) {  // the tile's strips' row orders (past the last strip: identity)
+                const int64_t s0i = r0 / 16, ns = (n + 15) / 16 + kPairPad;
                 const auto pr = __builtin_amdgcn_make_buffer_rsrc(const_cast<uint64_t *>(pairs + s0i), (short)0,
                                                                   (int)((ns - s0i) * 8), 0x00020000);
                 ws_dma(pr, st[s].pr, C::PR_PIECES, lane);
@@ -937,13 +942,9 @@ __global__ __launch_bounds__(64 * (NC + NL)) void k_fused_pp16(
     // epilogue of the pending strip: Y parked in S0 (swizzled), W/Q rows in wv/qv
     auto epilogue = [&]() {
         const int ar = lane & 15;
-        // rows past n: the parked tile holds whatever the LDS held (a strip
-        // past the end has no row order, so only its row 0 is written); they
-        // must not reach the slab accumulation as NaN * 0
-        const bool live_row = s0p + ar < n;
         double ya[4];
 #pragma unroll
-        for (int kc = 0; kc < 4; ++kc) ya[kc] = live_row ? S0[fw_sw(ar, 4 * (lane >> 4) + kc)] : 0.0;
+        for (int kc = 0; kc < 4; ++kc) ya[kc] = S0[fw_sw(ar, 4 * (lane >> 4) + kc)];
         d4_t q1 = {0.0, 0.0, 0.0, 0.0}, wn = {0.0, 0.0, 0.0, 0.0};
 #pragma unroll
         for (int kc = 0; kc < 4; ++kc) q1 = mfma16(wa[kc], ops[0][64 * kc + lane], q1);
@@ -1732,6 +1733,7 @@ int fused_spmm16(lz_handle *h, int64_t n, const int64_t *rp, const int32_t *col,
     // against 1.73-1.76 for k_fused_ws16 (LZ_FUSED_KERNEL=ws) in the Q-free iteration
     if (buf && (!variant || variant[0] == 'r')) {
         constexpr int NCR = 14;
+        static_assert(NCR <= kPairPad, "row orders must cover the last tile's strips");
         const int grid = (int)std::max<int64_t>(1, std::min<int64_t>(ceil_div(n, (int64_t)16 * NCR), h->n_cu));
         LZ_TRY(ensure_partials(h, (size_t)grid * NCR * 256));
         const int ev = prof_begin(h, PROF_SPMM_PASS);
