@@ -492,6 +492,11 @@ int lz_init(int device, lz_handle **out)
     LZ_HIP_TRY(hipMalloc(&h->scratch, sizeof(double) * 8 * kMaxB * kMaxB));
     LZ_HIP_TRY(hipMalloc(&h->err_flag, 64));
     LZ_HIP_TRY(hipMemset(h->err_flag, 0, 64));
+    if (const char *pz = getenv("LZ_POISON"); pz && pz[0] == '1') {  // test support: NaN-filled workspaces
+        LZ_HIP_TRY(hipMemset(h->partials, 0xFF, sizeof(double) * h->partials_cap));
+        LZ_HIP_TRY(hipMemset(h->partials2, 0xFF, sizeof(double) * (256 * kMaxB * kMaxB + 4096 * 256)));
+        LZ_HIP_TRY(hipMemset(h->scratch, 0xFF, sizeof(double) * 8 * kMaxB * kMaxB));
+    }
     *out = h;
     return LZ_OK;
 }

@@ -68,6 +68,7 @@ int lz_device_error(lz_handle *h, int *code);
  * with its low byte, on the handle's stream, so a kernel that reads LDS or
  * workspace it did not write shows it deterministically instead of by chance. */
 int lz_debug_poison_lds(lz_handle *h, uint32_t pattern);
+/* (LZ_POISON=1 in the environment: lz_init fills the new handle's workspaces with 0xFF.) */
 
 int lz_prof_enable(lz_handle *h, int on);
 int lz_prof_read(lz_handle *h, int kernel_class, double *ms_total, int *count);

@@ -10,6 +10,9 @@ if ROOT not in sys.path:
 
 import __graft_entry__ as ge  # noqa: E402
 
+# every handle the tests create starts with NaN-filled workspaces (lz_init)
+os.environ.setdefault("LZ_POISON", "1")
+
 
 def pytest_configure(config):
     config.addinivalue_line("markers", "gpu: needs a gfx950 GPU (run with -m gpu)")
