@@ -508,6 +508,7 @@ int lz_finalize(lz_handle *h)
     halo_free(h);
     (void)hipFree(h->pairs);
     (void)hipFree(h->longq);
+    (void)hipFree(h->cm_buf);
     if (h->comm) ncclCommDestroy(comm_of(h));
     if (h->ev_pool) {
         for (int i = 0; i < h->ev_cap; ++i) (void)hipEventDestroy(h->ev_pool[i]);
@@ -607,9 +608,9 @@ int lz_csr_spmm(lz_handle *h, int64_t n_rows, int64_t n_cols, int64_t nnz, const
     }
     LZ_ARG_CHECK(ldx >= n_cols && ldy >= n_rows, "column-major ld >= rows");
     if (dtype == LZ_F64)
-        return spmm_cm<double>(h, n_rows, rp, col, (const double *)val, b, (const double *)X, ldx,
+        return spmm_cm<double>(h, n_rows, rp, col, (const double *)val, b, (const double *)X, ldx, n_cols,
                                (double *)Y, ldy);
-    return spmm_cm<float>(h, n_rows, rp, col, (const float *)val, b, (const float *)X, ldx,
+    return spmm_cm<float>(h, n_rows, rp, col, (const float *)val, b, (const float *)X, ldx, n_cols,
                           (float *)Y, ldy);
 }
 

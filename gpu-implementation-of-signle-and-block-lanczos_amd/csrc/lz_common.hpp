@@ -74,6 +74,8 @@ struct lz_handle {
     int *longq = nullptr;         // k_spmm_seg long-tile queue: [0] count, [1..] tile ids
     size_t longq_cap = 0;         // ints
     size_t pairs_cap = 0;         // entries
+    void *cm_buf = nullptr;       // column-major SpMM: row-major copies of X and Y
+    size_t cm_cap = 0;            // bytes
     // optional per-kernel-class timing with hipEvents on the handle's stream
     // (lz_prof_enable / lz_prof_read): events recorded around each launch of
     // the class, elapsed times summed at read time.

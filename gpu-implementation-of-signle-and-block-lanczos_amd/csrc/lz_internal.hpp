@@ -10,7 +10,7 @@ int spmm_rm(lz_handle *h, int64_t n, const int64_t *rp, const int32_t *col, cons
             const T *X, int64_t ldx, int64_t nx, T *Y, int64_t ldy);  // nx: rows of X
 template <typename T>
 int spmm_cm(lz_handle *h, int64_t n, const int64_t *rp, const int32_t *col, const T *val, int b,
-            const T *X, int64_t ldx, T *Y, int64_t ldy);
+            const T *X, int64_t ldx, int64_t nx, T *Y, int64_t ldy);  // nx: rows of X
 template <typename T>
 int spmv(lz_handle *h, int64_t n, const int64_t *rp, const int32_t *col, const T *val, const T *x,
          T *y, int64_t nnz_hint);

@@ -61,10 +61,32 @@ def test_spmm_rowmajor_f32(lz, orc, handle, torch_cuda, b):
     check_spmm(lz, orc, handle, torch_cuda, A, b, np.float32)
 
 
-@pytest.mark.parametrize("b", [1, 4, 5])
-def test_spmm_colmajor(lz, orc, handle, torch_cuda, b):
+@pytest.mark.parametrize("b", [1, 4, 5, 16, 32, 64])
+@pytest.mark.parametrize("dtype", [np.float64, np.float32])
+def test_spmm_colmajor(lz, orc, handle, torch_cuda, b, dtype):
+    """Column-major X/Y (b >= 2: transposed in and out around the row-major kernel)."""
     A = lz.gen_banded(3001, 8.0, 100, seed=9)
-    check_spmm(lz, orc, handle, torch_cuda, A, b, np.float64, layout="col")
+    check_spmm(lz, orc, handle, torch_cuda, A, b, dtype, layout="col")
+
+
+@pytest.mark.parametrize("direct", [False, True])
+def test_spmm_colmajor_padded_ld(lz, handle, torch_cuda, monkeypatch, direct):
+    """The reference's Dense_matrix: leading dimension = padded rows (> n)."""
+    torch = torch_cuda
+    if direct:
+        monkeypatch.setenv("LZ_SPMM_CM", "direct")  # read once per process: may stay on the first value
+    A = lz.gen_banded(1000, 6.0, 50, seed=4)
+    n, b, ld = A.n, 16, 1024 + 7
+    rng = np.random.default_rng(2)
+    X = rng.uniform(-1, 1, (n, b))
+    Xp = torch.full((b, ld), np.nan, dtype=torch.float64, device="cuda")
+    Xp[:, :n] = torch.from_numpy(X.T.copy()).cuda()
+    Yp = torch.full((b, ld), 7.0, dtype=torch.float64, device="cuda")
+    handle.spmm(lz.CsrDevice.from_host(A), Xp[:, :n], Yp[:, :n], layout=lz.LZ_COL_MAJOR)
+    M = dense_of(A)
+    Y = Yp.cpu().numpy()
+    assert np.all(np.abs(Y[:, :n].T - M @ X) <= 64 * EPS[np.float64] * (abs(M) @ np.abs(X)))
+    assert np.all(Y[:, n:] == 7.0)  # padding untouched
 
 
 def test_spmm_matrix_a_and_bug_compat(lz, orc, handle, torch_cuda, golden):
