@@ -530,63 +530,145 @@ __global__ __launch_bounds__(kRedThreads) void k_sqrtm_b(const T *__restrict__ G
     const long long t0 = clock64();
     int nsw = 0;
 #endif
-    for (int sweep = 0; sweep < 60; ++sweep) {
+    if constexpr (B == 16) {
+        // Register-resident form (B = 16).  Lane L owns the 2x2 pair-block of
+        // position rows {P, 15 - P} x columns {Q, 15 - Q} (P = L >> 3, Q = L & 7)
+        // of A, and the same rows x index columns {Q, 15 - Q} of U.  Per round:
+        // the diagonal lanes (P == Q) form their pair's rotation, every lane
+        // fetches the row and column rotations by lane shuffles and updates its
+        // block in registers (same products, same order as the generic path, so
+        // A stays bit-symmetric); the circle move is one scatter to the LDS copy
+        // (moved positions) and one gather back -- no LDS round trip for the
+        // rotation parameters, 16 LDS accesses per lane instead of ~40.
+        const int P = tid >> 3, Q = tid & 7;
+        const int X[2] = {P, B - 1 - P}, Y[2] = {Q, B - 1 - Q};
+        auto mv = [](int x) { return x == 0 ? 0 : (x == 1 ? B - 1 : x - 1); };
+        const int XM[2] = {mv(X[0]), mv(X[1])}, YM[2] = {mv(Y[0]), mv(Y[1])};
+        double a[2][2], u[2][2];
+#pragma unroll
+        for (int ii = 0; ii < 2; ++ii)
+#pragma unroll
+            for (int jj = 0; jj < 2; ++jj) {
+                a[ii][jj] = Am[X[ii] * LD + Y[jj]];
+                u[ii][jj] = Um[X[ii] * LD + Y[jj]];
+            }
+        for (int sweep = 0; sweep < 60; ++sweep) {
 #ifdef LZ_SQRTM_PROBE
-        nsw = sweep;
+            nsw = sweep;
 #endif
-        // converged when no off-diagonal entry exceeds the rotation threshold
-        bool need = false;
-        const double djj = fabs(Am[j * LD + j]);
-#pragma unroll UN
-        for (int k = 0; k < NE; ++k) {
-            const int i = r0 + RS * k;
-            const double aij = Am[i * LD + j];
-            if (i != j && aij != 0.0 && aij * aij > kTol2 * (fabs(Am[i * LD + i]) * djj)) need = true;
-        }
-        if (__ballot(need) == 0) break;  // wave-uniform
+            bool need = false;  // the LDS copy holds this sweep's matrix in index order
+#pragma unroll
+            for (int ii = 0; ii < 2; ++ii)
+#pragma unroll
+                for (int jj = 0; jj < 2; ++jj) {
+                    const int x = X[ii], y = Y[jj];
+                    const double aij = a[ii][jj];
+                    if (x != y && aij != 0.0 &&
+                        aij * aij > kTol2 * (fabs(Am[x * LD + x]) * fabs(Am[y * LD + y])))
+                        need = true;
+                }
+            if (__ballot(need) == 0) break;  // wave-uniform
 #pragma unroll 1
-        for (int rnd = 0; rnd < B - 1; ++rnd) {
-            if (tid < B / 2) {
-                const int p = tid, q = B - 1 - tid;
-                double c, s;
-                jacobi_rot(Am[p * LD + p], Am[q * LD + q], Am[p * LD + q], c, s);
-                cc[p] = c;
-                cc[q] = c;
-                ss[p] = -s;  // R[p][q]
-                ss[q] = s;   // R[q][p]
-            }
-            wave_lds_sync();
-            const double cj = cc[j], sj = ss[j];
-            for (int k0 = 0; k0 < NE; k0 += UN) {
-                double v[UN][6], ci[UN], si[UN];
+            for (int rnd = 0; rnd < B - 1; ++rnd) {
+                double c = 1.0, sn = 0.0;
+                if (P == Q) jacobi_rot(a[0][0], a[1][1], a[0][1], c, sn);
+                const double cP = __shfl(c, 9 * P, 64), sP = __shfl(sn, 9 * P, 64);
+                const double cQ = __shfl(c, 9 * Q, 64), sQ = __shfl(sn, 9 * Q, 64);
+                // R[x0][x0] = R[x1][x1] = c, R[x0][x1] = -s, R[x1][x0] = s
+                const double ci[2] = {cP, cP}, si[2] = {-sP, sP};
+                const double cj[2] = {cQ, cQ}, sj[2] = {-sQ, sQ};
+                double an[2][2], un[2][2];
 #pragma unroll
-                for (int kk = 0; kk < UN; ++kk) {  // all reads of the chunk first
-                    const int i = r0 + RS * (k0 + kk), iq = B - 1 - i;
-                    ci[kk] = cc[i];
-                    si[kk] = ss[i];
-                    v[kk][0] = Am[i * LD + j];
-                    v[kk][1] = Am[i * LD + jq];
-                    v[kk][2] = Am[iq * LD + j];
-                    v[kk][3] = Am[iq * LD + jq];
-                    v[kk][4] = Um[i * LD + j];
-                    v[kk][5] = Um[iq * LD + j];
-                }
+                for (int ii = 0; ii < 2; ++ii)
 #pragma unroll
-                for (int kk = 0; kk < UN; ++kk) {
-                    const int i = r0 + RS * (k0 + kk);
-                    const int in = i == 0 ? 0 : (i == 1 ? B - 1 : i - 1);
-                    const double x1 = v[kk][0] * (ci[kk] * cj), x2 = v[kk][1] * (ci[kk] * sj);
-                    const double x3 = v[kk][2] * (si[kk] * cj), x4 = v[kk][3] * (si[kk] * sj);
-                    const bool ann = (i == jq) && si[kk] != 0.0;  // the annihilated pair
-                    An[in * LD + jn] = ann ? 0.0 : (x1 + x4) + (x2 + x3);
-                    Un[in * LD + j] = v[kk][4] * ci[kk] + v[kk][5] * si[kk];
+                    for (int jj = 0; jj < 2; ++jj) {
+                        const double x1 = a[ii][jj] * (ci[ii] * cj[jj]), x2 = a[ii][1 - jj] * (ci[ii] * sj[jj]);
+                        const double x3 = a[1 - ii][jj] * (si[ii] * cj[jj]), x4 = a[1 - ii][1 - jj] * (si[ii] * sj[jj]);
+                        const bool ann = (P == Q) && (ii != jj) && sP != 0.0;  // the annihilated pair
+                        an[ii][jj] = ann ? 0.0 : (x1 + x4) + (x2 + x3);
+                        un[ii][jj] = u[ii][jj] * ci[ii] + u[1 - ii][jj] * si[ii];
+                    }
+#pragma unroll
+                for (int ii = 0; ii < 2; ++ii)
+#pragma unroll
+                    for (int jj = 0; jj < 2; ++jj) {
+                        Am[XM[ii] * LD + YM[jj]] = an[ii][jj];
+                        Um[XM[ii] * LD + Y[jj]] = un[ii][jj];
+                    }
+                wave_lds_sync();
+#pragma unroll
+                for (int ii = 0; ii < 2; ++ii)
+#pragma unroll
+                    for (int jj = 0; jj < 2; ++jj) {
+                        a[ii][jj] = Am[X[ii] * LD + Y[jj]];
+                        u[ii][jj] = Um[X[ii] * LD + Y[jj]];
+                    }
+                wave_lds_sync();
+            }
+        }
+        (void)An;
+        (void)Un;
+        (void)jn;
+        (void)jq;
+    } else {
+        for (int sweep = 0; sweep < 60; ++sweep) {
+    #ifdef LZ_SQRTM_PROBE
+            nsw = sweep;
+    #endif
+            // converged when no off-diagonal entry exceeds the rotation threshold
+            bool need = false;
+            const double djj = fabs(Am[j * LD + j]);
+    #pragma unroll UN
+            for (int k = 0; k < NE; ++k) {
+                const int i = r0 + RS * k;
+                const double aij = Am[i * LD + j];
+                if (i != j && aij != 0.0 && aij * aij > kTol2 * (fabs(Am[i * LD + i]) * djj)) need = true;
+            }
+            if (__ballot(need) == 0) break;  // wave-uniform
+    #pragma unroll 1
+            for (int rnd = 0; rnd < B - 1; ++rnd) {
+                if (tid < B / 2) {
+                    const int p = tid, q = B - 1 - tid;
+                    double c, s;
+                    jacobi_rot(Am[p * LD + p], Am[q * LD + q], Am[p * LD + q], c, s);
+                    cc[p] = c;
+                    cc[q] = c;
+                    ss[p] = -s;  // R[p][q]
+                    ss[q] = s;   // R[q][p]
                 }
+                wave_lds_sync();
+                const double cj = cc[j], sj = ss[j];
+                for (int k0 = 0; k0 < NE; k0 += UN) {
+                    double v[UN][6], ci[UN], si[UN];
+    #pragma unroll
+                    for (int kk = 0; kk < UN; ++kk) {  // all reads of the chunk first
+                        const int i = r0 + RS * (k0 + kk), iq = B - 1 - i;
+                        ci[kk] = cc[i];
+                        si[kk] = ss[i];
+                        v[kk][0] = Am[i * LD + j];
+                        v[kk][1] = Am[i * LD + jq];
+                        v[kk][2] = Am[iq * LD + j];
+                        v[kk][3] = Am[iq * LD + jq];
+                        v[kk][4] = Um[i * LD + j];
+                        v[kk][5] = Um[iq * LD + j];
+                    }
+    #pragma unroll
+                    for (int kk = 0; kk < UN; ++kk) {
+                        const int i = r0 + RS * (k0 + kk);
+                        const int in = i == 0 ? 0 : (i == 1 ? B - 1 : i - 1);
+                        const double x1 = v[kk][0] * (ci[kk] * cj), x2 = v[kk][1] * (ci[kk] * sj);
+                        const double x3 = v[kk][2] * (si[kk] * cj), x4 = v[kk][3] * (si[kk] * sj);
+                        const bool ann = (i == jq) && si[kk] != 0.0;  // the annihilated pair
+                        An[in * LD + jn] = ann ? 0.0 : (x1 + x4) + (x2 + x3);
+                        Un[in * LD + j] = v[kk][4] * ci[kk] + v[kk][5] * si[kk];
+                    }
+                }
+                {
+                    double *t = Am; Am = An; An = t;
+                    t = Um; Um = Un; Un = t;
+                }
+                wave_lds_sync();
             }
-            {
-                double *t = Am; Am = An; An = t;
-                t = Um; Um = Un; Un = t;
-            }
-            wave_lds_sync();
         }
     }
 #ifdef LZ_SQRTM_PROBE
