@@ -7,8 +7,11 @@ A "step" is one block-Lanczos iteration (fused SpMM pass + alpha finish +
 update pass + beta sqrtm) over the whole synthetic operator, inputs resident in
 HBM.  N = 1: config C3 on one GPU.  N > 1 (launched by torch.distributed.run):
 weak scaling -- every rank owns a 10M-row slab of an N*10M-row banded operator,
-row-partitioned, with an RCCL all-gather of the Krylov block each iteration;
-`value` counts slab-iterations/s summed over ranks.  rank 0 prints one JSON line.
+row-partitioned; each iteration exchanges only the Krylov-block rows other
+ranks reference (RCCL grouped send/recv, `--exchange halo`, default) or
+all-gathers the block (`--exchange allgather`); `value` counts
+slab-iterations/s summed over ranks.  rank 0 prints one JSON line on stdout
+(native libraries' own stdout output is routed to stderr).
 """
 from __future__ import annotations
 
@@ -110,6 +113,11 @@ def main():
     ap.add_argument("--dist", action="store_true",
                     help="run the distributed entry point even at N = 1 (rehearsal of the N > 1 path)")
     args = ap.parse_args()
+    # Native libraries write to fd 1 (RCCL prints a version banner at communicator
+    # init): route fd 1 to stderr and keep the real stdout for the one JSON line.
+    sys.stdout.flush()
+    json_fd = os.dup(1)
+    os.dup2(2, 1)
 
     import torch
     import torch.distributed as dist
@@ -361,7 +369,7 @@ def main():
                 "iteration_min_bytes": iter_min_bytes,
             },
         }
-        print(json.dumps(out), flush=True)
+        os.write(json_fd, (json.dumps(out) + "\n").encode())
     h.close()
     if world > 1:
         dist.destroy_process_group()
