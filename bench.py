@@ -276,7 +276,7 @@ def main():
     c3r = None
     if world == 1 and not dist_path and args.rand_steps > 0:
         kr = args.rand_steps
-        Ar = lz.gen_banded(n, args.nnz_per_row, n, seed + 7)
+        Ar = lz.gen_banded(n, args.nnz_per_row, n, seed)
         Ard = lz.CsrDevice.from_host(Ar)
         Yr = torch.empty(n, b, **kw)
         h.spmm(Ard, Bd, Yr)
@@ -301,6 +301,12 @@ def main():
                "spmm_GBs": round(spmm_bytes(n, Ar.nnz, b) / t_sp / 1e9, 1),
                "spmm_frac_of_hbm_peak": round(spmm_bytes(n, Ar.nnz, b) / t_sp / 1e9 / HBM_PEAK_GBS, 4),
                "finite": bool(torch.isfinite(alr).all())}
+        # measured HBM traffic of this SpMM (committed PMC passes of the same operator)
+        tr_r, src_r = pmc_traffic("k_spmm_seg_random_columns", n, Ar.nnz, n)
+        if tr_r:
+            c3r.update({"spmm_pmc_hbm_bytes": tr_r, "spmm_pmc_GBs": round(tr_r / t_sp / 1e9, 1),
+                        "spmm_pmc_frac_of_hbm_peak": round(tr_r / t_sp / 1e9 / HBM_PEAK_GBS, 4),
+                        "pmc_source": src_r})
         del Ard, Yr
 
     # ---- CPU baseline: the oracle (C, OpenMP) on this operator, rank 0, N = 1
