@@ -530,79 +530,105 @@ __global__ __launch_bounds__(kRedThreads) void k_sqrtm_b(const T *__restrict__ G
     const long long t0 = clock64();
     int nsw = 0;
 #endif
-    if constexpr (B == 16) {
-        // Register-resident form (B = 16).  Lane L owns the 2x2 pair-block of
-        // position rows {P, 15 - P} x columns {Q, 15 - Q} (P = L >> 3, Q = L & 7)
-        // of A, and the same rows x index columns {Q, 15 - Q} of U.  Per round:
-        // the diagonal lanes (P == Q) form their pair's rotation, every lane
-        // fetches the row and column rotations by lane shuffles and updates its
-        // block in registers (same products, same order as the generic path, so
-        // A stays bit-symmetric); the circle move is one scatter to the LDS copy
-        // (moved positions) and one gather back -- no LDS round trip for the
-        // rotation parameters, 16 LDS accesses per lane instead of ~40.
-        const int P = tid >> 3, Q = tid & 7;
-        const int X[2] = {P, B - 1 - P}, Y[2] = {Q, B - 1 - Q};
+    if constexpr (B == 16 || B == 32) {
+        // Register-resident form.  The NPB = B/2 pairs (p, B-1-p) cut A into
+        // NPB x NPB 2x2 pair-blocks; lane L owns QS = NPB^2/64 of them: position
+        // rows {P, B-1-P} x columns {Q_t, B-1-Q_t}, t < QS (P = L / LPP,
+        // Q_t = (L % LPP) QS + t, LPP = NPB / QS lanes per row pair), and the
+        // same rows x index columns of U.  Per round: the lanes holding a
+        // diagonal block form that pair's rotation, every lane fetches its row
+        // and column rotations by lane shuffles and updates its blocks in
+        // registers (same products, same order as the LDS form, so A stays
+        // bit-symmetric); the circle move is one scatter to the LDS copy (moved
+        // positions) and one gather back -- no LDS round trip for the rotation
+        // parameters and about half the LDS accesses of the LDS form.
+        constexpr int NPB = B / 2, QS = NPB * NPB / 64, LPP = NPB / QS;
+        const int P = tid / LPP, Q0 = (tid % LPP) * QS;
+        auto owner = [](int p) { return p * LPP + p / QS; };  // lane holding pair p's diagonal block
         auto mv = [](int x) { return x == 0 ? 0 : (x == 1 ? B - 1 : x - 1); };
-        const int XM[2] = {mv(X[0]), mv(X[1])}, YM[2] = {mv(Y[0]), mv(Y[1])};
-        double a[2][2], u[2][2];
+        const int X[2] = {P, B - 1 - P}, XM[2] = {mv(X[0]), mv(X[1])};
+        int Y[QS][2], YM[QS][2];
 #pragma unroll
-        for (int ii = 0; ii < 2; ++ii)
+        for (int t = 0; t < QS; ++t) {
+            Y[t][0] = Q0 + t;
+            Y[t][1] = B - 1 - (Q0 + t);
+            YM[t][0] = mv(Y[t][0]);
+            YM[t][1] = mv(Y[t][1]);
+        }
+        const bool has_diag = (tid % LPP) == P / QS;  // slot P % QS holds block (P, P)
+        double a[QS][2][2], u[QS][2][2];
 #pragma unroll
-            for (int jj = 0; jj < 2; ++jj) {
-                a[ii][jj] = Am[X[ii] * LD + Y[jj]];
-                u[ii][jj] = Um[X[ii] * LD + Y[jj]];
-            }
+        for (int t = 0; t < QS; ++t)
+#pragma unroll
+            for (int ii = 0; ii < 2; ++ii)
+#pragma unroll
+                for (int jj = 0; jj < 2; ++jj) {
+                    a[t][ii][jj] = Am[X[ii] * LD + Y[t][jj]];
+                    u[t][ii][jj] = Um[X[ii] * LD + Y[t][jj]];
+                }
         for (int sweep = 0; sweep < 60; ++sweep) {
 #ifdef LZ_SQRTM_PROBE
             nsw = sweep;
 #endif
             bool need = false;  // the LDS copy holds this sweep's matrix in index order
 #pragma unroll
-            for (int ii = 0; ii < 2; ++ii)
+            for (int t = 0; t < QS; ++t)
 #pragma unroll
-                for (int jj = 0; jj < 2; ++jj) {
-                    const int x = X[ii], y = Y[jj];
-                    const double aij = a[ii][jj];
-                    if (x != y && aij != 0.0 &&
-                        aij * aij > kTol2 * (fabs(Am[x * LD + x]) * fabs(Am[y * LD + y])))
-                        need = true;
-                }
+                for (int ii = 0; ii < 2; ++ii)
+#pragma unroll
+                    for (int jj = 0; jj < 2; ++jj) {
+                        const int x = X[ii], y = Y[t][jj];
+                        const double aij = a[t][ii][jj];
+                        if (x != y && aij != 0.0 &&
+                            aij * aij > kTol2 * (fabs(Am[x * LD + x]) * fabs(Am[y * LD + y])))
+                            need = true;
+                    }
             if (__ballot(need) == 0) break;  // wave-uniform
 #pragma unroll 1
             for (int rnd = 0; rnd < B - 1; ++rnd) {
                 double c = 1.0, sn = 0.0;
-                if (P == Q) jacobi_rot(a[0][0], a[1][1], a[0][1], c, sn);
-                const double cP = __shfl(c, 9 * P, 64), sP = __shfl(sn, 9 * P, 64);
-                const double cQ = __shfl(c, 9 * Q, 64), sQ = __shfl(sn, 9 * Q, 64);
+                if (has_diag) {
+                    double d00 = a[0][0][0], d11 = a[0][1][1], d01 = a[0][0][1];
+#pragma unroll
+                    for (int t = 1; t < QS; ++t)
+                        if (P % QS == t) {
+                            d00 = a[t][0][0];
+                            d11 = a[t][1][1];
+                            d01 = a[t][0][1];
+                        }
+                    jacobi_rot(d00, d11, d01, c, sn);
+                }
+                const double cP = __shfl(c, owner(P), 64), sP = __shfl(sn, owner(P), 64);
                 // R[x0][x0] = R[x1][x1] = c, R[x0][x1] = -s, R[x1][x0] = s
                 const double ci[2] = {cP, cP}, si[2] = {-sP, sP};
-                const double cj[2] = {cQ, cQ}, sj[2] = {-sQ, sQ};
-                double an[2][2], un[2][2];
 #pragma unroll
-                for (int ii = 0; ii < 2; ++ii)
+                for (int t = 0; t < QS; ++t) {
+                    const int Qt = Q0 + t;
+                    const double cQ = __shfl(c, owner(Qt), 64), sQ = __shfl(sn, owner(Qt), 64);
+                    const double cj[2] = {cQ, cQ}, sj[2] = {-sQ, sQ};
 #pragma unroll
-                    for (int jj = 0; jj < 2; ++jj) {
-                        const double x1 = a[ii][jj] * (ci[ii] * cj[jj]), x2 = a[ii][1 - jj] * (ci[ii] * sj[jj]);
-                        const double x3 = a[1 - ii][jj] * (si[ii] * cj[jj]), x4 = a[1 - ii][1 - jj] * (si[ii] * sj[jj]);
-                        const bool ann = (P == Q) && (ii != jj) && sP != 0.0;  // the annihilated pair
-                        an[ii][jj] = ann ? 0.0 : (x1 + x4) + (x2 + x3);
-                        un[ii][jj] = u[ii][jj] * ci[ii] + u[1 - ii][jj] * si[ii];
-                    }
+                    for (int ii = 0; ii < 2; ++ii)
 #pragma unroll
-                for (int ii = 0; ii < 2; ++ii)
-#pragma unroll
-                    for (int jj = 0; jj < 2; ++jj) {
-                        Am[XM[ii] * LD + YM[jj]] = an[ii][jj];
-                        Um[XM[ii] * LD + Y[jj]] = un[ii][jj];
-                    }
+                        for (int jj = 0; jj < 2; ++jj) {
+                            const double x1 = a[t][ii][jj] * (ci[ii] * cj[jj]);
+                            const double x2 = a[t][ii][1 - jj] * (ci[ii] * sj[jj]);
+                            const double x3 = a[t][1 - ii][jj] * (si[ii] * cj[jj]);
+                            const double x4 = a[t][1 - ii][1 - jj] * (si[ii] * sj[jj]);
+                            const bool ann = (P == Qt) && (ii != jj) && sP != 0.0;  // the annihilated pair
+                            Am[XM[ii] * LD + YM[t][jj]] = ann ? 0.0 : (x1 + x4) + (x2 + x3);
+                            Um[XM[ii] * LD + Y[t][jj]] = u[t][ii][jj] * ci[ii] + u[t][1 - ii][jj] * si[ii];
+                        }
+                }
                 wave_lds_sync();
 #pragma unroll
-                for (int ii = 0; ii < 2; ++ii)
+                for (int t = 0; t < QS; ++t)
 #pragma unroll
-                    for (int jj = 0; jj < 2; ++jj) {
-                        a[ii][jj] = Am[X[ii] * LD + Y[jj]];
-                        u[ii][jj] = Um[X[ii] * LD + Y[jj]];
-                    }
+                    for (int ii = 0; ii < 2; ++ii)
+#pragma unroll
+                        for (int jj = 0; jj < 2; ++jj) {
+                            a[t][ii][jj] = Am[X[ii] * LD + Y[t][jj]];
+                            u[t][ii][jj] = Um[X[ii] * LD + Y[t][jj]];
+                        }
                 wave_lds_sync();
             }
         }
