@@ -1,21 +1,35 @@
 """Benchmark: block-Lanczos iterations/sec + SpMM achieved HBM GB/s vs peak
 (BASELINE.json metric), n = 10M, nnz = 1e8, b = 16, fp64, on MI355X.
 
-    python bench.py [--gpus N] [--steps K] [--warmup W]
+    python bench.py [--gpus N] [--steps K] [--warmup W] [--config c3|c4]
 
 A "step" is one block-Lanczos iteration (fused SpMM pass + alpha finish +
 update pass + beta sqrtm) over the whole synthetic operator, inputs resident in
-HBM.  N = 1: config C3 on one GPU.  N > 1 (launched by torch.distributed.run):
-weak scaling -- every rank owns a 10M-row slab of an N*10M-row banded operator,
-row-partitioned; each iteration exchanges only the Krylov-block rows other
-ranks reference (RCCL grouped send/recv, `--exchange halo`, default) or
-all-gathers the block (`--exchange allgather`); `value` counts
-slab-iterations/s summed over ranks.  rank 0 prints one JSON line on stdout
-(native libraries' own stdout output is routed to stderr).
+HBM.
+
+--config c3 (default): BASELINE config C3.  N = 1: n = 1e7, nnz = 1e8, half
+  width 4096 on one GPU.  N > 1 (launched by torch.distributed.run): weak
+  scaling -- every rank owns a 10M-row slab of an N*10M-row banded operator,
+  row-partitioned; each iteration exchanges only the Krylov-block rows other
+  ranks reference (RCCL grouped send/recv, `--exchange halo`, default) or
+  all-gathers the block (`--exchange allgather`); `value` counts
+  slab-iterations/s summed over ranks.
+--config c4: BASELINE config C4, strong scaling -- n = 4e7 rows in total,
+  25 nnz/row (nnz = 1e9), half width 2^16, split over the N ranks.  At N > 1
+  the line reports the halo exchange as `value` and the north star's RCCL
+  all-gather form beside it (extra.c4_allgather).
+
+After the timed region the run checks itself: the device error word must be
+0 (no persistent kernel abandoned a bounded spin) and, on one GPU, the first
+steps' alpha / beta / row probe / Ritz values must match the CPU oracle run on
+the same operator and start block (the same call times the CPU baseline).
+rank 0 prints one JSON line on stdout (native libraries' own stdout output is
+routed to stderr).
 """
 from __future__ import annotations
 
 import argparse
+import glob
 import json
 import os
 import sys
@@ -28,7 +42,8 @@ sys.path.insert(0, ROOT)
 import __graft_entry__ as ge  # noqa: E402
 
 HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec (MI355X_MICROARCH.md)
-FP64_PEAK_TFS = 78.6
+FP64_MFMA_PEAK_TFS = 78.6  # v_mfma_f64_16x16x4f64: 32 FLOP/clk/SIMD x 1024 SIMDs x 2.4 GHz
+RITZ_TOL = 1e-10  # BASELINE.json north star: Ritz values within 1e-10 of the reference
 
 
 def log(*a):
@@ -46,73 +61,90 @@ def fused_pass_bytes(n, nnz, b, sv=8):
     return nnz * (sv + 4) + (n + 1) * 8 + 3 * n * b * sv
 
 
-def fused_kernel():
-    """(full name, PMC short name) of the pass-1 kernel lz_fused.hip launches for
-    b = 16 fp64 (LZ_FUSED_KERNEL selects the alternatives kept for A/B runs)."""
-    v = os.environ.get("LZ_FUSED_KERNEL", "")
-    if v.startswith("s"):
-        return "k_fused_seg16", "k_fused_seg16"
-    if v.startswith("t"):
-        return "k_fused_spmm16<true>", "k_fused_spmm16"
-    if v.startswith("p"):
-        return f"k_fused_pf16<{8 if v[1:2] == '8' else 4}>", "k_fused_pf16"
-    if not v or v.startswith("r"):
-        return "k_fused_pp16<14,2376,3,2>", "k_fused_pp16"
-    if v.startswith("wsq"):
-        return "k_fused_ws16<15,2536,2>", "k_fused_ws16"
-    if v.startswith("n"):
-        return "k_fused_ws16<14,2376,3,true,2>", "k_fused_ws16"
-    return "k_fused_ws16<15,2536,3,true>", "k_fused_ws16"
+# MFMA work of the dense step per row (b = 16, v_mfma_f64_16x16x4f64 = 2048 FLOP):
+# pass 1 epilogue, per 16-row strip: Q_j = W_j beta^-1 (4), W' = Y beta^-1 -
+# W_{j-1} P1 (8), slab Q_j^T W' (4) = 16 MFMAs; pass 2: W'' = W' - W_j P2 (4),
+# slab W''^T W'' (4) = 8 MFMAs.
+PASS1_MFMA_FLOP_PER_ROW = 16 * 2048 // 16
+PASS2_MFMA_FLOP_PER_ROW = 8 * 2048 // 16
 
 
-def spmm_kernel():
-    """The plain SpMM kernel lz_csr_spmm launches for b = 16 fp64 (LZ_SPMM_KERNEL A/B)."""
-    v = os.environ.get("LZ_SPMM_KERNEL", "")
-    if not v or v[0] == "s":
-        tr = {"3": 32, "6": 64, "9": 96}.get(v[1:2], 48)
-        return f"k_spmm_seg<double,16,{tr},{tr * 16},8,nt>"
-    return "k_spmm_buf<double,16,1024,2>" if v[0] == "b" else f"LZ_SPMM_KERNEL={v}"
+def fused_kernel(nnz, n):
+    """(full name, PMC short name) of the pass-1 kernel lz_fused.hip launches (b = 16 fp64)."""
+    wide = nnz > 10.2 * n
+    win = n >= (1 << 24)
+    shape = "10,4400,2,2" if wide else "14,2376,3,2"
+    return f"k_fused_pp16<{shape},{'true' if win else 'false'}>", "k_fused_pp16"
 
 
-def pmc_traffic(kernel, n, nnz, hw):
-    """HBM bytes per launch of `kernel` from the committed rocprofv3 PMC summary
-    (profiles/*_pmc_<kernel>.json, written by scripts/pmc_traffic.py from separate
-    FETCH_SIZE / WRITE_SIZE passes of this bench command; FETCH_SIZE doubled per
-    MI355X_MICROARCH.md's gfx950 note).  None unless it was taken on this workload."""
-    import glob
-    for f in sorted(glob.glob(os.path.join(ROOT, "profiles", f"*_pmc_{kernel}.json")), reverse=True):
+def spmm_kernel(nnz, n):
+    """The plain SpMM kernel lz_csr_spmm launches for b = 16 fp64 (lz_spmm.hip launch_spmm_rm)."""
+    cap = 1536 if nnz > 13.0 * n else 768
+    win = n >= (1 << 24)
+    return f"k_spmm_seg<double,16,48,{cap},{'true' if win else 'false'},0>"
+
+
+def pmc_record(kind, kernel, n, nnz, hw):
+    """A committed rocprofv3 PMC summary (profiles/*_pmc_<kind>_<kernel>.json or,
+    kind "", profiles/*_pmc_<kernel>.json) of this bench's workload, newest first."""
+    pat = f"*_pmc_{kind + '_' if kind else ''}{kernel}.json"
+    for f in sorted(glob.glob(os.path.join(ROOT, "profiles", pat)), reverse=True):
         try:
             d = json.load(open(f))
         except (OSError, ValueError):
             continue
         w = d.get("workload", {})
         if w.get("n") == n and w.get("nnz") == nnz and w.get("halfwidth") == hw:
-            return d.get("hbm_bytes_per_launch"), os.path.relpath(f, ROOT)
+            return d, os.path.relpath(f, ROOT)
     return None, None
 
 
-def main():
+def pmc_traffic(kernel, n, nnz, hw):
+    """HBM bytes per launch of `kernel` from the committed PMC summary (separate
+    FETCH_SIZE / WRITE_SIZE passes, FETCH_SIZE doubled per MI355X_MICROARCH.md's
+    gfx950 note; scripts/pmc_traffic.py).  None unless taken on this workload."""
+    d, src = pmc_record("", kernel, n, nnz, hw)
+    return (d.get("hbm_bytes_per_launch"), src) if d else (None, None)
+
+
+def parse_args():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=20)
     ap.add_argument("--warmup", type=int, default=3)
-    ap.add_argument("--n", type=int, default=10_000_000, help="rows per GPU")
-    ap.add_argument("--nnz-per-row", type=float, default=10.0)
-    ap.add_argument("--halfwidth", type=int, default=4096)
+    ap.add_argument("--config", choices=["c3", "c4"], default="c3")
+    ap.add_argument("--n", type=int, default=None, help="c3: rows per GPU (1e7); c4: rows in total (4e7)")
+    ap.add_argument("--nnz-per-row", type=float, default=None)
+    ap.add_argument("--halfwidth", type=int, default=None)
     ap.add_argument("--b", type=int, default=16)
     ap.add_argument("--unfused", action="store_true")
-    ap.add_argument("--cpu-iters", type=int, default=3)
-    ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--cpu-iters", type=int, default=None,
+                    help="oracle iterations after the start-up step; the first is a warm-up, the "
+                         "CPU baseline is the best of the rest (BASELINE.md 3: best of 5; c3 default 6, "
+                         "c4 default 2: BASELINE.md reports the C4 CPU baseline at C3 scale only)")
+    ap.add_argument("--no-cpu-baseline", action="store_true", help="skip the oracle leg (CPU baseline + parity)")
     ap.add_argument("--spmm-reps", type=int, default=20)
-    ap.add_argument("--c2-steps", type=int, default=200, help="single-vector Lanczos steps at BASELINE config 1 (0: skip)")
-    ap.add_argument("--c5-steps", type=int, default=10, help="block-32 fp32 power-law steps at BASELINE config 4 (0: skip)")
-    ap.add_argument("--rand-steps", type=int, default=10,
+    ap.add_argument("--c2-steps", type=int, default=None, help="single-vector Lanczos steps at BASELINE config 1 (0: skip)")
+    ap.add_argument("--c5-steps", type=int, default=None, help="block-32 fp32 power-law steps at BASELINE config 4 (0: skip)")
+    ap.add_argument("--rand-steps", type=int, default=None,
                     help="block-Lanczos steps on the C3 uniform-random-column stress operator (0: skip)")
     ap.add_argument("--exchange", choices=["halo", "allgather"], default="halo",
                     help="multi-GPU Krylov-block exchange (N > 1, or with --dist at N = 1)")
+    ap.add_argument("--no-second-exchange", action="store_true",
+                    help="c4, N > 1: do not time the other exchange form beside the headline one")
     ap.add_argument("--dist", action="store_true",
                     help="run the distributed entry point even at N = 1 (rehearsal of the N > 1 path)")
     args = ap.parse_args()
+    c4 = args.config == "c4"
+    for k, v3, v4 in (("n", 10_000_000, 40_000_000), ("nnz_per_row", 10.0, 25.0), ("halfwidth", 4096, 1 << 16),
+                      ("c2_steps", 200, 0), ("c5_steps", 10, 0), ("rand_steps", 10, 0), ("cpu_iters", 6, 2)):
+        if getattr(args, k) is None:
+            setattr(args, k, v4 if c4 else v3)
+    return args
+
+
+def main():
+    args = parse_args()
     # Native libraries write to fd 1 (RCCL prints a version banner at communicator
     # init): route fd 1 to stderr and keep the real stdout for the one JSON line.
     sys.stdout.flush()
@@ -133,106 +165,183 @@ def main():
 
     lz = ge.load_package()
     h = lz.Handle(local)
-    b, n = args.b, args.n
+    c4 = args.config == "c4"
+    b = args.b
     seed = 20261015
+    # the global operator and this rank's rows [r0, r1)
+    if c4:  # strong scaling: a fixed n_total split over the ranks
+        n_total = args.n
+        bounds = [n_total * g // world for g in range(world + 1)]
+    else:  # weak scaling: n rows per rank
+        n_total = args.n * world
+        bounds = [args.n * g for g in range(world + 1)]
+    r0, r1 = bounds[rank], bounds[rank + 1]
+    n = r1 - r0
     t_gen = time.time()
-    dist_path = world > 1 or args.dist
     if world == 1:
         A = lz.gen_banded(n, args.nnz_per_row, args.halfwidth, seed)
     else:
-        A = lz.gen_banded_local(n * world, rank * n, (rank + 1) * n, args.nnz_per_row, args.halfwidth, seed)
-    B = lz.uniform_B(n, b, seed + rank)
-    log(f"[rank {rank}] generated n={A.n} nnz={A.nnz} in {time.time() - t_gen:.1f}s")
+        A = lz.gen_banded_local(n_total, r0, r1, args.nnz_per_row, args.halfwidth, seed)
+    B = lz.uniform_B(n, b, seed, r0=r0)
+    log(f"[rank {rank}] generated rows [{r0}, {r1}) of n={n_total}: nnz={A.nnz} in {time.time() - t_gen:.1f}s")
     kw = dict(dtype=torch.float64, device="cuda")
     m_max = max(args.steps, args.warmup, 1)
     q = torch.zeros(m_max * b, **kw)
     alpha = torch.zeros(m_max, b, b, **kw)
     beta = torch.zeros(m_max + 1, b, b, **kw)
     Bd = torch.from_numpy(B).cuda()
-    halo_rows = 0
+    dist_path = world > 1 or args.dist
+    lc, lc_rank = 84, 0
 
-    if not dist_path:
-        Ad = lz.CsrDevice.from_host(A)
-        Q0, Q1, W = (torch.zeros(n, b, **kw) for _ in range(3))
+    def make_runner(exchange):
+        """(run(m), description, halo rows) for this rank's path."""
+        if not dist_path:
+            Ad = lz.CsrDevice.from_host(A)
+            Q0, Q1, W = (torch.zeros(n, b, **kw) for _ in range(3))
+
+            def run(m):
+                h.block_lanczos_blas(Ad, Bd, m, lc, q, alpha, beta, Q0, Q1, W, fused=not args.unfused)
+            return run, "single", 0, Ad
+        if exchange == "halo":
+            # only the referenced off-rank rows move each step
+            ccol, rcnt, hrows = lz.halo_plan(A.col, np.asarray(bounds, np.int64), rank)
+            h.halo_init(r0, n, rcnt, hrows)
+            nh = int(hrows.size)
+            Ad = lz.CsrDevice.from_host(lz.CsrHost(A.n, A.row_ptr, ccol, A.val), n_cols=n + nh)
+            X0, X1 = (torch.zeros(n + nh, b, **kw) for _ in range(2))
+            log(f"[rank {rank}] halo rows {nh}")
+
+            def run(m):
+                h.block_lanczos_halo(Ad, Bd, m, lc, lc_rank, q, alpha, beta, X0, X1)
+            return run, f"rows{world}+rccl_halo({nh} halo rows on rank {rank})", nh, Ad
+        # all-gather (north star): padded slabs, columns in the padded numbering
+        n_pad = max(bounds[g + 1] - bounds[g] for g in range(world))
+        pcol = lz.remap_cols_padded(A.col, np.asarray(bounds, np.int64), n_pad)
+        Ad = lz.CsrDevice.from_host(lz.CsrHost(A.n, A.row_ptr, pcol, A.val), n_cols=n_pad * world)
+        Bp = torch.zeros(n_pad, b, **kw)
+        Bp[:n] = Bd
+        Q0, W = (torch.zeros(n_pad, b, **kw) for _ in range(2))
+        X_full = torch.zeros(n_pad * world, b, **kw)
 
         def run(m):
-            h.block_lanczos_blas(Ad, Bd, m, 84, q, alpha, beta, Q0, Q1, W, fused=not args.unfused)
-    else:
+            h.block_lanczos_dist(Ad, n_pad, n_pad * world, Bp, m, lc, lc_rank, q, alpha, beta, Q0, W, X_full)
+        return run, f"rows{world}+rccl_allgather", 0, Ad
+
+    if dist_path:
         uid = [lz.comm_unique_id() if rank == 0 else None]
         if world > 1:
             dist.broadcast_object_list(uid, src=0)
         h.comm_init(world, rank, uid[0])
-        if args.exchange == "halo":
-            # rank g owns rows [g n, (g+1) n); only referenced off-rank rows move
-            bounds = np.arange(world + 1, dtype=np.int64) * n
-            ccol, rcnt, hrows = lz.halo_plan(A.col, bounds, rank)
-            h.halo_init(rank * n, n, rcnt, hrows)
-            halo_rows = int(hrows.size)
-            Ad = lz.CsrDevice.from_host(lz.CsrHost(A.n, A.row_ptr, ccol, A.val), n_cols=n + halo_rows)
-            X0, X1 = (torch.zeros(n + halo_rows, b, **kw) for _ in range(2))
-            log(f"[rank {rank}] halo rows {halo_rows}")
+    run, parallelism, halo_rows, Ad = make_runner(args.exchange)
 
-            def run(m):
-                h.block_lanczos_halo(Ad, Bd, m, 84, 0, q, alpha, beta, X0, X1)
-        else:
-            Ad = lz.CsrDevice.from_host(A, n_cols=n * world)
-            Q0, W = (torch.zeros(n, b, **kw) for _ in range(2))
-            X_full = torch.zeros(n * world, b, **kw)
+    def timed(run_fn, K, W):
+        """W warmup steps, then exactly K steps between barriers; max over ranks."""
+        if W > 0:
+            run_fn(W)
+        torch.cuda.synchronize()
+        h.prof_enable(True)
+        if world > 1:
+            dist.barrier()
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        run_fn(K)
+        torch.cuda.synchronize()
+        if world > 1:
+            dist.barrier()
+        el = time.perf_counter() - t0
+        prof = {c: h.prof_read(c) for c in (h.PROF_SPMM_PASS, h.PROF_UPDATE_PASS, h.PROF_SMALL, h.PROF_GRAM)}
+        h.prof_enable(False)
+        if world > 1:
+            t = torch.tensor([el], dtype=torch.float64, device="cuda")
+            dist.all_reduce(t, op=dist.ReduceOp.MAX)
+            el = float(t.item())
+        return el, prof
 
-            def run(m):
-                h.block_lanczos_dist(Ad, n, n * world, Bd, m, 84, 0, q, alpha, beta, Q0, W, X_full)
+    elapsed, prof = timed(run, args.steps, args.warmup)
+    # ---- the run checks itself: device error word, finite outputs
+    err = h.device_error()
+    if err != 0:
+        raise RuntimeError(f"device error word {err}: a persistent kernel abandoned a bounded spin; "
+                           "the timed results are invalid")
+    if not bool(torch.isfinite(alpha[: args.steps]).all()):
+        raise RuntimeError("non-finite alpha in the timed run")
+    K = args.steps
+    al_gpu = alpha[:K].cpu().numpy()
+    be_gpu = beta[: K + 1].cpu().numpy()
+    q_gpu = q[: K * b].cpu().numpy()
+    spmm_ms, spmm_cnt = prof[h.PROF_SPMM_PASS]
+    upd_ms, upd_cnt = prof[h.PROF_UPDATE_PASS]
+    small_ms, _ = prof[h.PROF_SMALL]
+    gram_ms, _ = prof[h.PROF_GRAM]
 
-    # ---- warmup
-    if args.warmup > 0:
-        run(args.warmup)
-    torch.cuda.synchronize()
+    # ---- c4, N > 1: the other exchange form on the same partition
+    other = None
+    if c4 and world > 1 and not args.no_second_exchange:
+        ex2 = "allgather" if args.exchange == "halo" else "halo"
+        del run, Ad
+        torch.cuda.empty_cache()
+        run2, par2, _, Ad = make_runner(ex2)
+        el2, _ = timed(run2, K, args.warmup)
+        if h.device_error() != 0:
+            raise RuntimeError(f"device error word set in the {ex2} run")
+        a2 = alpha[:K].cpu().numpy()
+        other = {"exchange": ex2, "parallelism": par2, "iters_per_s": round(K / el2, 3),
+                 "ms_per_step": round(el2 / K * 1e3, 4),
+                 "max_dalpha_vs_headline": float(np.max(np.abs(a2 - al_gpu)))}
+        del run2
 
-    # ---- timed region: exactly K steps
-    h.prof_enable(True)
-    if world > 1:
-        dist.barrier()
-    torch.cuda.synchronize()
-    t0 = time.perf_counter()
-    run(args.steps)
-    torch.cuda.synchronize()
-    if world > 1:
-        dist.barrier()
-    t1 = time.perf_counter()
-    elapsed = t1 - t0
-    spmm_ms, spmm_cnt = h.prof_read(h.PROF_SPMM_PASS)
-    upd_ms, upd_cnt = h.prof_read(h.PROF_UPDATE_PASS)
-    small_ms, small_cnt = h.prof_read(h.PROF_SMALL)
-    gram_ms, gram_cnt = h.prof_read(h.PROF_GRAM)
-    h.prof_enable(False)
-    if world > 1:
-        t = torch.tensor([elapsed], dtype=torch.float64, device="cuda")
-        dist.all_reduce(t, op=dist.ReduceOp.MAX)
-        elapsed = float(t.item())
-    assert torch.isfinite(alpha[: args.steps]).all(), "non-finite alpha"
-
-    # ---- plain SpMM kernel (the BASELINE headline kernel), same operator
+    # ---- plain SpMM kernel (the BASELINE headline kernel) on the same operator
     plain = None
-    if world == 1 and args.spmm_reps > 0:
+    if world == 1 and not dist_path and args.spmm_reps > 0:
         Y = torch.empty(n, b, **kw)
-        h.spmm(Ad, Q0, Y)
+        h.spmm(Ad, Bd, Y)
         torch.cuda.synchronize()
         h.prof_enable(True)
         for _ in range(args.spmm_reps):
-            h.spmm(Ad, Q0, Y)
+            h.spmm(Ad, Bd, Y)
         torch.cuda.synchronize()
         ms, cnt = h.prof_read(h.PROF_SPMM)
         h.prof_enable(False)
         t_avg = ms / cnt * 1e-3
         gbs = spmm_bytes(n, A.nnz, b) / t_avg / 1e9
-        plain = {"kernel": spmm_kernel(), "avg_ms": round(ms / cnt, 4),
+        plain = {"kernel": spmm_kernel(A.nnz, n), "avg_ms": round(ms / cnt, 4),
                  "bytes_per_launch": spmm_bytes(n, A.nnz, b), "achieved_GBs": round(gbs, 1),
                  "frac_of_hbm_peak": round(gbs / HBM_PEAK_GBS, 4)}
+        del Y
+
+    # ---- CPU oracle on the same operator and start block, rank 0, N = 1: the CPU
+    # baseline (best of the timed iterations) and the bench's own parity check
+    cpu = parity = None
+    if world == 1 and not args.no_cpu_baseline:
+        orc = ge.load_oracle()
+        m_o = min(K, 1 + max(1, args.cpu_iters))
+        t_o = time.time()
+        qo, ao, bo, t_each = orc.block_lanczos_timed(A, B, m_o, lc)
+        log(f"oracle: {m_o} steps in {time.time() - t_o:.1f}s")
+        samples = t_each[1:] if t_each.size > 1 else t_each  # the first iteration warms the caches
+        cpu = {"value": round(1.0 / float(samples.min()), 4), "unit": "iters/s", "cores": orc.num_threads(),
+               "kind": "port", "mean_iters_per_s": round(1.0 / float(samples.mean()), 4),
+               "sample": f"best of {samples.size} block-Lanczos iterations (after the start-up step and one "
+                         f"warm-up iteration) of the same n={n} nnz={A.nnz} b={b} fp64 operator and start "
+                         f"block, oracle/lz_oracle.c OpenMP"}
+        scale = max(1.0, np.abs(ao).max(), np.abs(bo[:m_o]).max())
+        r_gpu = lz.ritz_values(m_o, b, al_gpu[:m_o], be_gpu[: m_o + 1])
+        r_cpu = lz.ritz_values(m_o, b, ao, bo)
+        parity = {"steps_checked": m_o, "ritz_tol": RITZ_TOL,
+                  "max_dalpha_rel": float(np.max(np.abs(al_gpu[:m_o] - ao)) / scale),
+                  "max_dbeta_rel": float(np.max(np.abs(be_gpu[:m_o] - bo[:m_o])) / scale),
+                  "max_dq": float(np.max(np.abs(q_gpu[: m_o * b] - qo))),
+                  "max_dritz": float(np.max(np.abs(r_gpu - r_cpu))),
+                  "device_error": err, "against": "oracle/lz_oracle.c (CPU restatement), same A and B"}
+        parity["ok"] = parity["max_dritz"] <= RITZ_TOL and parity["max_dalpha_rel"] <= 1e-9
+        if not parity["ok"]:
+            raise RuntimeError(f"bench parity check failed: {parity}")
 
     # ---- BASELINE config 1 (single-vector Lanczos, n=1M, nnz=1e7): an extra line
     c2 = None
     if world == 1 and args.c2_steps > 0:
         n2 = 1_000_000
-        A2 = lz.gen_banded(n2, 10.0, args.halfwidth, seed)
+        A2 = lz.gen_banded(n2, 10.0, 4096, seed)
         A2d = lz.CsrDevice.from_host(A2)
         b2 = torch.from_numpy(lz.uniform_B(n2, 1, seed)[:, 0].copy()).cuda()
         k2 = args.c2_steps
@@ -253,7 +362,7 @@ def main():
     # ---- BASELINE config 4 (block Lanczos b=32 fp32, power-law rows): an extra line
     c5 = None
     if world == 1 and args.c5_steps > 0:
-        n5, k5 = args.n, args.c5_steps
+        n5, k5 = 10_000_000, args.c5_steps
         A5 = lz.gen_powerlaw(n5, 10.0, 2.1, 100000, seed=seed, dtype=np.float32)
         A5d = lz.CsrDevice.from_host(A5)
         kw5 = dict(dtype=torch.float32, device="cuda")
@@ -288,10 +397,11 @@ def main():
         ms_r, cnt_r = h.prof_read(h.PROF_SPMM)
         h.prof_enable(False)
         qr, alr, ber = torch.zeros(kr * b, **kw), torch.zeros(kr, b, b, **kw), torch.zeros(kr + 1, b, b, **kw)
-        h.block_lanczos_blas(Ard, Bd, 2, 84, qr, alr, ber, Q0, Q1, W)  # warm
+        Pr = [torch.zeros(n, b, **kw) for _ in range(3)]
+        h.block_lanczos_blas(Ard, Bd, 2, 84, qr, alr, ber, *Pr)  # warm
         torch.cuda.synchronize()
         t0c = time.perf_counter()
-        h.block_lanczos_blas(Ard, Bd, kr, 84, qr, alr, ber, Q0, Q1, W)
+        h.block_lanczos_blas(Ard, Bd, kr, 84, qr, alr, ber, *Pr)
         torch.cuda.synchronize()
         dtr = time.perf_counter() - t0c
         t_sp = ms_r / cnt_r * 1e-3
@@ -301,45 +411,61 @@ def main():
                "spmm_GBs": round(spmm_bytes(n, Ar.nnz, b) / t_sp / 1e9, 1),
                "spmm_frac_of_hbm_peak": round(spmm_bytes(n, Ar.nnz, b) / t_sp / 1e9 / HBM_PEAK_GBS, 4),
                "finite": bool(torch.isfinite(alr).all())}
-        # measured HBM traffic of this SpMM (committed PMC passes of the same operator)
+        # measured HBM traffic of this SpMM (committed PMC passes of the same operator): re-fetched
+        # bytes, NOT algorithmic throughput
         tr_r, src_r = pmc_traffic("k_spmm_seg_random_columns", n, Ar.nnz, n)
         if tr_r:
-            c3r.update({"spmm_pmc_hbm_bytes": tr_r, "spmm_pmc_GBs": round(tr_r / t_sp / 1e9, 1),
-                        "spmm_pmc_frac_of_hbm_peak": round(tr_r / t_sp / 1e9 / HBM_PEAK_GBS, 4),
+            c3r.update({"spmm_pmc_hbm_bytes": tr_r, "spmm_pmc_refetch_ratio": round(tr_r / spmm_bytes(n, Ar.nnz, b), 2),
+                        "spmm_pmc_hbm_GBs_incl_refetch": round(tr_r / t_sp / 1e9, 1),
                         "pmc_source": src_r})
-        del Ard, Yr
-
-    # ---- CPU baseline: the oracle (C, OpenMP) on this operator, rank 0, N = 1
-    cpu = None
-    if world == 1 and rank == 0 and not args.no_cpu_baseline:
-        orc = ge.load_oracle()
-        iters = max(1, args.cpu_iters)
-        t_cpu = orc.time_block_iters(A, B, iters)
-        cpu = {"value": round(iters / t_cpu, 4), "unit": "iters/s", "cores": orc.num_threads(),
-               "kind": "port",
-               "sample": f"{iters} block-Lanczos iterations (after the start-up step) of the same "
-                         f"n={n} nnz={A.nnz} b={b} fp64 operator, oracle/lz_oracle.c OpenMP"}
+        del Ard, Yr, Pr
 
     if rank == 0:
-        K = args.steps
-        value = world * K / elapsed
+        value = world * K / elapsed if not c4 else K / elapsed
         fused = not args.unfused
         t_pass = spmm_ms / max(spmm_cnt, 1) * 1e-3 if spmm_cnt else None
+        t_upd = upd_ms / max(upd_cnt, 1) * 1e-3 if upd_cnt else None
+        roof = mfma = None
+        hw = args.halfwidth
         if fused and t_pass:
             ach = fused_pass_bytes(n, A.nnz, b) / t_pass / 1e9
-            kname, kshort = fused_kernel()
-            traffic, tsrc = pmc_traffic(kshort, n, A.nnz, args.halfwidth)
+            kname, kshort = fused_kernel(A.nnz, n)
+            traffic, tsrc = pmc_traffic(kshort, n, A.nnz, hw)
             roof = {"bound": "hbm", "kernel": kname, "achieved": round(ach, 1),
                     "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": round(ach / HBM_PEAK_GBS, 4),
                     "traffic": traffic, "traffic_unit": "bytes/launch", "traffic_source": tsrc,
                     "avg_ms": round(t_pass * 1e3, 4),
                     "bytes_per_launch": fused_pass_bytes(n, A.nnz, b)}
+            # MFMA utilisation of the dense step (north star): algorithmic MFMA FLOP / kernel time
+            # against the fp64 MFMA peak, plus the rocprofv3 MfmaUtil counter of the same kernels
+            mfma = {"unit": "TFLOP/s", "peak": FP64_MFMA_PEAK_TFS, "dtype": "f64 (v_mfma_f64_16x16x4f64)",
+                    "pass2_update_gram": None, "pass1_epilogue": None}
+            for key, kern, fl, t in (("pass2_update_gram", "k_fused_update16", PASS2_MFMA_FLOP_PER_ROW, t_upd),
+                                     ("pass1_epilogue", kshort, PASS1_MFMA_FLOP_PER_ROW, t_pass)):
+                if not t:
+                    continue
+                tf = fl * n / t / 1e12
+                ent = {"kernel": kern, "mfma_flop_per_launch": fl * n, "avg_ms": round(t * 1e3, 4),
+                       "achieved": round(tf, 3), "frac": round(tf / FP64_MFMA_PEAK_TFS, 4)}
+                d, src = pmc_record("mfma", kern, n, A.nnz, hw)
+                if d:
+                    ent.update({"pmc_MfmaUtil_pct": d.get("MfmaUtil_pct"),
+                                "pmc_mfma_flop_per_launch": d.get("mfma_flop_per_launch"), "pmc_source": src})
+                mfma[key] = ent
         elif plain:
             roof = {"bound": "hbm", "kernel": plain["kernel"], "achieved": plain["achieved_GBs"],
                     "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": plain["frac_of_hbm_peak"], "traffic": None}
+        # iteration roofline: SURVEY.md 8(d)'s fixed convention (A + 8 n b s) and the bytes the
+        # Q-free design actually moves (A + 6 n b s); per rank
+        a_bytes = A.nnz * 12 + (n + 1) * 8
+        it_s = elapsed / K
+        if c4:
+            workload = (f"C4 block Lanczos b=16 fp64, banded-random symmetric CSR n={n_total} total "
+                        f"({world} rank(s), {n} rows on rank 0), nnz~{args.nnz_per_row:g}/row, "
+                        f"halfwidth {args.halfwidth}")
         else:
-            roof = None
-        iter_min_bytes = A.nnz * 12 + (n + 1) * 8 + 8 * n * b * 8  # SURVEY.md 8(d) convention, fixed
+            workload = ("C3 block Lanczos b=16 fp64, banded-random symmetric CSR "
+                        f"n={args.n} per GPU, nnz~{args.nnz_per_row:g}/row, halfwidth {args.halfwidth}")
         out = {
             "metric": "block-Lanczos iters/sec + SpMM achieved HBM GB/s vs peak, n=10M nnz=1e8 b=16",
             "value": round(value, 3),
@@ -349,21 +475,21 @@ def main():
             "warmup": args.warmup,
             "ms_per_step": round(elapsed / K * 1e3, 4),
             "higher_is_better": True,
-            "scaling": "weak",
+            "scaling": "strong" if c4 else "weak",
             "vs_baseline": None,
             "dtype": "f64",
             "data": "synthetic (splitmix64 banded-random symmetric CSR, seed 20261015)",
-            "config": {"workload": "C3 block Lanczos b=16 fp64, banded-random symmetric CSR "
-                                   f"n={n} per GPU, nnz~{args.nnz_per_row:g}/row, halfwidth {args.halfwidth}",
-                       "n_per_gpu": n, "nnz_per_gpu": A.nnz, "b": b, "m_timed": K,
+            "config": {"workload": workload, "config": args.config.upper(),
+                       "n_total": n_total, "n_per_gpu": n, "nnz_per_gpu": A.nnz, "b": b, "m_timed": K,
                        "path": "fused" if fused else "unfused",
-                       "parallelism": ("single" if not dist_path else
-                                       f"rows{world}+rccl_{args.exchange}" + (f"({halo_rows} halo rows/rank)"
-                                                                              if args.exchange == "halo" else ""))},
+                       "parallelism": parallelism},
             "roofline": roof,
             "cpu_baseline": cpu,
+            "parity": parity,
+            "mfma": mfma,
             "extra": {
                 "plain_spmm": plain,
+                "c4_other_exchange": other,
                 "c2_vector_lanczos": c2,
                 "c5_block32_f32_powerlaw": c5,
                 "c3_random_columns_stress": c3r,
@@ -371,8 +497,12 @@ def main():
                                        "update_pass": round(upd_ms / K, 4),
                                        "finish_sqrtm": round(small_ms / K, 4),
                                        "gram": round(gram_ms / K, 4)},
-                "iteration_frac_of_roofline": round(iter_min_bytes / (elapsed / K) / 1e9 / HBM_PEAK_GBS, 4),
-                "iteration_min_bytes": iter_min_bytes,
+                "iteration_frac_of_roofline": round((a_bytes + 8 * n * b * 8) / it_s / 1e9 / HBM_PEAK_GBS, 4),
+                "iteration_min_bytes": a_bytes + 8 * n * b * 8,
+                "iteration_frac_qfree_bytes": round((a_bytes + 6 * n * b * 8) / it_s / 1e9 / HBM_PEAK_GBS, 4),
+                "iteration_qfree_bytes": a_bytes + 6 * n * b * 8,
+                "iteration_bytes_note": "min_bytes: SURVEY.md 8(d) convention A + 8nbs (fixed); qfree_bytes: "
+                                        "A + 6nbs, what the implemented Q-free iteration moves",
             },
         }
         os.write(json_fd, (json.dumps(out) + "\n").encode())

@@ -104,6 +104,7 @@ HOST_SYMBOLS = [
     ("lzh_rand_B", _c_int, [_c_i64, _c_int, _c_u32, _c_i64, _c_int, _c_vp]),
     ("lzh_rand_lc", _c_i64, [_c_u32]),
     ("lzh_uniform_B", _c_int, [_c_i64, _c_int, _c_u64, _c_vp, _c_vp]),
+    ("lzh_uniform_B_rows", _c_int, [_c_i64, _c_i64, _c_int, _c_u64, _c_vp, _c_vp]),
     ("lzh_sym_eig", _c_int, [_c_int, _c_vp, _c_vp, _c_vp]),
     ("lzh_assemble_T", _c_int, [_c_int, _c_int, _c_vp, _c_vp, _c_vp]),
     ("lzh_ritz_values", _c_int, [_c_int, _c_int, _c_vp, _c_vp, _c_vp]),
@@ -281,13 +282,15 @@ def rand_lc(seed: int = 1) -> int:
     return int(host_lib().lzh_rand_lc(seed))
 
 
-def uniform_B(n: int, b: int, seed: int = 20261015, dtype=np.float64) -> np.ndarray:
+def uniform_B(n: int, b: int, seed: int = 20261015, dtype=np.float64, r0: int = 0) -> np.ndarray:
+    """Start block, uniform [1, 2) per row from a counter-based stream: rows
+    [r0, r0 + n) of the global block (a rank's slab)."""
     out = np.empty((n, b), dtype)
     L = host_lib()
     if dtype == np.float64:
-        L.lzh_uniform_B(n, b, seed, _p(out), None)
+        L.lzh_uniform_B_rows(r0, n, b, seed, _p(out), None)
     else:
-        L.lzh_uniform_B(n, b, seed, None, _p(out))
+        L.lzh_uniform_B_rows(r0, n, b, seed, None, _p(out))
     return out
 
 

@@ -100,7 +100,7 @@ static int axpy(lz_handle *h, int64_t n, T a, const T *x, T *y)
 // Reference op order, one kernel (or kernel pair) per reference call
 // (methods/block_lanczos.hpp:104-166).  Any b <= 32, fp64 or fp32.
 template <typename T>
-static int block_lanczos_unfused(lz_handle *h, int64_t n, const int64_t *rp, const int32_t *col,
+static int block_lanczos_unfused(lz_handle *h, int64_t n, int64_t nnz, const int64_t *rp, const int32_t *col,
                                  const T *val, int b, int m, int64_t lc, const T *B, T *q, T *alpha,
                                  T *beta, T *Q0, T *Q1, T *W)
 {
@@ -112,7 +112,7 @@ static int block_lanczos_unfused(lz_handle *h, int64_t n, const int64_t *rp, con
     LZ_TRY(sqrtm_pair<T>(h, b, nullptr, P, beta, binv, nullptr));
     LZ_TRY(tsmm<T>(h, n, b, T(0), T(1), B, binv, Q0, b));          // Q0 = B*beta_inv (:114)
     LZ_TRY(copy_row<T>(h, b, Q0, b, 0, lc, q));                     // (:118)
-    LZ_TRY(spmm_rm<T>(h, n, rp, col, val, b, Q0, b, n, W, b));          // W = A*Q0 (:121)
+    LZ_TRY(spmm_rm<T>(h, n, nnz, rp, col, val, b, Q0, b, n, W, b));          // W = A*Q0 (:121)
     LZ_TRY(gram_partials<T>(h, n, b, W, Q0, b, &P));                 // alpha[0] (:124)
     LZ_TRY(gram_finish<T>(h, b, P, 1, alpha));
     LZ_TRY(tsmm<T>(h, n, b, T(1), T(-1), Q0, alpha, W, b));          // W -= Q0*alpha (:128)
@@ -121,7 +121,7 @@ static int block_lanczos_unfused(lz_handle *h, int64_t n, const int64_t *rp, con
         LZ_TRY(gram_partials<T>(h, n, b, W, W, b, &P));              // (:137)
         LZ_TRY(sqrtm_pair<T>(h, b, nullptr, P, bj, binv, nullptr));  // (:142)
         LZ_TRY(tsmm<T>(h, n, b, T(0), T(1), W, binv, Q1, b));        // Q1 = W*beta_inv (:145)
-        LZ_TRY(spmm_rm<T>(h, n, rp, col, val, b, Q1, b, n, W, b));      // W = A*Q1 (:149)
+        LZ_TRY(spmm_rm<T>(h, n, nnz, rp, col, val, b, Q1, b, n, W, b));      // W = A*Q1 (:149)
         LZ_TRY(tsmm<T>(h, n, b, T(1), T(-1), Q0, bj, W, b));         // W -= Q0*beta (:152)
         LZ_TRY(gram_partials<T>(h, n, b, W, Q1, b, &P));             // alpha[j] (:155)
         LZ_TRY(gram_finish<T>(h, b, P, 1, aj));
@@ -142,12 +142,30 @@ static int block_lanczos_unfused(lz_handle *h, int64_t n, const int64_t *rp, con
 // j = 1 and from then on in place over W_{j-1} (row r read, then written, by
 // the same wave).  The inverse square roots of two consecutive steps live in
 // two scratch slots; beta[m] gets the last one, as the reference's.
+// Once-per-solve set-up of pass 1: the strips' row orders and, for a gather
+// source of 2^24+ rows, whether the windowed kernel applies.
+struct Pass1Plan {
+    const uint64_t *pairs = nullptr;
+    int win = 0;
+};
+static int pass1_plan(lz_handle *h, int64_t n, const int64_t *rp, const int32_t *col, int64_t nx, int64_t row_off,
+                      Pass1Plan *pl)
+{
+    LZ_TRY(strip_pairs(h, n, rp, &pl->pairs));
+    if (nx >= (1 << 24)) {
+        bool ok = false;
+        LZ_TRY(gather_window_ok(h, n, rp, col, nx, row_off, &ok));
+        pl->win = ok ? 1 : 0;
+    }
+    return LZ_OK;
+}
+
 struct QfreeBufs {
     double *binv[2], *P;
     explicit QfreeBufs(lz_handle *h) : binv{h->scratch + 4 * 256, h->scratch + 5 * 256}, P(h->scratch + 6 * 256) {}
 };
 
-static int block_lanczos_fused16(lz_handle *h, int64_t n, const int64_t *rp, const int32_t *col,
+static int block_lanczos_fused16(lz_handle *h, int64_t n, int64_t nnz, const int64_t *rp, const int32_t *col,
                                  const double *val, int m, int64_t lc, const double *B, double *q,
                                  double *alpha, double *beta, double *Q0, double *Q1, double *W)
 {
@@ -155,8 +173,8 @@ static int block_lanczos_fused16(lz_handle *h, int64_t n, const int64_t *rp, con
     (void)Q0;
     QfreeBufs qb(h);
     int P = 0;
-    const uint64_t *pairs = nullptr;
-    LZ_TRY(strip_pairs(h, n, rp, &pairs));
+    Pass1Plan pl;
+    LZ_TRY(pass1_plan(h, n, rp, col, n, 0, &pl));
     LZ_TRY(gram_partials<double>(h, n, 16, B, B, 16, &P));
     LZ_TRY(sqrtm_pair<double>(h, 16, nullptr, P, beta, qb.binv[0], nullptr));
     const double *in = B, *prev = nullptr;
@@ -164,7 +182,7 @@ static int block_lanczos_fused16(lz_handle *h, int64_t n, const int64_t *rp, con
         double *out = j == 0 ? W : j == 1 ? Q1 : const_cast<double *>(prev);
         const double *bi = qb.binv[j & 1];
         LZ_TRY(fused_spmm16(h, n, rp, col, val, in, n, in, prev, out, bi, j ? qb.P : nullptr, lc, q + j * 16, &P,
-                            pairs));
+                            pl.pairs, nnz, 0, pl.win));
         // alpha_j and P2 = beta_j^-1 alpha_j in one kernel (P1 of this step is consumed)
         LZ_TRY(gram_finish<double>(h, 16, P, 1, alpha + j * bb, h->partials2, bi, qb.P));
         LZ_TRY(fused_update16(h, n, out, in, qb.P, &P));
@@ -184,7 +202,7 @@ constexpr int64_t kFdtdGraph = 256;
 constexpr int64_t kFdtdFusedRows = 1 << 18;
 
 template <typename T>
-static int fdtd_block(lz_handle *h, int64_t n, const int64_t *rp, const int32_t *col, const T *val,
+static int fdtd_block(lz_handle *h, int64_t n, int64_t nnz, const int64_t *rp, const int32_t *col, const T *val,
                       int b, const T *U0, int64_t steps, double T_end, int64_t lc, T *U, T *D,
                       T *out)
 {
@@ -205,7 +223,7 @@ static int fdtd_block(lz_handle *h, int64_t n, const int64_t *rp, const int32_t 
             cur = nxt;
             return LZ_OK;
         }
-        LZ_TRY(spmm_rm<T>(h, n, rp, col, val, b, U, b, n, D, b));    // fdtd.hpp:48
+        LZ_TRY(spmm_rm<T>(h, n, nnz, rp, col, val, b, U, b, n, D, b));    // fdtd.hpp:48
         return axpy<T>(h, n * b, dt, D, U);                           // fdtd.hpp:49
     };
     // The reference runs 10^6 steps of two small launches each: launch-bound.
@@ -213,7 +231,7 @@ static int fdtd_block(lz_handle *h, int64_t n, const int64_t *rp, const int32_t 
     // allocate inside a capture) kFdtdGraph steps are captured into a hipGraph
     // once and replayed; the remainder runs eagerly.  Same kernels, same order;
     // kFdtdGraph is even, so every replay starts from the same ping-pong buffer.
-    static const char *graph_env = getenv("LZ_FDTD_GRAPH");  // "0": eager loop (A/B)
+    const char *graph_env = getenv("LZ_FDTD_GRAPH");  // "0": eager loop (A/B)
     const bool use_graph = !(graph_env && graph_env[0] == '0');
     int64_t s = 0;
     LZ_TRY(step());
@@ -278,7 +296,7 @@ static ncclComm_t comm_of(lz_handle *h) { return reinterpret_cast<ncclComm_t>(h-
 // local rows, two b x b ncclAllReduce (alpha and Gram partial sums), sqrtm
 // redundantly on every rank.  Local residual slabs (n_pad rows): W at step 0,
 // Q0 at step 1, then in place over the previous step's slab.
-static int block_lanczos_dist16(lz_handle *h, int64_t n_local, int64_t n_pad, const int64_t *rp,
+static int block_lanczos_dist16(lz_handle *h, int64_t n_local, int64_t n_pad, int64_t nnz, const int64_t *rp,
                                 const int32_t *col, const double *val, int m, int64_t lc_local,
                                 const double *B, double *q, double *alpha, double *beta, double *Q0,
                                 double *W, double *X)
@@ -289,8 +307,8 @@ static int block_lanczos_dist16(lz_handle *h, int64_t n_local, int64_t n_pad, co
     double *slab = h->scratch;  // one reduced b x b slab, all-reduced in place
     const double *own = X + (int64_t)h->rank * n_pad * 16;
     int P = 0;
-    const uint64_t *pairs = nullptr;
-    LZ_TRY(strip_pairs(h, n_local, rp, &pairs));
+    Pass1Plan pl;
+    LZ_TRY(pass1_plan(h, n_local, rp, col, n_pad * h->nranks, (int64_t)h->rank * n_pad, &pl));
     // beta_0 from the global Gram of B
     LZ_TRY(gram_partials<double>(h, n_local, 16, B, B, 16, &P));
     LZ_TRY(gram_finish<double>(h, 16, P, 0, slab));
@@ -302,7 +320,8 @@ static int block_lanczos_dist16(lz_handle *h, int64_t n_local, int64_t n_pad, co
         double *out = j == 0 ? W : j == 1 ? Q0 : const_cast<double *>(prev);
         const double *bi = qb.binv[j & 1];
         LZ_TRY(fused_spmm16(h, n_local, rp, col, val, X, n_pad * h->nranks, own, prev, out, bi,
-                            j ? qb.P : nullptr, lc_local, q + j * 16, &P, pairs));
+                            j ? qb.P : nullptr, lc_local, q + j * 16, &P, pl.pairs, nnz, (int64_t)h->rank * n_pad,
+                            pl.win));
         LZ_TRY(gram_finish<double>(h, 16, P, 0, slab, h->partials2));
         LZ_NCCL_TRY(ncclAllReduce(slab, slab, bb, ncclDouble, ncclSum, comm, h->stream));
         LZ_TRY(gram_finish<double>(h, 16, 1, 1, alpha + j * bb, slab, bi, qb.P));
@@ -400,7 +419,7 @@ static int allreduce_bb(lz_handle *h, double *slab)
 // by the halo exchange; the residual alternates between X0 and X1: the fused
 // pass gathers from one and writes the other, whose own rows hold W_{j-1}
 // (read, then overwritten, row by row) -- Q-free as block_lanczos_fused16.
-static int block_lanczos_halo16(lz_handle *h, const HaloPlan &hp, const int64_t *rp, const int32_t *col,
+static int block_lanczos_halo16(lz_handle *h, const HaloPlan &hp, int64_t nnz, const int64_t *rp, const int32_t *col,
                                 const double *val, int m, int64_t lc_local, const double *B, double *q,
                                 double *alpha, double *beta, double *X0, double *X1)
 {
@@ -409,8 +428,8 @@ static int block_lanczos_halo16(lz_handle *h, const HaloPlan &hp, const int64_t 
     QfreeBufs qb(h);
     double *slab = h->scratch;
     int P = 0;
-    const uint64_t *pairs = nullptr;
-    LZ_TRY(strip_pairs(h, n, rp, &pairs));
+    Pass1Plan pl;
+    LZ_TRY(pass1_plan(h, n, rp, col, nx, 0, &pl));
     LZ_TRY(gram_partials<double>(h, n, 16, B, B, 16, &P));
     LZ_TRY(gram_finish<double>(h, 16, P, 0, slab));
     LZ_TRY(allreduce_bb(h, slab));
@@ -422,7 +441,7 @@ static int block_lanczos_halo16(lz_handle *h, const HaloPlan &hp, const int64_t 
         double *in = xs[j & 1], *out = xs[(j + 1) & 1];
         const double *bi = qb.binv[j & 1];
         LZ_TRY(fused_spmm16(h, n, rp, col, val, in, nx, in, j ? out : nullptr, out, bi, j ? qb.P : nullptr,
-                            lc_local, q + j * 16, &P, pairs));
+                            lc_local, q + j * 16, &P, pl.pairs, nnz, 0, pl.win));
         LZ_TRY(gram_finish<double>(h, 16, P, 0, slab, h->partials2));
         LZ_TRY(allreduce_bb(h, slab));
         LZ_TRY(gram_finish<double>(h, 16, 1, 1, alpha + j * bb, slab, bi, qb.P));
@@ -467,22 +486,15 @@ int lz_device_ok(int device)
     return std::strncmp(prop.gcnArchName, "gfx950", 6) == 0 ? 1 : 0;
 }
 
-int lz_init(int device, lz_handle **out)
+// allocate the handle's workspaces; on any failure the caller frees the
+// partly built handle with lz_finalize (no leak on an error path)
+static int init_handle(lz_handle *h, int device)
 {
-    LZ_ARG_CHECK(out != nullptr, "out handle pointer is NULL");
-    *out = nullptr;
-    int count = 0;
-    LZ_HIP_TRY(hipGetDeviceCount(&count));
-    LZ_ARG_CHECK(device >= 0 && device < count, "device index");
-    LZ_HIP_TRY(hipSetDevice(device));
-    lz_handle *h = new lz_handle();
     h->device = device;
     hipDeviceProp_t prop;
     LZ_HIP_TRY(hipGetDeviceProperties(&prop, device));
     if (std::strncmp(prop.gcnArchName, "gfx950", 6) != 0) {
-        set_error("device %d is %s, liblz_hip.so is built for gfx950 only", device,
-                  prop.gcnArchName);
-        delete h;
+        set_error("device %d is %s, liblz_hip.so is built for gfx950 only", device, prop.gcnArchName);
         return LZ_E_HIP;
     }
     h->n_cu = prop.multiProcessorCount;
@@ -496,6 +508,23 @@ int lz_init(int device, lz_handle **out)
         LZ_HIP_TRY(hipMemset(h->partials, 0xFF, sizeof(double) * h->partials_cap));
         LZ_HIP_TRY(hipMemset(h->partials2, 0xFF, sizeof(double) * (256 * kMaxB * kMaxB + 4096 * 256)));
         LZ_HIP_TRY(hipMemset(h->scratch, 0xFF, sizeof(double) * 8 * kMaxB * kMaxB));
+    }
+    return LZ_OK;
+}
+
+int lz_init(int device, lz_handle **out)
+{
+    LZ_ARG_CHECK(out != nullptr, "out handle pointer is NULL");
+    *out = nullptr;
+    int count = 0;
+    LZ_HIP_TRY(hipGetDeviceCount(&count));
+    LZ_ARG_CHECK(device >= 0 && device < count, "device index");
+    LZ_HIP_TRY(hipSetDevice(device));
+    lz_handle *h = new lz_handle();
+    const int rc = init_handle(h, device);
+    if (rc != LZ_OK) {
+        lz_finalize(h);
+        return rc;
     }
     *out = h;
     return LZ_OK;
@@ -601,16 +630,16 @@ int lz_csr_spmm(lz_handle *h, int64_t n_rows, int64_t n_cols, int64_t nnz, const
     if (layout == LZ_ROW_MAJOR) {
         LZ_ARG_CHECK(ldx >= b && ldy >= b, "row-major ld >= b");
         if (dtype == LZ_F64)
-            return spmm_rm<double>(h, n_rows, rp, col, (const double *)val, b, (const double *)X,
+            return spmm_rm<double>(h, n_rows, nnz, rp, col, (const double *)val, b, (const double *)X,
                                    ldx, n_cols, (double *)Y, ldy);
-        return spmm_rm<float>(h, n_rows, rp, col, (const float *)val, b, (const float *)X, ldx,
+        return spmm_rm<float>(h, n_rows, nnz, rp, col, (const float *)val, b, (const float *)X, ldx,
                               n_cols, (float *)Y, ldy);
     }
     LZ_ARG_CHECK(ldx >= n_cols && ldy >= n_rows, "column-major ld >= rows");
     if (dtype == LZ_F64)
-        return spmm_cm<double>(h, n_rows, rp, col, (const double *)val, b, (const double *)X, ldx, n_cols,
+        return spmm_cm<double>(h, n_rows, nnz, rp, col, (const double *)val, b, (const double *)X, ldx, n_cols,
                                (double *)Y, ldy);
-    return spmm_cm<float>(h, n_rows, rp, col, (const float *)val, b, (const float *)X, ldx, n_cols,
+    return spmm_cm<float>(h, n_rows, nnz, rp, col, (const float *)val, b, (const float *)X, ldx, n_cols,
                           (float *)Y, ldy);
 }
 
@@ -713,11 +742,11 @@ int lz_block_lanczos_unfused(lz_handle *h, int64_t n, int64_t nnz, const int64_t
     LZ_HANDLE_CHECK(h);
     LZ_TRY(block_args(n, nnz, rp, col, val, b, m, lc, B, q, alpha, beta, Q0, Q1, W));
     if (dtype == LZ_F64)
-        return block_lanczos_unfused<double>(h, n, rp, col, (const double *)val, b, m, lc,
+        return block_lanczos_unfused<double>(h, n, nnz, rp, col, (const double *)val, b, m, lc,
                                              (const double *)B, (double *)q, (double *)alpha,
                                              (double *)beta, (double *)Q0, (double *)Q1,
                                              (double *)W);
-    return block_lanczos_unfused<float>(h, n, rp, col, (const float *)val, b, m, lc,
+    return block_lanczos_unfused<float>(h, n, nnz, rp, col, (const float *)val, b, m, lc,
                                         (const float *)B, (float *)q, (float *)alpha,
                                         (float *)beta, (float *)Q0, (float *)Q1, (float *)W);
 }
@@ -729,7 +758,7 @@ int lz_block_lanczos(lz_handle *h, int64_t n, int64_t nnz, const int64_t *rp, co
     LZ_HANDLE_CHECK(h);
     LZ_TRY(block_args(n, nnz, rp, col, val, b, m, lc, B, q, alpha, beta, Q0, Q1, W));
     if (dtype == LZ_F64 && b == 16)
-        return block_lanczos_fused16(h, n, rp, col, (const double *)val, m, lc,
+        return block_lanczos_fused16(h, n, nnz, rp, col, (const double *)val, m, lc,
                                      (const double *)B, (double *)q, (double *)alpha,
                                      (double *)beta, (double *)Q0, (double *)Q1, (double *)W);
     return lz_block_lanczos_unfused(h, n, nnz, rp, col, val, dtype, b, m, lc, B, q, alpha, beta,
@@ -760,9 +789,9 @@ int lz_fdtd_block(lz_handle *h, int64_t n, int64_t nnz, const int64_t *rp, const
     LZ_TRY(check_csr(n, nnz, rp, col, val));
     LZ_ARG_CHECK(steps >= 1 && lc >= 0 && lc < n && U0 && U && D && out, "fdtd args");
     if (dtype == LZ_F64)
-        return fdtd_block<double>(h, n, rp, col, (const double *)val, b, (const double *)U0, steps,
+        return fdtd_block<double>(h, n, nnz, rp, col, (const double *)val, b, (const double *)U0, steps,
                                   T_end, lc, (double *)U, (double *)D, (double *)out);
-    return fdtd_block<float>(h, n, rp, col, (const float *)val, b, (const float *)U0, steps,
+    return fdtd_block<float>(h, n, nnz, rp, col, (const float *)val, b, (const float *)U0, steps,
                              T_end, lc, (float *)U, (float *)D, (float *)out);
 }
 
@@ -810,11 +839,12 @@ int lz_block_lanczos_dist(lz_handle *h, int64_t n_local, int64_t n_pad, int64_t 
     LZ_ARG_CHECK(h->comm != nullptr, "lz_comm_init first");
     LZ_TRY(check_csr(n_local, nnz_local, rp, col, val));
     LZ_ARG_CHECK(dtype == LZ_F64 && b == 16, "distributed path: b = 16 fp64");
-    LZ_ARG_CHECK(n_pad >= n_local && n_pad * h->nranks >= n_global && m >= 1, "dist sizes");
+    LZ_ARG_CHECK(n_pad >= n_local && n_pad * h->nranks == n_global && m >= 1,
+                 "dist sizes: n_pad >= n_local and n_global == n_pad * nranks (padded numbering)");
     LZ_ARG_CHECK(B_local && q && alpha && beta && Q0 && W && X_full, "NULL buffer");
     (void)Q1;
     const int64_t lc = (lc_rank == h->rank) ? lc_local : -1;
-    return block_lanczos_dist16(h, n_local, n_pad, rp, col, (const double *)val, m, lc,
+    return block_lanczos_dist16(h, n_local, n_pad, nnz_local, rp, col, (const double *)val, m, lc,
                                 (const double *)B_local, (double *)q, (double *)alpha,
                                 (double *)beta, (double *)Q0, (double *)W, (double *)X_full);
 }
@@ -965,7 +995,7 @@ int lz_block_lanczos_halo(lz_handle *h, int64_t n_local, int64_t nnz_local, cons
     LZ_ARG_CHECK(m >= 1 && n_local >= 1, "sizes");
     LZ_ARG_CHECK(B_local && q && alpha && beta && X0 && X1 && X0 != X1, "NULL / aliased buffer");
     const int64_t lc = (lc_rank == h->rank) ? lc_local : -1;
-    return block_lanczos_halo16(h, hp, rp, col, (const double *)val, m, lc, (const double *)B_local,
+    return block_lanczos_halo16(h, hp, nnz_local, rp, col, (const double *)val, m, lc, (const double *)B_local,
                                 (double *)q, (double *)alpha, (double *)beta, (double *)X0, (double *)X1);
 }
 

@@ -503,296 +503,9 @@ int strip_pairs(lz_handle *h, int64_t n, const int64_t *rp, const uint64_t **out
     return LZ_OK;
 }
 
-// DMA NC 16-row strips of a row-major n x 16 block (buffer `r` based at the
-// tile's first row) into dst in slot order: strip j, slot c4*16 + r holds row
-// 16j + r, doubles 2c4, 2c4+1.
-template <int NC>
-__device__ __forceinline__ void fw_strips_dma(__amdgpu_buffer_rsrc_t r, double *dst, int lane)
-{
-#pragma unroll
-    for (int j = 0; j < NC; ++j)
-#pragma unroll
-        for (int h2 = 0; h2 < 2; ++h2) {
-            const int slot = 64 * h2 + lane, c4 = slot >> 4, rr = slot & 15;
-            const uint32_t off = (uint32_t)(((16 * j + rr) * 16 + 2 * c4) * 8);
-            __builtin_amdgcn_raw_ptr_buffer_load_lds(r, (ws_lds_t *)(dst + 256 * j + 128 * h2), 16, off, 0, 0, 0);
-        }
-}
-
 // 16x16 scratch with XOR swizzle: element (r, c) at r*16 + (c ^ r); the MFMA
 // operand read (16 rows, one column per lane group) hits 16 distinct banks.
 __device__ __forceinline__ int fw_sw(int r, int c) { return r * 16 + (c ^ r); }
-
-template <int NC, int CAP, int FW_K, bool QREG = false, int NL = 1>
-__global__ __launch_bounds__(64 * (NC + NL)) void k_fused_ws16(
-    int64_t n, const int64_t *__restrict__ rp, const int32_t *__restrict__ col,
-    const double *__restrict__ val, const double *__restrict__ Wg, int64_t nx,
-    const double *__restrict__ Wown, const double *Qbuf, double *Wn,
-    const double *__restrict__ binv, const double *__restrict__ beta, int64_t lc,
-    double *__restrict__ qrow, double *__restrict__ part, int *__restrict__ err)
-{
-    using C = FwCfg<NC, CAP, QREG>;
-    constexpr int TR = C::TR;
-#ifdef LZ_WS_PROBE
-    // diagnostic timing masks (results invalid): bit 0 Q DMA, bit 2 stores, bit 3 gathers
-    const int dbg = lz_ws_dbg;
-#else
-    constexpr int dbg = 0;
-#endif
-    __shared__ typename C::Stage st[FW_K];
-    __shared__ double ops[2][256];  // beta^-1, -beta in MFMA B-operand order
-    __shared__ int ready[FW_K], done[FW_K];
-    __shared__ double scr[QREG ? NC : 1][256];  // QREG: per-consumer transpose scratch
-    const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
-    const bool has_prev = beta != nullptr;
-    if (threadIdx.x < FW_K) {
-        ready[threadIdx.x] = -1;
-        done[threadIdx.x] = 0;
-    }
-    for (int e = threadIdx.x; e < 256; e += blockDim.x) {
-        const int kc = e >> 6, l = e & 63;
-        const int idx = (4 * kc + (l >> 4)) * 16 + (l & 15);
-        ops[0][e] = binv[idx];
-        ops[1][e] = has_prev ? -beta[idx] : 0.0;
-    }
-    __syncthreads();  // the only block barrier
-    const int64_t T = ceil_div(n, (int64_t)TR);
-    int64_t begin, end, k, K;
-    {
-        const int64_t G = gridDim.x, b = blockIdx.x;
-        if (G < 8) {
-            begin = 0; end = T; k = b; K = G;
-        } else {
-            const int64_t x = b & 7;
-            begin = T * x / 8;
-            end = T * (x + 1) / 8;
-            k = b >> 3;
-            K = (G - x + 7) >> 3;
-        }
-    }
-    const int64_t nt = (end - begin - k + K - 1) / K > 0 ? (end - begin - k + K - 1) / K : 0;
-    auto tile_r0 = [&](int64_t i) { return (begin + k + i * K) * TR; };
-    if (NL > 1 && w < NL) {
-        // ------------------------------------------------ NL parallel loaders
-        // loader l stages tiles l, l + NL, ...: one tile in flight per loader,
-        // published as soon as it lands (its own vmcnt(0)), so NL tiles are in
-        // flight and a slow consumer delays only the slot it holds
-        __builtin_amdgcn_s_setprio(3);
-        const int64_t nnz = rp[n];
-        for (int64_t i = w; i < nt; i += NL) {
-            const int s = (int)(i % FW_K);
-            const int64_t r0 = tile_r0(i), r1 = (r0 + TR < n) ? r0 + TR : n;
-            const int64_t kA = rp[r0];
-            if (i >= FW_K) {
-                long spin = 0;
-                const uint32_t da = ws_lds_addr(&done[s]);
-                while (ws_lds_read(da) < NC * (int)(i / FW_K) && ++spin < kWsSpin) __builtin_amdgcn_s_sleep(1);
-                if (spin >= kWsSpin) { *err = 3; break; }
-            }
-            WS_TL(i, 0);
-            const int64_t ca = kA & ~(int64_t)3, va = kA & ~(int64_t)1;
-            const int64_t cb = (nnz - ca) * 4, vb = (nnz - va) * 8;
-            const auto rr = __builtin_amdgcn_make_buffer_rsrc(const_cast<int64_t *>(rp + r0), (short)0,
-                                                              (int)((r1 - r0 + 1) * 8), 0x00020000);
-            const auto cr = __builtin_amdgcn_make_buffer_rsrc(const_cast<int32_t *>(col + ca), (short)0,
-                                                              (int)(cb < 0x7fffffff ? cb : 0x7fffffff), 0x00020000);
-            const auto vr = __builtin_amdgcn_make_buffer_rsrc(const_cast<double *>(val + va), (short)0,
-                                                              (int)(vb < 0x7fffffff ? vb : 0x7fffffff), 0x00020000);
-            ws_dma(rr, st[s].rp, C::RP_PIECES, lane);
-            ws_dma(cr, st[s].col, C::COL_PIECES, lane);
-            ws_dma(vr, st[s].val, C::VAL_PIECES, lane);
-            if constexpr (!QREG) {
-                const auto qr = __builtin_amdgcn_make_buffer_rsrc(const_cast<double *>(Qbuf) + r0 * 16, (short)0,
-                                                                  has_prev && !(dbg & 1) ? (int)((r1 - r0) * 128) : 0,
-                                                                  0x00020000);
-                fw_strips_dma<NC>(qr, st[s].qt, lane);
-            }
-            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-            if (lane == 0) ws_lds_write(ws_lds_addr(&ready[s]), (int)i);
-            WS_TL(i, 1);
-        }
-        return;
-    }
-    if (w == 0) {
-        // ------------------------------------------------------------ loader
-        // highest issue priority: the loader's DMA must not queue behind the
-        // consumers' gathers, or the consumers starve waiting for stages
-        __builtin_amdgcn_s_setprio(3);
-#ifdef LZ_WS_PROBE
-        long long c_done = 0;
-        const long long c_start = clock64();
-#endif
-        const int64_t nnz = rp[n];
-        int64_t kA_next = nt > 0 ? rp[tile_r0(0)] : 0;
-        for (int64_t i = 0; i < nt; ++i) {
-            const int s = (int)(i % FW_K);
-            const int64_t r0 = tile_r0(i), r1 = (r0 + TR < n) ? r0 + TR : n;
-            const int64_t kA = kA_next;
-            if (i + 1 < nt) kA_next = rp[tile_r0(i + 1)];
-            if (i >= FW_K) {
-                long spin = 0;
-                WS_T(t0);
-                const uint32_t da = ws_lds_addr(&done[s]);
-                while (ws_lds_read(da) < NC * (int)(i / FW_K) && ++spin < kWsSpin) __builtin_amdgcn_s_sleep(1);
-                if (spin >= kWsSpin) { *err = 3; break; }
-#ifdef LZ_WS_PROBE
-                c_done += clock64() - t0;
-#endif
-            }
-            WS_TL(i, 0);
-            const int64_t ca = kA & ~(int64_t)3, va = kA & ~(int64_t)1;
-            const int64_t cb = (nnz - ca) * 4, vb = (nnz - va) * 8;
-            const auto rr = __builtin_amdgcn_make_buffer_rsrc(const_cast<int64_t *>(rp + r0), (short)0,
-                                                              (int)((r1 - r0 + 1) * 8), 0x00020000);
-            const auto cr = __builtin_amdgcn_make_buffer_rsrc(const_cast<int32_t *>(col + ca), (short)0,
-                                                              (int)(cb < 0x7fffffff ? cb : 0x7fffffff), 0x00020000);
-            const auto vr = __builtin_amdgcn_make_buffer_rsrc(const_cast<double *>(val + va), (short)0,
-                                                              (int)(vb < 0x7fffffff ? vb : 0x7fffffff), 0x00020000);
-            const auto qr = __builtin_amdgcn_make_buffer_rsrc(const_cast<double *>(Qbuf) + r0 * 16, (short)0,
-                                                              has_prev && !(dbg & 1) ? (int)((r1 - r0) * 128) : 0,
-                                                              0x00020000);
-            ws_dma(rr, st[s].rp, C::RP_PIECES, lane);
-            ws_dma(cr, st[s].col, C::COL_PIECES, lane);
-            ws_dma(vr, st[s].val, C::VAL_PIECES, lane);
-            if constexpr (!QREG) fw_strips_dma<NC>(qr, st[s].qt, lane);
-            if (i >= 1) {  // tile i-1 has landed once only tile i's DMA is younger
-                asm volatile("s_waitcnt vmcnt(%0)" ::"n"(C::DMA_INSTR) : "memory");
-                if (lane == 0) ws_lds_write(ws_lds_addr(&ready[(int)((i - 1) % FW_K)]), (int)(i - 1));
-                WS_TL(i - 1, 1);
-            }
-        }
-        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-        if (nt > 0 && lane == 0) ws_lds_write(ws_lds_addr(&ready[(int)((nt - 1) % FW_K)]), (int)(nt - 1));
-#ifdef LZ_WS_PROBE
-        if (lane == 0) {
-            lz_ws_probe[8 * blockIdx.x + 4] = clock64() - c_start;
-            lz_ws_probe[8 * blockIdx.x + 5] = nt;
-            lz_ws_probe[8 * blockIdx.x + 1] = c_done;
-        }
-#endif
-        return;
-    }
-    // -------------------------------------------------------------- consumers
-    const int cw = w - NL, g = lane >> 3, p = lane & 7;
-    const __amdgpu_buffer_rsrc_t xr = __builtin_amdgcn_make_buffer_rsrc(const_cast<double *>(Wg), (short)0,
-                                                                        (dbg & 8) ? 0 : (int)(nx * 128), 0x00020000);
-    const uint32_t lane_off = 16u * p;
-    d4_t macc = {0.0, 0.0, 0.0, 0.0};
-#ifdef LZ_WS_PROBE
-    long long c_ready = 0, c_gather = 0;
-    const long long c_cstart = clock64();
-#endif
-    for (int64_t i = 0; i < nt; ++i) {
-        const int s = (int)(i % FW_K);
-        const int64_t r0 = tile_r0(i);
-        const int64_t s0 = r0 + 16 * cw;  // this wave's strip
-        // own W rows (L2): lane holds row s0 + (lane >> 2), doubles 4(lane&3)..+3
-        double wv[4], qv[4] = {0.0, 0.0, 0.0, 0.0};
-        tile_load(Wown, s0, n, lane, wv);
-        if (QREG && has_prev) tile_load(Qbuf, s0, n, lane, qv);  // Q_{j-1} rows (L2: touched)
-        long spin = 0;
-        WS_T(t2);
-        while (__hip_atomic_load(&ready[s], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP) != (int)i &&
-               ++spin < kWsSpin)
-            __builtin_amdgcn_s_sleep(1);
-        if (spin >= kWsSpin) { *err = 4; break; }
-#ifdef LZ_WS_PROBE
-        c_ready += clock64() - t2;
-#endif
-        WS_TL(i, 2 + 2 * cw);
-        asm volatile("" ::: "memory");
-        typename C::Stage &S = st[s];
-        const int64_t kA = S.rp[0];
-        const int co = (int)(kA & 3), vo = (int)(kA & 1);
-        const int nrow = (int)(n - r0 < TR ? n - r0 : TR);
-        const int runlen = (int)(S.rp[nrow] - kA);
-        const int lr = 16 * cw + g;
-        const int o0 = lr < nrow ? (int)(S.rp[lr] - kA) : 0;
-        const int len0 = lr < nrow ? (int)(S.rp[lr + 1] - kA) - o0 : 0;
-        const int o1 = lr + 8 < nrow ? (int)(S.rp[lr + 8] - kA) : 0;
-        const int len1 = lr + 8 < nrow ? (int)(S.rp[lr + 9] - kA) - o1 : 0;
-        double y[4] = {0.0, 0.0, 0.0, 0.0};
-        WS_T(t3);
-        if (runlen <= CAP)  // tile-uniform, outside the loop (see k_spmm_ws)
-            ws_gather(S.col + co, S.val + vo, o0, len0, o1, len0 + len1, xr, lane_off, y);
-        else
-            ws_gather(col + kA, val + kA, o0, len0, o1, len0 + len1, xr, lane_off, y);
-#ifdef LZ_WS_PROBE
-        c_gather += clock64() - t3;
-#endif
-        if constexpr (QREG) {  // the stage holds only the CSR run: release it now
-            asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-            if (lane == 0) atomicAdd(&done[s], 1);
-        }
-        // ---- epilogue operands (A operand a[kc] = M[l&15][4kc + (l>>4)])
-        double *Sc = QREG ? scr[cw] : S.qt + 256 * cw;  // Q strip, then this wave's scratch
-        double ya[4], wa[4], qa[4];
-        const int ar = lane & 15;
-        if constexpr (QREG) {
-#pragma unroll
-            for (int q = 0; q < 4; ++q) Sc[fw_sw(lane >> 2, 4 * (lane & 3) + q)] = qv[q];
-            wave_lds_sync();
-#pragma unroll
-            for (int kc = 0; kc < 4; ++kc) qa[kc] = Sc[fw_sw(ar, 4 * kc + (lane >> 4))];
-        } else {
-#pragma unroll
-            for (int kc = 0; kc < 4; ++kc) {
-                const int c = 4 * kc + (lane >> 4);
-                qa[kc] = Sc[((c >> 1) * 16 + ar) * 2 + (c & 1)];
-            }
-        }
-        wave_lds_sync();
-        // W rows -> scratch -> operand
-#pragma unroll
-        for (int q = 0; q < 4; ++q) Sc[fw_sw(lane >> 2, 4 * (lane & 3) + q)] = (s0 + (lane >> 2) < n) ? wv[q] : 0.0;
-        wave_lds_sync();
-#pragma unroll
-        for (int kc = 0; kc < 4; ++kc) wa[kc] = Sc[fw_sw(ar, 4 * kc + (lane >> 4))];
-        wave_lds_sync();
-        // Y rows -> scratch -> operand
-        Sc[fw_sw(g, 2 * p)] = y[0];
-        Sc[fw_sw(g, 2 * p + 1)] = y[1];
-        Sc[fw_sw(g + 8, 2 * p)] = y[2];
-        Sc[fw_sw(g + 8, 2 * p + 1)] = y[3];
-        wave_lds_sync();
-#pragma unroll
-        for (int kc = 0; kc < 4; ++kc) ya[kc] = Sc[fw_sw(ar, 4 * kc + (lane >> 4))];
-        if constexpr (!QREG) {  // the stage is no longer used by this wave
-            asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-            if (lane == 0) atomicAdd(&done[s], 1);
-        }
-        d4_t q1 = {0.0, 0.0, 0.0, 0.0}, wn = {0.0, 0.0, 0.0, 0.0};
-#pragma unroll
-        for (int kc = 0; kc < 4; ++kc) q1 = mfma16(wa[kc], ops[0][64 * kc + lane], q1);
-#pragma unroll
-        for (int kc = 0; kc < 4; ++kc) wn = mfma16(ya[kc], ops[0][64 * kc + lane], wn);
-        if (has_prev) {
-#pragma unroll
-            for (int kc = 0; kc < 4; ++kc) wn = mfma16(qa[kc], ops[1][64 * kc + lane], wn);
-        }
-#pragma unroll
-        for (int r = 0; r < 4; ++r) {
-            const int64_t row = s0 + (lane >> 4) + 4 * r;
-            if (row < n && !(dbg & 4)) {
-                Wn[s0 * 16 + 64 * r + lane] = wn[r];
-                if (row == lc) qrow[lane & 15] = q1[r];
-            }
-        }
-#pragma unroll
-        for (int r = 0; r < 4; ++r) macc = mfma16(q1[r], wn[r], macc);
-        WS_TL(i, 3 + 2 * cw);
-    }
-    double *slab = part + ((int64_t)blockIdx.x * NC + cw) * 256;
-#pragma unroll
-    for (int r = 0; r < 4; ++r) slab[((lane >> 4) + 4 * r) * 16 + (lane & 15)] = macc[r];
-#ifdef LZ_WS_PROBE
-    if (cw == 0 && lane == 0) {
-        lz_ws_probe[8 * blockIdx.x + 2] = c_ready;
-        lz_ws_probe[8 * blockIdx.x + 3] = clock64() - c_cstart;
-        lz_ws_probe[8 * blockIdx.x + 0] = c_gather;
-    }
-#endif
-}
 
 // ---------------------------------------------------------------------------
 // Pipelined wave-specialised pass 1.  Timelines of k_fused_ws16
@@ -806,15 +519,22 @@ __global__ __launch_bounds__(64 * (NC + NL)) void k_fused_ws16(
 //   of strip i-1 (its Y tile parked in LDS, its W / Q_{j-1} rows loaded into
 //   registers after strip i-1's gather), so the epilogue hides the first
 //   gather round trip;
-template <int NC, int CAP, int K, int NL, bool BP = false>
+// WIN: the gather source has 2^24 rows or more (X >= 2 GiB: past a 32-bit
+//   buffer offset); each strip gathers through a window of kWinRows rows
+//   centred on its own row (row_off + s0; a once-per-solve check,
+//   gather_window_ok, proved every column of the strip lies inside it), so the
+//   buffer-addressed gather keeps working at any n (BASELINE config C4: 40M
+//   rows on one GPU, or the all-gathered block at N >= 2).
+template <int NC, int CAP, int K, int NL, bool WIN = false>
 __global__ __launch_bounds__(64 * (NC + NL)) void k_fused_pp16(
     int64_t n, const int64_t *__restrict__ rp, const int32_t *__restrict__ col,
     const double *__restrict__ val, const double *__restrict__ Wg, int64_t nx,
     const double *__restrict__ Wown, const double *Qbuf, double *Wn,
     const double *__restrict__ binv, const double *__restrict__ beta, int64_t lc,
     double *__restrict__ qrow, double *__restrict__ part, int *__restrict__ err,
-    const uint64_t *__restrict__ pairs)
+    const uint64_t *__restrict__ pairs, int64_t row_off)
 {
+    constexpr bool BP = true;
     using C = FwCfg<NC, CAP, true, BP>;
     constexpr int TR = C::TR;
 #ifdef LZ_WS_PROBE
@@ -912,8 +632,10 @@ __global__ __launch_bounds__(64 * (NC + NL)) void k_fused_pp16(
         if (pr == 1) __builtin_amdgcn_s_setprio(1);
         else if (pr == 2) __builtin_amdgcn_s_setprio(2);
     }
-    const __amdgpu_buffer_rsrc_t xr =
-        __builtin_amdgcn_make_buffer_rsrc(const_cast<double *>(Wg), (short)0, (int)(nx * 128), 0x00020000);
+    __amdgpu_buffer_rsrc_t xr =
+        __builtin_amdgcn_make_buffer_rsrc(const_cast<double *>(Wg), (short)0, (int)(WIN ? kWinRows * 128 : nx * 128),
+                                          0x00020000);
+    uint32_t wb = 0;  // WIN: first row of the strip's gather window
     double *S0 = scr[cw];
     d4_t macc = {0.0, 0.0, 0.0, 0.0};
     // the pending strip's W_j and W_{j-1} rows, loaded straight into MFMA
@@ -969,6 +691,14 @@ __global__ __launch_bounds__(64 * (NC + NL)) void k_fused_pp16(
         const int64_t s0 = r0 + 16 * cw;
         const int g = lane >> 3, p = lane & 7;
         const uint32_t lane_off = 16u * p;
+        if constexpr (WIN) {  // the strip's window: kWinRows rows centred on it
+            const int64_t hi = nx - kWinRows > 0 ? nx - kWinRows : 0;
+            int64_t b0 = s0 + row_off - kWinRows / 2;
+            b0 = b0 < 0 ? 0 : (b0 > hi ? hi : b0);
+            wb = (uint32_t)b0;
+            xr = __builtin_amdgcn_make_buffer_rsrc(const_cast<double *>(Wg + b0 * 16), (short)0, (int)(kWinRows * 128),
+                                                   0x00020000);
+        }
         long spin = 0;
         PP_T(ta);
         while (__hip_atomic_load(&ready[s], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP) != (int)i &&
@@ -1013,7 +743,7 @@ __global__ __launch_bounds__(64 * (NC + NL)) void k_fused_pp16(
 #pragma unroll
                 for (int tt = 0; tt < 8; ++tt) {
                     const uint32_t off =
-                        f + tt < cnt ? __umul24((unsigned)c[tt], 128u) + lane_off : 0x80000000u;
+                        f + tt < cnt ? __umul24((unsigned)c[tt] - wb, 128u) + lane_off : 0x80000000u;
                     const auto u4 = __builtin_amdgcn_raw_buffer_load_b128(xr, off, 0, 0);
                     __builtin_memcpy(&xs[tt], &u4, 16);
                 }
@@ -1049,7 +779,7 @@ __global__ __launch_bounds__(64 * (NC + NL)) void k_fused_pp16(
 #endif
         } else {  // long run (rare): epilogue first, then gather from global
             if (s0p >= 0) epilogue();
-            ws_gather(col + kA, val + kA, o0, len0, o1, cnt, xr, lane_off, y);
+            ws_gather(col + kA, val + kA, o0, len0, o1, cnt, xr, lane_off, y, wb);
         }
         // the CSR stage is no longer read by this wave
         asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
@@ -1084,583 +814,6 @@ __global__ __launch_bounds__(64 * (NC + NL)) void k_fused_pp16(
     for (int r = 0; r < 4; ++r) slab[((lane >> 4) + 4 * r) * 16 + (lane & 15)] = macc[r];
 }
 
-// ---------------------------------------------------------------------------
-// Per-wave software-pipelined persistent pass 1.  Every wave is independent
-// (no loader, no block barrier after the first): it walks its own strips of 16
-// rows (XCD-contiguous strip ranges, adjacent strips on adjacent waves) and
-// keeps ONE strip of HBM streams in flight in registers -- the next strip's CSR
-// run (16-B loads), its W rows and its Q_{j-1} rows, and the row pointers of
-// the strip after that.  vmcnt retires in order, so the prefetch is issued
-// right AFTER the first gather step of the current strip: that step's wait
-// (usually the only long one -- a 16-row strip of a 10-nnz/row operator is 160
-// entries, 20 per lane group, 3 steps) does not cover the HBM latency, and the
-// prefetched registers have the rest of the strip to land.  At the top of the
-// next strip the registers are committed to the wave's LDS: the run (gather
-// indices), and W/Q rows in XOR-swizzled 16x16 layout for the MFMA epilogue.
-// The prefetch is straight-line code (out-of-range buffer offsets instead of
-// branches): the waitcnt pass merges control-flow paths conservatively, and a
-// path without the prefetch would make every later wait cover it.  Runs longer
-// than kPfCap - 3 entries gather straight from global memory.
-constexpr int kPfCap = 256;
-struct PfWave {
-    int32_t col[kPfCap + 16];  // + slack: slots past the run end read stale entries
-    double val[kPfCap + 16];
-    double wq[2][256];  // W rows, Q_{j-1} rows (then the Y transpose scratch)
-};
-
-struct PfRegs {
-    uint4 c;        // 4 column indices from ca + 4 lane
-    double2 v[2];   // values from va + 2 lane, va + 128 + 2 lane
-    double2 wr[2];  // W row s0 + (lane >> 2), doubles 4 (lane & 3) .. + 3
-    double2 qr[2];  // Q_{j-1}, same layout
-};
-
-__device__ __forceinline__ uint4 pf_ld16(__amdgpu_buffer_rsrc_t r, uint32_t off)
-{
-    const auto u = __builtin_amdgcn_raw_buffer_load_b128(r, off, 0, 0);
-    uint4 o;
-    __builtin_memcpy(&o, &u, 16);
-    return o;
-}
-__device__ __forceinline__ double2 pf_ld16d(__amdgpu_buffer_rsrc_t r, uint32_t off)
-{
-    const auto u = __builtin_amdgcn_raw_buffer_load_b128(r, off, 0, 0);
-    double2 o;
-    __builtin_memcpy(&o, &u, 16);
-    return o;
-}
-
-// lane l <= 16 loads rp[s0 + l] (rows past n are fixed up by pf_rp_fix)
-__device__ __forceinline__ int64_t pf_rp_load(const int64_t *__restrict__ rp, int64_t s0, int64_t n,
-                                              bool live, int lane)
-{
-    const int64_t avail = n + 1 - s0;
-    const int bytes = live ? (int)((avail < 17 ? avail : 17) * 8) : 0;
-    const auto r = __builtin_amdgcn_make_buffer_rsrc(const_cast<int64_t *>(rp + s0), (short)0, bytes, 0x00020000);
-    const auto u = __builtin_amdgcn_raw_buffer_load_b64(r, lane <= 16 ? 8u * lane : 0x80000000u, 0, 0);
-    int64_t v;
-    __builtin_memcpy(&v, &u, 8);
-    return v;
-}
-__device__ __forceinline__ int64_t pf_rp_fix(int64_t v, int64_t s0, int64_t n, int64_t nnz, int lane)
-{
-    return s0 + lane <= n ? v : nnz;
-}
-
-// a wave-uniform int64 from lane `l`
-__device__ __forceinline__ int64_t pf_lane(int64_t v, int l)
-{
-    const int lo = __builtin_amdgcn_readlane((int)(uint64_t)v, l);
-    const int hi = __builtin_amdgcn_readlane((int)((uint64_t)v >> 32), l);
-    return (int64_t)(((uint64_t)(uint32_t)hi << 32) | (uint32_t)lo);
-}
-
-__device__ __forceinline__ int64_t pf_shfl(int64_t v, int src)
-{
-    const int lo = __builtin_amdgcn_ds_bpermute(src << 2, (int)(uint64_t)v);
-    const int hi = __builtin_amdgcn_ds_bpermute(src << 2, (int)((uint64_t)v >> 32));
-    return (int64_t)(((uint64_t)(uint32_t)hi << 32) | (uint32_t)lo);
-}
-
-template <int UNR>
-__global__ __launch_bounds__(512, 4) void k_fused_pf16(
-    int64_t n, const int64_t *__restrict__ rp, const int32_t *__restrict__ col,
-    const double *__restrict__ val, const double *__restrict__ Wg, int64_t nx,
-    const double *__restrict__ Wown, const double *Qbuf, double *Wn,
-    const double *__restrict__ binv, const double *__restrict__ beta, int64_t lc,
-    double *__restrict__ qrow, double *__restrict__ part, int dbg)
-{
-    // dbg (diagnostic timing only, results invalid): bit 0 masks the X gathers,
-    // bit 1 masks the HBM streams (run, W, Q), bit 2 drops the stores
-    __shared__ PfWave wl[8];
-    __shared__ double ops[2][256];  // beta^-1, -beta in MFMA B-operand order
-    const int lane_ = threadIdx.x & 63, w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-    const bool has_prev = beta != nullptr;
-    for (int e = threadIdx.x; e < 256; e += 512) {
-        const int kc = e >> 6, l = e & 63;
-        const int idx = (4 * kc + (l >> 4)) * 16 + (l & 15);
-        ops[0][e] = binv[idx];
-        ops[1][e] = has_prev ? -beta[idx] : 0.0;
-    }
-    __syncthreads();  // the only block barrier
-    PfWave &L = wl[w];
-    // strips of XCD x: [S x / 8, S (x + 1) / 8); wave kk of the XCD takes
-    // begin + kk, begin + kk + KK, ...
-    const int64_t S = ceil_div(n, (int64_t)16);
-    int64_t begin, end, kk, KK;
-    {
-        const int64_t G = gridDim.x, b = blockIdx.x;
-        if (G < 8) {
-            begin = 0; end = S; kk = b * 8 + w; KK = G * 8;
-        } else {
-            const int64_t x = b & 7;
-            begin = S * x / 8;
-            end = S * (x + 1) / 8;
-            kk = (b >> 3) * 8 + w;
-            KK = ((G - x + 7) >> 3) * 8;
-        }
-    }
-    const int64_t nt = (end - begin - kk + KK - 1) / KK > 0 ? (end - begin - kk + KK - 1) / KK : 0;
-    // strip i's first row (clamped so a dead prefetch still forms a valid base)
-    auto strip0 = [&](int64_t i) {
-        const int64_t s = begin + kk + i * KK;
-        return (s < S ? s : S - 1) * 16;
-    };
-    const int64_t nnz = rp[n];
-    const __amdgpu_buffer_rsrc_t xr =
-        __builtin_amdgcn_make_buffer_rsrc(const_cast<double *>(Wg), (short)0, (int)(nx * 128), 0x00020000);
-
-    // issue the HBM streams of the strip at s0 (row pointers R, fixed up); all
-    // loads are issued, dead ones with out-of-range offsets
-    auto issue = [&](int64_t s0, int64_t R, bool live, PfRegs &P, int lane) {
-        const int64_t kA = pf_lane(R, 0), kB = pf_lane(R, 16);
-        const int64_t ca = kA & ~(int64_t)3, va = kA & ~(int64_t)1;
-        const int cend = (int)(kA - ca + (kB - kA)), vend = (int)(kA - va + (kB - kA));
-        const bool stage = live && cend <= kPfCap && !(dbg & 2);
-        const int64_t cb = (nnz - ca) * 4, vb = (nnz - va) * 8;
-        const auto cr = __builtin_amdgcn_make_buffer_rsrc(const_cast<int32_t *>(col + ca), (short)0,
-                                                          stage ? (int)(cb < 0x7fffffff ? cb : 0x7fffffff) : 0,
-                                                          0x00020000);
-        const auto vr = __builtin_amdgcn_make_buffer_rsrc(const_cast<double *>(val + va), (short)0,
-                                                          stage ? (int)(vb < 0x7fffffff ? vb : 0x7fffffff) : 0,
-                                                          0x00020000);
-        P.c = pf_ld16(cr, 4 * lane < cend ? 16u * lane : 0x80000000u);
-        P.v[0] = pf_ld16d(vr, 2 * lane < vend ? 16u * lane : 0x80000000u);
-        P.v[1] = pf_ld16d(vr, 128 + 2 * lane < vend ? 16u * (64 + lane) : 0x80000000u);
-        const int64_t rows = n - s0 < 16 ? n - s0 : 16;
-        const int wb = live && !(dbg & 2) ? (int)(rows * 128) : 0;
-        const auto wr = __builtin_amdgcn_make_buffer_rsrc(const_cast<double *>(Wown + s0 * 16), (short)0, wb,
-                                                          0x00020000);
-        const auto qr = __builtin_amdgcn_make_buffer_rsrc(const_cast<double *>(Qbuf) + s0 * 16, (short)0, has_prev ? wb : 0, 0x00020000);
-        const uint32_t o = (uint32_t)(lane * 32);  // row lane >> 2, doubles 4 (lane & 3) .. + 3
-        P.wr[0] = pf_ld16d(wr, o);
-        P.wr[1] = pf_ld16d(wr, o + 16);
-        P.qr[0] = pf_ld16d(qr, o);
-        P.qr[1] = pf_ld16d(qr, o + 16);
-    };
-
-    PfRegs P;
-    int64_t R0 = 0, R1 = 0;
-    if (nt > 0) {
-        R0 = pf_rp_fix(pf_rp_load(rp, strip0(0), n, true, lane_), strip0(0), n, nnz, lane_);
-        R1 = pf_rp_load(rp, strip0(1), n, nt > 1, lane_);
-        issue(strip0(0), R0, true, P, lane_);
-    }
-    d4_t macc = {0.0, 0.0, 0.0, 0.0};
-    for (int64_t i = 0; i < nt; ++i) {
-        // lane-derived LDS addresses are recomputed per strip (a few VALU ops)
-        // rather than hoisted out of the loop and spilled
-        int lane = lane_;
-        asm volatile("" : "+v"(lane));
-        const int q = lane >> 2, ar = lane & 15;  // group q gathers row s0 + q
-        const uint32_t lane_off = 32u * (lane & 3);
-        const int64_t s0 = strip0(i);
-        const int64_t kA = pf_lane(R0, 0), kB = pf_lane(R0, 16);
-        const int co = (int)(kA & 3), vo = (int)(kA & 1);
-        const bool fast = co + (int)(kB - kA) <= kPfCap;
-        // ---- commit the prefetched registers to the wave's LDS
-        *reinterpret_cast<uint4 *>(&L.col[4 * lane]) = P.c;
-        *reinterpret_cast<double2 *>(&L.val[2 * lane]) = P.v[0];
-        *reinterpret_cast<double2 *>(&L.val[128 + 2 * lane]) = P.v[1];
-        {
-            const int r = lane >> 2, c = 4 * (lane & 3);
-            L.wq[0][fw_sw(r, c + 0)] = P.wr[0].x;
-            L.wq[0][fw_sw(r, c + 1)] = P.wr[0].y;
-            L.wq[0][fw_sw(r, c + 2)] = P.wr[1].x;
-            L.wq[0][fw_sw(r, c + 3)] = P.wr[1].y;
-            L.wq[1][fw_sw(r, c + 0)] = P.qr[0].x;
-            L.wq[1][fw_sw(r, c + 1)] = P.qr[0].y;
-            L.wq[1][fw_sw(r, c + 2)] = P.qr[1].x;
-            L.wq[1][fw_sw(r, c + 3)] = P.qr[1].y;
-        }
-        // this group's row: entries [o, o + len) of the run; steps: the longest row
-        const int o = (int)(pf_shfl(R0, q) - kA);
-        const int len = (int)(pf_shfl(R0, q + 1) - kA) - o;
-        int mx = len;
-#pragma unroll
-        for (int d = 4; d < 64; d <<= 1) mx = max(mx, __shfl_xor(mx, d));
-        const int maxlen = __builtin_amdgcn_readfirstlane(mx);
-        wave_lds_sync();
-        const int32_t *cp = L.col + co + o;
-        const double *vp = L.val + vo + o;
-        double y[4] = {0.0, 0.0, 0.0, 0.0};
-        // UNR slots of this group's row from entry f: 2 x 16-B loads per lane
-        auto gather_issue = [&](int f, double2 (*xs)[2]) {
-            int32_t c[UNR];
-#pragma unroll
-            for (int tt = 0; tt < UNR; ++tt) c[tt] = cp[f + tt];
-            if (dbg & 2) {  // streams masked: synthetic in-band columns
-#pragma unroll
-                for (int tt = 0; tt < UNR; ++tt) {
-                    const int64_t cc = s0 + ((q * 8 + f + tt) * 131) % 8192 - 4096;
-                    c[tt] = (int)(cc < 0 ? 0 : cc >= nx ? nx - 1 : cc);
-                }
-            }
-#pragma unroll
-            for (int tt = 0; tt < UNR; ++tt) {
-                // slots past the row end load a live entry of a later row (or,
-                // past the run, any row: buffer-clamped) and are skipped below
-                const uint32_t off = (dbg & 1) ? 0x80000000u : __umul24((unsigned)c[tt], 128u) + lane_off;
-                const auto u0 = __builtin_amdgcn_raw_buffer_load_b128(xr, off, 0, 0);
-                const auto u1 = __builtin_amdgcn_raw_buffer_load_b128(xr, off + 16, 0, 0);
-                __builtin_memcpy(&xs[tt][0], &u0, 16);
-                __builtin_memcpy(&xs[tt][1], &u1, 16);
-            }
-        };
-        auto fma_step = [&](int f, double2 (*xs)[2]) {
-#pragma unroll
-            for (int tt = 0; tt < UNR; ++tt) {
-                const double v = vp[f + tt];
-                if (f + tt < len) {
-                    y[0] = fma(v, xs[tt][0].x, y[0]);
-                    y[1] = fma(v, xs[tt][0].y, y[1]);
-                    y[2] = fma(v, xs[tt][1].x, y[2]);
-                    y[3] = fma(v, xs[tt][1].y, y[3]);
-                }
-            }
-        };
-        // ---- gather step 0 (every lane)
-        double2 xs[UNR][2];
-        gather_issue(0, xs);
-        // ---- prefetch strip i + 1 and the row pointers of strip i + 2
-        asm volatile("" ::: "memory");
-        const int64_t s1 = strip0(i + 1);
-        issue(s1, pf_rp_fix(R1, s1, n, nnz, lane), i + 1 < nt, P, lane);
-        const int64_t R2 = pf_rp_load(rp, strip0(i + 2), n, i + 2 < nt, lane);
-        asm volatile("" ::: "memory");
-        if (fast) {
-            fma_step(0, xs);
-            for (int f = UNR; f < maxlen; f += UNR) {  // wave-uniform
-                gather_issue(f, xs);
-                fma_step(f, xs);
-            }
-        } else {  // long run (rare): gather from global
-            const int64_t ko = kA + o;
-            for (int f = 0; f < maxlen; ++f) {
-                const bool on = f < len;
-                const int32_t c = on ? col[ko + f] : 0;
-                const double v = on ? val[ko + f] : 0.0;
-                const uint32_t off = on ? __umul24((unsigned)c, 128u) + lane_off : 0x80000000u;
-                const auto u0 = __builtin_amdgcn_raw_buffer_load_b128(xr, off, 0, 0);
-                const auto u1 = __builtin_amdgcn_raw_buffer_load_b128(xr, off + 16, 0, 0);
-                double2 x0, x1;
-                __builtin_memcpy(&x0, &u0, 16);
-                __builtin_memcpy(&x1, &u1, 16);
-                y[0] = fma(v, x0.x, y[0]);
-                y[1] = fma(v, x0.y, y[1]);
-                y[2] = fma(v, x1.x, y[2]);
-                y[3] = fma(v, x1.y, y[3]);
-            }
-        }
-        // ---- epilogue: operands from LDS, products on the matrix cores
-        double ya[4], wa[4], qa[4];
-#pragma unroll
-        for (int kc = 0; kc < 4; ++kc) {
-            wa[kc] = L.wq[0][fw_sw(ar, 4 * kc + (lane >> 4))];
-            qa[kc] = L.wq[1][fw_sw(ar, 4 * kc + (lane >> 4))];
-        }
-        wave_lds_sync();
-        {
-            const int r = lane >> 2, c = 4 * (lane & 3);
-#pragma unroll
-            for (int e = 0; e < 4; ++e) L.wq[0][fw_sw(r, c + e)] = y[e];
-        }
-        wave_lds_sync();
-#pragma unroll
-        for (int kc = 0; kc < 4; ++kc) ya[kc] = L.wq[0][fw_sw(ar, 4 * kc + (lane >> 4))];
-        d4_t q1 = {0.0, 0.0, 0.0, 0.0}, wn = {0.0, 0.0, 0.0, 0.0};
-#pragma unroll
-        for (int kc = 0; kc < 4; ++kc) q1 = mfma16(wa[kc], ops[0][64 * kc + lane], q1);
-#pragma unroll
-        for (int kc = 0; kc < 4; ++kc) wn = mfma16(ya[kc], ops[0][64 * kc + lane], wn);
-#pragma unroll
-        for (int kc = 0; kc < 4; ++kc) wn = mfma16(qa[kc], ops[1][64 * kc + lane], wn);  // 0 if !has_prev
-#pragma unroll
-        for (int r = 0; r < 4; ++r) {
-            const int64_t row = s0 + (lane >> 4) + 4 * r;
-            if (row < n && !(dbg & 4)) {
-                Wn[s0 * 16 + 64 * r + lane] = wn[r];
-                if (row == lc) qrow[lane & 15] = q1[r];
-            }
-        }
-#pragma unroll
-        for (int r = 0; r < 4; ++r) macc = mfma16(q1[r], wn[r], macc);
-        R0 = pf_rp_fix(R1, s1, n, nnz, lane);
-        R1 = R2;
-    }
-    double *slab = part + ((int64_t)blockIdx.x * 8 + w) * 256;
-#pragma unroll
-    for (int r = 0; r < 4; ++r) slab[((lane_ >> 4) + 4 * r) * 16 + (lane_ & 15)] = macc[r];
-}
-
-// ---------------------------------------------------------------------------
-// nnz-split fused pass 1: the k_spmm_seg structure (lz_spmm.hip) with the
-// fused epilogue.  PMC (r01): the texture path is busy ~97 % of a gather
-// kernel and every load or store wave-instruction costs it about the same
-// whatever its live lanes, so this pass is built to issue as few as possible:
-//   * 48-row tiles; each of the 32 lane groups gathers an equal 8-aligned slice
-//     of the tile's nonzero run (rows split across slices are summed in fixed
-//     order from LDS head slots), so gather instructions run ~94 % lanes live;
-//   * the CSR run arrives by 16-B nt loads, issued together with the tile's
-//     W and Q_{j-1} strips (one HBM round trip for all three);
-//   * A*W rows land in an LDS tile; waves 0-2 each run one 16-row strip's MFMA
-//     epilogue (Q_j = W beta^-1, W' = Y beta^-1 - Q_{j-1} beta) and write Q_j
-//     and W' back with 16-B stores through their LDS scratch;
-//   * persistent blocks over XCD-contiguous tile ranges (XcdSched) keep the
-//     Q_j^T W' accumulator in registers; one slab per block.
-constexpr int kSegTR = 48, kSegCap = 768;
-
-__device__ __forceinline__ __amdgpu_buffer_rsrc_t seg_rsrc(const void *p, uint32_t bytes)
-{
-    return __builtin_amdgcn_make_buffer_rsrc(const_cast<void *>(p), (short)0, (int)bytes, 0x00020000);
-}
-
-__global__ __launch_bounds__(256, 4) void k_fused_seg16(
-    int64_t n, const int64_t *__restrict__ rp, const int32_t *__restrict__ col,
-    const double *__restrict__ val, const double *__restrict__ Wg, int64_t nx,
-    const double *__restrict__ Wown, const double *Qbuf,
-    double *Wn, const double *__restrict__ binv, const double *__restrict__ beta,
-    int64_t lc, double *__restrict__ qrow, double *__restrict__ part)
-{
-    constexpr int TR = kSegTR, CAP = kSegCap, G = 32, UNR = 8, YS = 17;
-    constexpr int SPTC = ((CAP + 4) / 4 + 255) / 256, SPTV = ((CAP + 2) / 2 + 255) / 256;
-    __shared__ int32_t rel[TR + 1];
-    __shared__ double sbuf[(CAP + UNR) * 3 / 2 + 2];  // vs | cs during the gather; scratch after
-    __shared__ uint8_t rid[CAP + UNR];
-    __shared__ double yt[TR * YS];                    // the tile's A*W rows (stride 17)
-    __shared__ double2 head[G][8];
-    __shared__ double bsh[2][256];                    // beta^-1, -beta (epilogue operands)
-    double *vs = sbuf;
-    int32_t *cs = reinterpret_cast<int32_t *>(sbuf + CAP + UNR);
-    const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
-    const int gi = tid >> 3, p = tid & 7;
-    const bool has_prev = beta != nullptr;
-    bsh[0][tid] = binv[tid];
-    bsh[1][tid] = has_prev ? -beta[tid] : 0.0;
-    const __amdgpu_buffer_rsrc_t xr = seg_rsrc(Wg, (uint32_t)(nx * 128));
-    const uint32_t lane_off = 16u * (uint32_t)p;
-    const int64_t nnz = rp[n];
-    d4_t macc = {0.0, 0.0, 0.0, 0.0};
-    const int64_t ntile = ceil_div(n, (int64_t)TR);
-    XcdSched s(ntile);
-    for (int64_t u = s.begin; u < s.end; u += s.step) {
-        const int64_t r0 = u * TR;
-        const int nrows = (int)((n - r0) < TR ? (n - r0) : TR);
-        const int64_t kA = rp[r0];
-        __syncthreads();  // the previous tile's epilogue is done with sbuf / yt
-        if (tid <= nrows) rel[tid] = (int)(rp[r0 + tid] - kA);
-        const int64_t kB = rp[r0 + nrows];
-        const int N = (int)(kB - kA);
-        // this wave's epilogue strip (waves 0-2): W and Q_{j-1} rows, issued with the CSR run
-        const int64_t rs = r0 + 16 * w;
-        double wv[4] = {0.0, 0.0, 0.0, 0.0}, qv[4] = {0.0, 0.0, 0.0, 0.0};
-        if (w < 3 && 16 * w < nrows) {
-            tile_load(Wown, rs, n, lane, wv);
-            if (has_prev) tile_load(Qbuf, rs, n, lane, qv);
-        }
-        if (N <= CAP) {  // block-uniform
-            const int64_t bc = kA & ~(int64_t)3, bv = kA & ~(int64_t)1;
-            const __amdgpu_buffer_rsrc_t cr = seg_rsrc(col + bc, 0x7fffffffu);
-            const __amdgpu_buffer_rsrc_t vr = seg_rsrc(val + bv, 0x7fffffffu);
-            int4 ct[SPTC], vt[SPTV];
-#pragma unroll
-            for (int q = 0; q < SPTC; ++q) {
-                const int64_t k = bc + 4 * (int64_t)(tid + 256 * q);
-                ct[q] = int4{0, 0, 0, 0};
-                if (k + 4 <= nnz && k < kB)
-                    ct[q] = __builtin_bit_cast(int4, __builtin_amdgcn_raw_buffer_load_b128(cr, (uint32_t)((k - bc) * 4), 0, 2));
-                else if (k < kB) {
-                    ct[q].x = col[k];
-                    if (k + 1 < nnz) ct[q].y = col[k + 1];
-                    if (k + 2 < nnz) ct[q].z = col[k + 2];
-                }
-            }
-#pragma unroll
-            for (int q = 0; q < SPTV; ++q) {
-                const int64_t k = bv + 2 * (int64_t)(tid + 256 * q);
-                vt[q] = int4{0, 0, 0, 0};
-                if (k + 2 <= nnz && k < kB)
-                    vt[q] = __builtin_bit_cast(int4, __builtin_amdgcn_raw_buffer_load_b128(vr, (uint32_t)((k - bv) * 8), 0, 2));
-                else if (k < kB) {
-                    const double t0 = val[k];
-                    __builtin_memcpy(&vt[q], &t0, 8);
-                }
-            }
-            __syncthreads();  // rel
-            if (tid < nrows)
-                for (int k = rel[tid]; k < rel[tid + 1]; ++k) rid[k] = (uint8_t)tid;
-#pragma unroll
-            for (int q = 0; q < SPTC; ++q) {
-                const int64_t k = bc + 4 * (int64_t)(tid + 256 * q);
-                const int32_t cv[4] = {ct[q].x, ct[q].y, ct[q].z, ct[q].w};
-#pragma unroll
-                for (int e = 0; e < 4; ++e)
-                    if (k + e >= kA && k + e < kB) cs[k + e - kA] = cv[e];
-            }
-#pragma unroll
-            for (int q = 0; q < SPTV; ++q) {
-                const int64_t k = bv + 2 * (int64_t)(tid + 256 * q);
-                double tv[2];
-                __builtin_memcpy(tv, &vt[q], 16);
-#pragma unroll
-                for (int e = 0; e < 2; ++e)
-                    if (k + e >= kA && k + e < kB) vs[k + e - kA] = tv[e];
-            }
-            if (tid < UNR) {
-                cs[N + tid] = 0;
-                vs[N + tid] = 0.0;
-                rid[N + tid] = 255;
-            }
-            __syncthreads();
-            const int E = ((N + G - 1) / G + UNR - 1) / UNR * UNR;
-            const int start = gi * E, end = (start + E < N) ? start + E : N;
-            if (start < end) {  // group-uniform
-                int cur = rid[start];
-                bool open = rel[cur] < start;
-                double a0 = 0.0, a1 = 0.0;
-                for (int s0 = start; s0 < end; s0 += UNR) {
-                    int32_t cc[UNR];
-                    double vv[UNR];
-                    int rr[UNR];
-#pragma unroll
-                    for (int t = 0; t < UNR; ++t) {
-                        cc[t] = cs[s0 + t];
-                        vv[t] = vs[s0 + t];
-                        rr[t] = rid[s0 + t];
-                    }
-                    double2 xs[UNR];
-#pragma unroll
-                    for (int t = 0; t < UNR; ++t) {
-                        const uint32_t off = s0 + t < end ? __umul24((unsigned)cc[t], 128u) + lane_off : 0x80000000u;
-                        const auto u4 = __builtin_amdgcn_raw_buffer_load_b128(xr, off, 0, 0);
-                        __builtin_memcpy(&xs[t], &u4, 16);
-                    }
-#pragma unroll
-                    for (int t = 0; t < UNR; ++t) {
-                        const int r = s0 + t < end ? rr[t] : cur;
-                        if (r != cur) {  // row cur ends inside the slice
-                            if (open) head[gi][p] = double2{a0, a1};
-                            else {
-                                yt[cur * YS + 2 * p] = a0;
-                                yt[cur * YS + 2 * p + 1] = a1;
-                            }
-                            a0 = a1 = 0.0;
-                            cur = r;
-                            open = false;
-                        }
-                        a0 = fma(vv[t], xs[t].x, a0);
-                        a1 = fma(vv[t], xs[t].y, a1);
-                    }
-                }
-                if (open) head[gi][p] = double2{a0, a1};
-                else {
-                    yt[cur * YS + 2 * p] = a0;
-                    yt[cur * YS + 2 * p + 1] = a1;
-                }
-            }
-            __syncthreads();
-            for (int r = gi; r < nrows; r += G) {  // rows over several slices; empty rows
-                const int a = rel[r], e = rel[r + 1];
-                if (a == e) {
-                    yt[r * YS + 2 * p] = 0.0;
-                    yt[r * YS + 2 * p + 1] = 0.0;
-                    continue;
-                }
-                const int g1 = a / E, g2 = (e - 1) / E;
-                if (g1 == g2) continue;
-                double s0 = yt[r * YS + 2 * p], s1 = yt[r * YS + 2 * p + 1];
-                for (int g = g1 + 1; g <= g2; ++g) {
-                    s0 += head[g][p].x;
-                    s1 += head[g][p].y;
-                }
-                yt[r * YS + 2 * p] = s0;
-                yt[r * YS + 2 * p + 1] = s1;
-            }
-        } else {  // a run longer than the stage: rows straight from global
-            for (int r = gi; r < nrows; r += G) {
-                const int64_t a = rp[r0 + r], e = rp[r0 + r + 1];
-                double a0 = 0.0, a1 = 0.0;
-                for (int64_t k = a; k < e; k += UNR) {
-                    double2 xs[UNR];
-                    double vv[UNR];
-#pragma unroll
-                    for (int t = 0; t < UNR; ++t) {
-                        const bool ok = k + t < e;
-                        vv[t] = ok ? val[k + t] : 0.0;
-                        const uint32_t off = ok ? __umul24((unsigned)col[k + t], 128u) + lane_off : 0x80000000u;
-                        const auto u4 = __builtin_amdgcn_raw_buffer_load_b128(xr, off, 0, 0);
-                        __builtin_memcpy(&xs[t], &u4, 16);
-                    }
-#pragma unroll
-                    for (int t = 0; t < UNR; ++t) {
-                        a0 = fma(vv[t], xs[t].x, a0);
-                        a1 = fma(vv[t], xs[t].y, a1);
-                    }
-                }
-                yt[r * YS + 2 * p] = a0;
-                yt[r * YS + 2 * p + 1] = a1;
-            }
-        }
-        __syncthreads();  // yt complete; sbuf free for the epilogue scratch
-        if (w < 3 && 16 * w < nrows) {  // wave-uniform
-            double *T = sbuf + w * (16 * 17);
-            const bool live = 16 * w + (lane & 15) < nrows;  // this lane's A-operand row
-            double ya[4], wa[4], qa[4] = {0.0, 0.0, 0.0, 0.0};
-#pragma unroll
-            for (int kc = 0; kc < 4; ++kc)
-                ya[kc] = live ? yt[(16 * w + (lane & 15)) * YS + 4 * kc + (lane >> 4)] : 0.0;
-            tile_regs_to_aop(T, wv, lane, wa);
-            if (has_prev) tile_regs_to_aop(T, qv, lane, qa);
-            double bi_op[4];
-#pragma unroll
-            for (int kc = 0; kc < 4; ++kc) bi_op[kc] = bsh[0][(4 * kc + (lane >> 4)) * 16 + (lane & 15)];
-            d4_t q1 = {0.0, 0.0, 0.0, 0.0}, wn = {0.0, 0.0, 0.0, 0.0};
-#pragma unroll
-            for (int kc = 0; kc < 4; ++kc) q1 = mfma16(wa[kc], bi_op[kc], q1);
-#pragma unroll
-            for (int kc = 0; kc < 4; ++kc) wn = mfma16(ya[kc], bi_op[kc], wn);
-            if (has_prev) {
-#pragma unroll
-                for (int kc = 0; kc < 4; ++kc)
-                    wn = mfma16(qa[kc], bsh[1][(4 * kc + (lane >> 4)) * 16 + (lane & 15)], wn);
-            }
-            // Q_j and W' leave as 16-B row pieces through the scratch
-            const int row = lane >> 3, c2 = 2 * (lane & 7);
-#pragma unroll
-            for (int m = 0; m < 2; ++m) {  // m = 0: Q_j (row probe only), m = 1: W'
-                const d4_t &v = m ? wn : q1;
-                double *dst = Wn;
-#pragma unroll
-                for (int r = 0; r < 4; ++r) T[((lane >> 4) + 4 * r) * 17 + (lane & 15)] = v[r];
-                wave_lds_sync();
-#pragma unroll
-                for (int hh = 0; hh < 2; ++hh) {
-                    const int rr = row + 8 * hh;
-                    const int64_t grow = rs + rr;
-                    const double x0 = T[rr * 17 + c2], x1 = T[rr * 17 + c2 + 1];
-                    if (16 * w + rr < nrows) {
-                        if (m == 1) *reinterpret_cast<double2 *>(dst + grow * 16 + c2) = double2{x0, x1};
-                        if (m == 0 && grow == lc) {
-                            qrow[c2] = x0;
-                            qrow[c2 + 1] = x1;
-                        }
-                    }
-                }
-                wave_lds_sync();
-            }
-            // rows past n have zero operands, so they add nothing here
-#pragma unroll
-            for (int r = 0; r < 4; ++r) macc = mfma16(q1[r], wn[r], macc);
-        }
-    }
-    // one slab per block: the waves' accumulators summed in wave order
-    __syncthreads();
-#pragma unroll
-    for (int r = 0; r < 4; ++r) sbuf[w * 256 + ((lane >> 4) + 4 * r) * 16 + (lane & 15)] = macc[r];
-    __syncthreads();
-    part[(int64_t)blockIdx.x * 256 + tid] = ((sbuf[tid] + sbuf[256 + tid]) + sbuf[512 + tid]) + sbuf[768 + tid];
-}
-
 // C = A * B, 16 x 16 row-major fp64 (the per-step P1 = beta_{j-1}^-1 beta_j and
 // P2 = beta_j^-1 alpha_j of the Q-free iteration, lz_api.hip)
 __global__ __launch_bounds__(256) void k_mm16(const double *__restrict__ A, const double *__restrict__ B,
@@ -1687,99 +840,81 @@ int mm16(lz_handle *h, const double *A, const double *B, double *C)
     return LZ_OK;
 }
 
-// Qbuf: W_{j-1} (own rows; may be the same buffer as Wn, row r is read before
-// it is written by the same wave), beta: P1 = beta_{j-1}^-1 beta_j (or null at j = 0)
+// Once per solve, when the gather source has 2^24 rows or more: does every
+// column of every 16-row strip fall inside the strip's kWinRows window
+// (k_fused_pp16<..., WIN>)?  One pass over col, one host read-back.
+__global__ __launch_bounds__(256) void k_window_check(int64_t n, const int64_t *__restrict__ rp,
+                                                      const int32_t *__restrict__ col, int64_t nx,
+                                                      int64_t row_off, int *__restrict__ bad)
+{
+    const int64_t hi = nx - kWinRows > 0 ? nx - kWinRows : 0;
+    int out = 0;
+    for (int64_t r = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; r < n; r += (int64_t)gridDim.x * blockDim.x) {
+        int64_t b0 = (r & ~(int64_t)15) + row_off - kWinRows / 2;
+        b0 = b0 < 0 ? 0 : (b0 > hi ? hi : b0);
+        for (int64_t k = rp[r], e = rp[r + 1]; k < e; ++k) {
+            const int64_t d = (int64_t)col[k] - b0;
+            out |= (d < 0) | (d >= kWinRows);
+        }
+    }
+    if (out) atomicOr(bad, 1);
+}
+
+int gather_window_ok(lz_handle *h, int64_t n, const int64_t *rp, const int32_t *col, int64_t nx, int64_t row_off,
+                     bool *ok)
+{
+    int *flag = h->err_flag + 8;  // err_flag[0] is the device error word
+    LZ_HIP_TRY(hipMemsetAsync(flag, 0, sizeof(int), h->stream));
+    const int grid = (int)std::max<int64_t>(1, std::min<int64_t>(ceil_div(n, (int64_t)256), (int64_t)h->n_cu * 8));
+    hipLaunchKernelGGL(k_window_check, dim3(grid), dim3(256), 0, h->stream, n, rp, col, nx, row_off, flag);
+    LZ_LAUNCH_CHECK();
+    int bad = 1;
+    LZ_HIP_TRY(hipMemcpyAsync(&bad, flag, sizeof(int), hipMemcpyDeviceToHost, h->stream));
+    LZ_HIP_TRY(hipStreamSynchronize(h->stream));
+    *ok = bad == 0;
+    return LZ_OK;
+}
+
+// Pass 1 (Q-free).  Qbuf: W_{j-1} (own rows; may be the same buffer as Wn, row
+// r is read before it is written by the same wave), beta: P1 =
+// beta_{j-1}^-1 beta_j (or null at j = 0).  k_fused_pp16 in one of two
+// shapes by mean row length: 14 consumers x 16 rows with a 2376-entry stage
+// (C3: 10 nnz/row) or 10 consumers with 4400 entries (C4: 25 nnz/row), both
+// one 1024 / 768-thread block per CU.  Gather sources past 2^24 rows use the
+// windowed instantiation when every strip's columns fit its window
+// (gather_window_ok), else the 64-bit tile kernel.
 int fused_spmm16(lz_handle *h, int64_t n, const int64_t *rp, const int32_t *col, const double *val,
                  const double *Wg, int64_t nx, const double *Wown, const double *Qbuf, double *Wn,
                  const double *binv, const double *beta, int64_t lc, double *qrow, int *nparts,
-                 const uint64_t *pairs)
+                 const uint64_t *pairs, int64_t nnz, int64_t row_off, int win)
 {
     const int64_t tiles = ceil_div(n, kFusedRows);
     LZ_ARG_CHECK(tiles >= 1 && tiles < (1LL << 31), "tile count");
-    const bool buf = nx * 128 < (1LL << 31) && nx < (1 << 24);
-    static const char *variant = getenv("LZ_FUSED_KERNEL");  // "tile": the tile-per-block kernel
-    if (buf && variant && variant[0] == 's') {  // nnz-split tiles (k_fused_seg16)
-        static int bpc = 0;
-        if (!bpc) {
-            LZ_HIP_TRY(hipOccupancyMaxActiveBlocksPerMultiprocessor(&bpc, k_fused_seg16, 256, 0));
-            bpc = std::max(bpc, 1);
-        }
-        const int64_t ntile = ceil_div(n, (int64_t)kSegTR);
-        const int grid = (int)std::max<int64_t>(1, std::min<int64_t>(ntile, (int64_t)h->n_cu * bpc));
-        LZ_TRY(ensure_partials(h, (size_t)grid * 256));
-        const int ev = prof_begin(h, PROF_SPMM_PASS);
-        hipLaunchKernelGGL(k_fused_seg16, dim3(grid), dim3(256), 0, h->stream, n, rp, col, val, Wg, nx, Wown,
-                           Qbuf, Wn, binv, beta, lc, qrow, h->partials);
-        prof_end(h, ev);
-        LZ_LAUNCH_CHECK();
-        return fold_slabs(h, h->partials, grid, 256, nparts);
-    }
-    if (buf && variant && variant[0] == 'p') {
-        const int grid = (int)std::max<int64_t>(1, std::min<int64_t>(ceil_div(ceil_div(n, (int64_t)16), 8),
-                                                                     2 * (int64_t)h->n_cu));
-        LZ_TRY(ensure_partials(h, (size_t)grid * 8 * 256));
-        const int ev = prof_begin(h, PROF_SPMM_PASS);
-        if (variant[1] == '8')
-            hipLaunchKernelGGL(k_fused_pf16<8>, dim3(grid), dim3(512), 0, h->stream, n, rp, col, val, Wg, nx,
-                               Wown, Qbuf, Wn, binv, beta, lc, qrow, h->partials, 0);
-        else
-            hipLaunchKernelGGL(k_fused_pf16<4>, dim3(grid), dim3(512), 0, h->stream, n, rp, col, val, Wg, nx,
-                               Wown, Qbuf, Wn, binv, beta, lc, qrow, h->partials, 0);
-        prof_end(h, ev);
-        LZ_LAUNCH_CHECK();
-        return fold_slabs(h, h->partials, (int64_t)grid * 8, 256, nparts);
-    }
-    // default: k_fused_pp16 (pipelined consumers, two parallel loaders): 1.65 ms
-    // against 1.73-1.76 for k_fused_ws16 (LZ_FUSED_KERNEL=ws) in the Q-free iteration
-    if (buf && (!variant || variant[0] == 'r')) {
-        constexpr int NCR = 14;
-        static_assert(NCR <= kPairPad, "row orders must cover the last tile's strips");
-        const int grid = (int)std::max<int64_t>(1, std::min<int64_t>(ceil_div(n, (int64_t)16 * NCR), h->n_cu));
-        LZ_TRY(ensure_partials(h, (size_t)grid * NCR * 256));
-        const int ev = prof_begin(h, PROF_SPMM_PASS);
-        if (pairs && !(variant && variant[1] == 'p'))  // LZ_FUSED_KERNEL=rp: rows (g, g+8)
-            hipLaunchKernelGGL((k_fused_pp16<NCR, 2376, 3, 2, true>), dim3(grid), dim3(64 * 16), 0, h->stream, n, rp,
-                               col, val, Wg, nx, Wown, Qbuf, Wn, binv, beta, lc, qrow, h->partials, h->err_flag,
-                               pairs);
-        else
-            hipLaunchKernelGGL((k_fused_pp16<NCR, 2376, 3, 2>), dim3(grid), dim3(64 * 16), 0, h->stream, n, rp, col,
-                               val, Wg, nx, Wown, Qbuf, Wn, binv, beta, lc, qrow, h->partials, h->err_flag,
-                               nullptr);
-        prof_end(h, ev);
-        LZ_LAUNCH_CHECK();
-        return fold_slabs(h, h->partials, (int64_t)grid * NCR, 256, nparts);
-    }
-    if (buf && !(variant && variant[0] == 't')) {
-        // LZ_FUSED_KERNEL=ws: one loader, CSR-only stages (3), W_{j-1} rows loaded by
-        // the consumers; =wsq: W_{j-1} strips in the stage (2 stages);
-        // =nl2: two loaders staging alternate tiles, 14 consumers
-        const bool wsq = variant && variant[0] == 'w' && variant[2] == 'q';
-        const bool nl2 = variant && variant[0] == 'n';
-        const int nc = nl2 ? 14 : 15;
+    LZ_ARG_CHECK(pairs != nullptr, "strip row orders (strip_pairs) missing");
+    const bool buf = nx < (1 << 24);  // 128-B rows: X < 2 GiB
+    if (buf || win) {
+        const bool wide = (double)nnz > 10.2 * (double)n;  // rows too long for the 2376-entry stage
+        const int nc = wide ? 10 : 14;
+        static_assert(14 <= kPairPad, "row orders must cover the last tile's strips");
         const int grid = (int)std::max<int64_t>(1, std::min<int64_t>(ceil_div(n, (int64_t)16 * nc), h->n_cu));
         LZ_TRY(ensure_partials(h, (size_t)grid * nc * 256));
         const int ev = prof_begin(h, PROF_SPMM_PASS);
-        if (wsq)
-            hipLaunchKernelGGL((k_fused_ws16<15, 2536, 2>), dim3(grid), dim3(64 * 16), 0, h->stream, n, rp, col,
-                               val, Wg, nx, Wown, Qbuf, Wn, binv, beta, lc, qrow, h->partials, h->err_flag);
-        else if (nl2)
-            hipLaunchKernelGGL((k_fused_ws16<14, 2376, 3, true, 2>), dim3(grid), dim3(64 * 16), 0, h->stream, n,
-                               rp, col, val, Wg, nx, Wown, Qbuf, Wn, binv, beta, lc, qrow, h->partials, h->err_flag);
-        else
-            hipLaunchKernelGGL((k_fused_ws16<15, 2536, 3, true>), dim3(grid), dim3(64 * 16), 0, h->stream, n, rp,
-                               col, val, Wg, nx, Wown, Qbuf, Wn, binv, beta, lc, qrow, h->partials, h->err_flag);
+        auto go = [&](auto kern) {
+            hipLaunchKernelGGL(kern, dim3(grid), dim3(64 * (nc + 2)), 0, h->stream, n, rp, col, val, Wg, nx, Wown,
+                               Qbuf, Wn, binv, beta, lc, qrow, h->partials, h->err_flag, pairs, row_off);
+        };
+        if (!wide && buf) go(k_fused_pp16<14, 2376, 3, 2, false>);
+        else if (!wide) go(k_fused_pp16<14, 2376, 3, 2, true>);
+        else if (buf) go(k_fused_pp16<10, 4400, 2, 2, false>);
+        else go(k_fused_pp16<10, 4400, 2, 2, true>);
         prof_end(h, ev);
         LZ_LAUNCH_CHECK();
         return fold_slabs(h, h->partials, (int64_t)grid * nc, 256, nparts);
     }
     LZ_TRY(ensure_partials(h, tiles * 256));
     const int ev = prof_begin(h, PROF_SPMM_PASS);
-    if (buf)
-        hipLaunchKernelGGL(k_fused_spmm16<true>, dim3((unsigned)tiles), dim3(512), 0, h->stream, n,
-                           rp, col, val, Wg, nx, Wown, Qbuf, Wn, binv, beta, lc, qrow, h->partials);
-    else
-        hipLaunchKernelGGL(k_fused_spmm16<false>, dim3((unsigned)tiles), dim3(512), 0, h->stream, n,
-                           rp, col, val, Wg, nx, Wown, Qbuf, Wn, binv, beta, lc, qrow, h->partials);
+    hipLaunchKernelGGL(k_fused_spmm16<false>, dim3((unsigned)tiles), dim3(512), 0, h->stream, n, rp, col, val, Wg, nx,
+                       Wown, Qbuf, Wn, binv, beta, lc, qrow, h->partials);
     prof_end(h, ev);
     LZ_LAUNCH_CHECK();
     // fold the per-tile slabs to <= 256 (fixed order) at h->partials2
@@ -1789,33 +924,15 @@ int fused_spmm16(lz_handle *h, int64_t n, const int64_t *rp, const int32_t *col,
 int fused_update16(lz_handle *h, int64_t n, double *Wn, const double *Q, const double *alpha,
                    int *nparts)
 {
-    // one block per CU (256 slabs for the sqrtm to reduce); LZ_UPDATE_BPC /
-    // LZ_UPDATE_NW (8 or 16 waves per block) for A/B.  Measured (C3): 1 block
-    // of 8 waves 0.723 ms, 2 blocks 0.740, 3 0.758, 4 0.738
-    static const char *gm = getenv("LZ_UPDATE_BPC");
-    static const char *nw_env = getenv("LZ_UPDATE_NW");
-    const int bpc = gm ? std::max(1, atoi(gm)) : 1;
-    const int nw = (nw_env && atoi(nw_env) == 16) ? 16 : 8;
-    const int64_t units = ceil_div(ceil_div(n, 16), nw);
-    const int grid = (int)std::max<int64_t>(1, std::min<int64_t>(units, (int64_t)h->n_cu * bpc));
+    // persistent, one block of 8 waves per CU (256 slabs for the sqrtm to
+    // reduce), rows walked last-first.  Measured (C3): 1 block of 8 waves
+    // 0.723 ms, 2 blocks 0.740, 3 0.758, 4 0.738; forward order 0.761 ms
+    const int64_t units = ceil_div(ceil_div(n, 16), 8);
+    const int grid = (int)std::max<int64_t>(1, std::min<int64_t>(units, (int64_t)h->n_cu));
     LZ_TRY(ensure_partials(h, (size_t)grid * 256));
-    static const char *order = getenv("LZ_UPDATE_ORDER");  // "f": forward (A/B)
-    const bool fwd = order && order[0] == 'f';
     const int ev = prof_begin(h, PROF_UPDATE_PASS);
-    if (nw == 16) {
-        if (fwd)
-            hipLaunchKernelGGL((k_fused_update16<false, 16>), dim3(grid), dim3(1024), 0, h->stream, n, Wn, Q, alpha,
-                               h->partials);
-        else
-            hipLaunchKernelGGL((k_fused_update16<true, 16>), dim3(grid), dim3(1024), 0, h->stream, n, Wn, Q, alpha,
-                               h->partials);
-    } else if (fwd) {
-        hipLaunchKernelGGL((k_fused_update16<false, 8>), dim3(grid), dim3(512), 0, h->stream, n, Wn, Q, alpha,
-                           h->partials);
-    } else {
-        hipLaunchKernelGGL((k_fused_update16<true, 8>), dim3(grid), dim3(512), 0, h->stream, n, Wn, Q, alpha,
-                           h->partials);
-    }
+    hipLaunchKernelGGL((k_fused_update16<true, 8>), dim3(grid), dim3(512), 0, h->stream, n, Wn, Q, alpha,
+                       h->partials);
     prof_end(h, ev);
     LZ_LAUNCH_CHECK();
     *nparts = grid;

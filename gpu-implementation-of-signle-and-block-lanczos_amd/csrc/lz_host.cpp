@@ -494,14 +494,20 @@ int64_t lzh_rand_lc(uint32_t seed)
 
 int lzh_uniform_B(int64_t n, int b, uint64_t seed, double *o64, float *o32)
 {
-    if (n <= 0 || b <= 0) return -1;
+    return lzh_uniform_B_rows(0, n, b, seed, o64, o32);
+}
+
+int lzh_uniform_B_rows(int64_t r0, int64_t n, int b, uint64_t seed, double *o64, float *o32)
+{
+    if (n <= 0 || b <= 0 || r0 < 0) return -1;
 #pragma omp parallel for schedule(static)
-    for (int64_t r = 0; r < n; ++r) {
+    for (int64_t i = 0; i < n; ++i) {
+        const int64_t r = r0 + i;
         RowRng g(seed ^ 0x5bd1e995ULL, (uint64_t)r);
         for (int c = 0; c < b; ++c) {
             const double v = 1.0 + g.unif();
-            if (o64) o64[r * b + c] = v;
-            if (o32) o32[r * b + c] = (float)v;
+            if (o64) o64[i * b + c] = v;
+            if (o32) o32[i * b + c] = (float)v;
         }
     }
     return 0;

@@ -6,10 +6,10 @@ namespace lz {
 
 // ---- sparse (lz_spmm.hip)
 template <typename T>
-int spmm_rm(lz_handle *h, int64_t n, const int64_t *rp, const int32_t *col, const T *val, int b,
+int spmm_rm(lz_handle *h, int64_t n, int64_t nnz, const int64_t *rp, const int32_t *col, const T *val, int b,
             const T *X, int64_t ldx, int64_t nx, T *Y, int64_t ldy);  // nx: rows of X
 template <typename T>
-int spmm_cm(lz_handle *h, int64_t n, const int64_t *rp, const int32_t *col, const T *val, int b,
+int spmm_cm(lz_handle *h, int64_t n, int64_t nnz, const int64_t *rp, const int32_t *col, const T *val, int b,
             const T *X, int64_t ldx, int64_t nx, T *Y, int64_t ldy);  // nx: rows of X
 template <typename T>
 int spmv(lz_handle *h, int64_t n, const int64_t *rp, const int32_t *col, const T *val, const T *x,
@@ -47,7 +47,11 @@ int copy_row(lz_handle *h, int b, const T *Q, int64_t ld, int col_major, int64_t
 int fused_spmm16(lz_handle *h, int64_t n, const int64_t *rp, const int32_t *col,
                  const double *val, const double *Wg, int64_t nx, const double *Wown, const double *Wprev,
                  double *Wn, const double *binv, const double *P1, int64_t lc, double *qrow, int *nparts,
-                 const uint64_t *pairs = nullptr);
+                 const uint64_t *pairs, int64_t nnz, int64_t row_off, int win);
+// gather source of 2^24+ rows: does every strip's column set fit its window?
+// (row_off: X row of local row 0; synchronises the stream once)
+int gather_window_ok(lz_handle *h, int64_t n, const int64_t *rp, const int32_t *col, int64_t nx, int64_t row_off,
+                     bool *ok);
 // per-16-row-strip row order by length for fused_spmm16's `pairs` (once per solve)
 int strip_pairs(lz_handle *h, int64_t n, const int64_t *rp, const uint64_t **out);
 // Pass 2: Wn <- Wn - Wcur*P2 (P2 = beta_j^-1 alpha_j, so Wcur*P2 = Q_j alpha_j);

@@ -126,6 +126,12 @@ __device__ long long *lz_ws_tl;
 #endif
 constexpr long kWsSpin = 1L << 24;
 
+// Gather window of the 32-bit buffer-addressed kernels when the gather source
+// has 2^24 rows of 128 B or more (X past 2 GiB): a strip / tile reads X
+// through a buffer resource based kWinRows / 2 rows before its own row, and a
+// once-per-operator check (gather_window_ok) proved its columns fall inside.
+constexpr int64_t kWinRows = (1 << 24) - 1;
+
 typedef __attribute__((address_space(3))) void ws_lds_t;
 
 // LDS word access from the loader wave in inline asm: after an LDS-DMA the
@@ -162,7 +168,8 @@ __device__ __forceinline__ void ws_dma(__amdgpu_buffer_rsrc_t r, void *lds_base,
 // step; masked slots read entry o0 and load nothing (out-of-range offset).
 template <typename CP, typename VP>
 __device__ __forceinline__ void ws_gather(CP cp, VP vp, int o0, int len0, int o1, int cnt,
-                                          __amdgpu_buffer_rsrc_t xr, uint32_t lane_off, double y[4])
+                                          __amdgpu_buffer_rsrc_t xr, uint32_t lane_off, double y[4],
+                                          uint32_t wb = 0)
 {
     for (int f = 0; f < cnt; f += 8) {
         int32_t c[8];
@@ -178,7 +185,7 @@ __device__ __forceinline__ void ws_gather(CP cp, VP vp, int o0, int len0, int o1
         double2 xs[8];
 #pragma unroll
         for (int tt = 0; tt < 8; ++tt) {
-            const uint32_t off = f + tt < cnt ? __umul24((unsigned)c[tt], 128u) + lane_off : 0x80000000u;
+            const uint32_t off = f + tt < cnt ? __umul24((unsigned)c[tt] - wb, 128u) + lane_off : 0x80000000u;
             const auto u4 = __builtin_amdgcn_raw_buffer_load_b128(xr, off, 0, 0);
             __builtin_memcpy(&xs[tt], &u4, 16);
         }

@@ -1,5 +1,6 @@
 // test_lanczos.cpp -- the reference driver (test_lanczos.cu:131-362) rebuilt on
-// the C ABI: same CLI (-N grid, -m iterations) and output lines, plus
+// the C++ drop-in layer include/lz_methods.hpp (the reference's methods/ API
+// over the C ABI): same CLI (-N grid, -m iterations) and output lines, plus
 // options for the block width, the operator and the validation run.
 //
 //   test_lanczos [-N 10] [-m 5] [--block 4] [--vector] [--unfused]
@@ -20,8 +21,7 @@
 #include <string>
 #include <vector>
 
-#include "lz_hip.h"
-#include "lz_host.h"
+#include "lz_methods.hpp"
 
 #define CHECK(x)                                                                        \
     do {                                                                                \
@@ -31,15 +31,6 @@
             std::exit(1);                                                               \
         }                                                                               \
     } while (0)
-#define HCHECK(x)                                                                       \
-    do {                                                                                \
-        hipError_t e_ = (x);                                                            \
-        if (e_ != hipSuccess) {                                                         \
-            std::fprintf(stderr, "%s: %s\n", #x, hipGetErrorString(e_));                \
-            std::exit(1);                                                               \
-        }                                                                               \
-    } while (0)
-
 struct Csr {
     int64_t n = 0, nnz = 0;
     std::vector<int64_t> rp;
@@ -63,15 +54,6 @@ static Csr matrix_a(int N, bool bug)
     CHECK(lzh_ell_to_csr_fill(n, 4, d.data(), ix.data(), 0, A.rp.data(), A.col.data(),
                               A.val.data()));
     return A;
-}
-
-template <typename T>
-static T *dev_copy(const std::vector<T> &h)
-{
-    T *d = nullptr;
-    HCHECK(hipMalloc(&d, sizeof(T) * std::max<size_t>(1, h.size())));
-    if (!h.empty()) HCHECK(hipMemcpy(d, h.data(), sizeof(T) * h.size(), hipMemcpyHostToDevice));
-    return d;
 }
 
 int main(int argc, char **argv)
@@ -145,52 +127,57 @@ int main(int argc, char **argv)
     std::vector<double> B((size_t)n * b);
     CHECK(lzh_rand_B(n, b, 1, 1, 1, B.data()));
 
-    lz_handle *h = nullptr;
-    CHECK(lz_init(device, &h));
-    int64_t *d_rp = dev_copy(A.rp);
-    int32_t *d_col = dev_copy(A.col);
-    double *d_val = dev_copy(A.val);
-    double *d_B = dev_copy(B);
-    double *d_q0, *d_q1, *d_w, *d_q, *d_alpha, *d_beta;
-    const size_t blk = sizeof(double) * n * b;
-    HCHECK(hipMalloc(&d_q0, blk));
-    HCHECK(hipMalloc(&d_q1, blk));
-    HCHECK(hipMalloc(&d_w, blk));
-    HCHECK(hipMalloc(&d_q, sizeof(double) * m * b));
-    HCHECK(hipMalloc(&d_alpha, sizeof(double) * m * b * b));
-    HCHECK(hipMalloc(&d_beta, sizeof(double) * (m + 1) * b * b));
-    HCHECK(hipDeviceSynchronize());
-
-    std::printf(" start Lanczos \n");
-    auto t0 = std::chrono::steady_clock::now();
-    if (vector)
-        CHECK(lz_vector_lanczos(h, n, A.nnz, d_rp, d_col, d_val, LZ_F64, m, lc, d_B, d_q, d_alpha,
-                                d_beta, d_q0, d_q1, d_w));
-    else if (unfused)
-        CHECK(lz_block_lanczos_unfused(h, n, A.nnz, d_rp, d_col, d_val, LZ_F64, b, m, lc, d_B, d_q,
-                                       d_alpha, d_beta, d_q0, d_q1, d_w));
-    else
-        CHECK(lz_block_lanczos(h, n, A.nnz, d_rp, d_col, d_val, LZ_F64, b, m, lc, d_B, d_q,
-                               d_alpha, d_beta, d_q0, d_q1, d_w));
-    HCHECK(hipDeviceSynchronize());
-    auto t1 = std::chrono::steady_clock::now();
-    std::printf(" end Lanczos \n");
-    std::printf("elapsed time: %11.6f\n", std::chrono::duration<double>(t1 - t0).count());
-
-    std::vector<double> q(m * b), alpha(m * b * b), beta((m + 1) * b * b);
-    HCHECK(hipMemcpy(q.data(), d_q, sizeof(double) * q.size(), hipMemcpyDeviceToHost));
-    HCHECK(hipMemcpy(alpha.data(), d_alpha, sizeof(double) * alpha.size(), hipMemcpyDeviceToHost));
-    HCHECK(hipMemcpy(beta.data(), d_beta, sizeof(double) * beta.size(), hipMemcpyDeviceToHost));
+    // the reference driver's objects (test_lanczos.cu:190-236) as lz_methods.hpp containers
+    lz::Context ctx(device);
+    lz::Csr_matrix<double> Ad(n, n, A.rp, A.col, A.val);
+    lz::Vector<double> q((int64_t)m * b);
+    std::vector<double> alpha, beta;  // host copies, m * b * b and (m + 1) * b * b
+    std::vector<double> sol;
     if (vector) {
+        std::vector<double> bvec(n);
+        for (int64_t r = 0; r < n; ++r) bvec[r] = B[r];
+        lz::Vector<double> bv(bvec), q0(n), q1(n), w(n);
+        std::vector<double> al(m), be(m);
+        std::printf(" start Lanczos \n");
+        auto t0 = std::chrono::steady_clock::now();
+        lz::vector_lanczos(Ad, bv, m, lc, q, al.data(), be.data(), q0, q1, w, ctx);
+        auto t1 = std::chrono::steady_clock::now();
+        std::printf(" end Lanczos \n");
+        std::printf("elapsed time: %11.6f\n", std::chrono::duration<double>(t1 - t0).count());
         // scalar recurrence: beta[0] = ||b||; T off-diagonal = beta[1..]
-        std::vector<double> bsc(m);
-        for (int j = 0; j < m; ++j) bsc[j] = beta[j];
-        beta.assign(bsc.begin(), bsc.end());
+        alpha = al;
+        beta = be;
         beta.push_back(0.0);
+    } else {
+        lz::Dense_matrix<double> Bm(n, b, B), Q0(n, b), Q1(n, b), W(n, b);
+        std::vector<lz::Dense_matrix<double>> al, be;
+        for (int j = 0; j < m; ++j) al.emplace_back(b, b);
+        for (int j = 0; j <= m; ++j) be.emplace_back(b, b);
+        std::printf(" start Lanczos \n");
+        auto t0 = std::chrono::steady_clock::now();
+        if (unfused)
+            lz::block_lanczos_blas_reference_order(Ad, Bm, m, lc, q, al.data(), be.data(), Q0, Q1, W, ctx);
+        else
+            lz::block_lanczos_blas(Ad, Bm, m, lc, q, al.data(), be.data(), Q0, Q1, W, ctx);
+        auto t1 = std::chrono::steady_clock::now();
+        std::printf(" end Lanczos \n");
+        std::printf("elapsed time: %11.6f\n", std::chrono::duration<double>(t1 - t0).count());
+        if (ctx.device_error()) {
+            std::fprintf(stderr, "device error word set: results invalid\n");
+            return 1;
+        }
+        for (auto &x : al) {
+            const auto v = x.copy_to_host();
+            alpha.insert(alpha.end(), v.begin(), v.end());
+        }
+        for (auto &x : be) {
+            const auto v = x.copy_to_host();
+            beta.insert(beta.end(), v.begin(), v.end());
+        }
     }
-    std::vector<double> ritz(m * b), sol(b);
-    CHECK(lzh_ritz_values(m, b, alpha.data(), beta.data(), ritz.data()));
-    CHECK(lzh_block_solution(m, b, T_end, alpha.data(), beta.data(), q.data(), sol.data()));
+    const std::vector<double> qh = q.copy_to_host();
+    const std::vector<double> ritz = lz::ritz_values(m, b, alpha, beta);
+    sol = lz::block_solution(m, b, T_end, alpha, beta, qh);
     std::printf("Ritz values (%d):", m * b);
     for (double r : ritz) std::printf(" %.15e", r);
     std::printf("\nSolution for block lanczos\n");
@@ -198,12 +185,8 @@ int main(int argc, char **argv)
 
     if (fdtd_steps > 0) {
         std::printf(" start fdtd \n");
-        double *d_out;
-        HCHECK(hipMalloc(&d_out, sizeof(double) * b));
-        CHECK(lz_fdtd_block(h, n, A.nnz, d_rp, d_col, d_val, LZ_F64, b, d_B, fdtd_steps, T_end, lc,
-                            d_q0, d_q1, d_out));
-        std::vector<double> fd(b);
-        HCHECK(hipMemcpy(fd.data(), d_out, sizeof(double) * b, hipMemcpyDeviceToHost));
+        lz::Dense_matrix<double> U0(n, b, B);
+        const std::vector<double> fd = lz::ftdt_block(Ad, U0, (unsigned)fdtd_steps, T_end, lc, ctx);
         std::printf("Solution from fdtd\n");
         double num = 0, den = 0;
         for (int c = 0; c < b; ++c) {
@@ -212,8 +195,6 @@ int main(int argc, char **argv)
             den += fd[c] * fd[c];
         }
         std::printf("Relative error for block lanczos is %.6e\n", std::sqrt(num / den));
-        HCHECK(hipFree(d_out));
     }
-    lz_finalize(h);
     return 0;
 }

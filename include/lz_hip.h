@@ -172,14 +172,22 @@ int lz_comm_unique_id(unsigned char out[128]);
 int lz_comm_init(lz_handle *h, int nranks, int rank, const unsigned char id[128]);
 int lz_comm_destroy(lz_handle *h);
 
-/* Distributed block Lanczos.  A_local: the rank's n_local rows in CSR with
- * GLOBAL column indices; X_full: n_global x b row-major workspace that receives
- * the all-gathered Krylov block every iteration (ncclAllGather over xGMI);
- * row_counts[nranks] (host) = rows per rank (the all-gather needs equal counts:
- * every rank passes max(row_counts) as n_pad and pads its slab).  B_local,
- * Q0, W: n_pad x b (the residual slab alternates between W and Q0 and is
- * all-gathered whole); Q1 unused.  lc_rank: the rank owning row lc (q written there only;
- * other ranks' q untouched).  Outputs alpha/beta identical on every rank. */
+/* Distributed block Lanczos, all-gather form (the north star's exchange).
+ * Every rank's slab is padded to n_pad rows (n_pad >= max rows per rank) and
+ * ncclAllGather places rank g's slab at rows [g*n_pad, (g+1)*n_pad) of X_full,
+ * so:
+ *   - A_local: the rank's n_local rows in CSR whose columns are in the PADDED
+ *     numbering (global row r of rank g -> g*n_pad + (r - row0_g); host helper
+ *     lzh_remap_cols_padded of include/lz_host.h);
+ *   - X_full: n_global x b row-major workspace with n_global == n_pad * nranks
+ *     (checked), receiving the all-gathered residual every iteration;
+ *   - B_local, Q0, W: n_pad x b (rows past n_local are zero padding; the
+ *     residual slab alternates between W and Q0 and is all-gathered whole);
+ *     Q1 unused.
+ * lc_rank: the rank owning row lc (q written there only; other ranks' q
+ * untouched).  Outputs alpha/beta identical on every rank.  Gather sources of
+ * 2^24+ rows take the windowed fused pass (each strip's columns within 2^23
+ * rows of its own padded row), else the 64-bit addressed one. */
 int lz_block_lanczos_dist(lz_handle *h, int64_t n_local, int64_t n_pad, int64_t n_global,
                           int64_t nnz_local, const int64_t *row_ptr, const int32_t *col,
                           const void *val, lz_dtype dtype, int b, int m, int64_t lc_local,

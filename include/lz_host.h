@@ -68,6 +68,8 @@ int lzh_rand_B(int64_t n, int b, uint32_t seed, int64_t skip, int row_major, dou
 int64_t lzh_rand_lc(uint32_t seed);
 /* uniform [1,2) start block from splitmix64 (row-major n x b) */
 int lzh_uniform_B(int64_t n, int b, uint64_t seed, double *out64, float *out32);
+/* rows [r0, r0 + n) of the same block (one rank's slab of the global start block) */
+int lzh_uniform_B_rows(int64_t r0, int64_t n, int b, uint64_t seed, double *o64, float *o32);
 
 /* ------------------------------------------------------ post-processing */
 /* symmetric eigen-decomposition: Householder tridiagonalisation + implicit QL.

@@ -46,7 +46,8 @@ def lib():
             "lzo_ritz_values": (_c_int, [_c_int, _c_int, _c_vp, _c_vp, _c_vp]),
             "lzo_block_solution": (_c_int, [_c_int, _c_int, _c_dbl, _c_vp, _c_vp, _c_vp, _c_vp]),
             "lzo_fdtd_block": (_c_int, [_c_i64, _c_vp, _c_vp, _c_vp, _c_int, _c_vp, _c_i64, _c_dbl, _c_i64, _c_vp]),
-            "lzo_time_block_iters": (_c_dbl, [_c_i64, _c_vp, _c_vp, _c_vp, _c_int, _c_int, _c_vp]),
+            "lzo_block_lanczos_timed": (_c_int, [_c_i64, _c_vp, _c_vp, _c_vp, _c_int, _c_int, _c_i64, _c_vp, _c_vp,
+                                                 _c_vp, _c_vp, _c_vp]),
         }
         for k, (r, a) in sig.items():
             f = getattr(L, k)
@@ -155,11 +156,21 @@ def fdtd_block(A, B, steps, T_end, lc):
     return out
 
 
-def time_block_iters(A, B, iters: int) -> float:
-    """Seconds for `iters` block-Lanczos iterations (excluding the start-up step)."""
+def block_lanczos_timed(A, B: np.ndarray, m: int, lc: int):
+    """block_lanczos restated, with the wall seconds of each iteration j = 1..m-1
+    (the start-up step untimed): (q, alpha, beta, t_each[m-1])."""
     rp, col, val = _csr(A)
     B = np.ascontiguousarray(B, np.float64)
-    return lib().lzo_time_block_iters(A.n, _p(rp), _p(col), _p(val.astype(np.float64)), B.shape[1], iters, _p(B))
+    n, b = B.shape
+    q = np.zeros(m * b)
+    alpha = np.zeros((m, b, b))
+    beta = np.zeros((m + 1, b, b))
+    t = np.zeros(max(m - 1, 1))
+    rc = lib().lzo_block_lanczos_timed(n, _p(rp), _p(col), _p(val.astype(np.float64)), b, m, lc, _p(B), _p(q),
+                                       _p(alpha), _p(beta), _p(t))
+    if rc:
+        raise RuntimeError(f"lzo_block_lanczos_timed rc={rc}")
+    return q, alpha, beta, t[: m - 1]
 
 
 # ------------------------------------------------- reference host code (_ref)

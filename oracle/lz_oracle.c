@@ -183,22 +183,21 @@ int lzo_sqrtm_pair(int b, const double *G, double *beta, double *beta_inv)
 int lzo_block_lanczos(int64_t n, const int64_t *rp, const int32_t *col, const double *val, int b,
                       int m, int64_t lc, const double *B, double *q, double *alpha, double *beta)
 {
-    return block_lanczos_impl_f64(n, rp, col, val, b, m, lc, B, q, alpha, beta, 0, NULL);
+    return block_lanczos_impl_f64(n, rp, col, val, b, m, lc, B, q, alpha, beta, NULL);
 }
 
 int lzo_block_lanczos_f32(int64_t n, const int64_t *rp, const int32_t *col, const float *val,
                           int b, int m, int64_t lc, const float *B, float *q, float *alpha,
                           float *beta)
 {
-    return block_lanczos_impl_f32(n, rp, col, val, b, m, lc, B, q, alpha, beta, 0, NULL);
+    return block_lanczos_impl_f32(n, rp, col, val, b, m, lc, B, q, alpha, beta, NULL);
 }
 
-double lzo_time_block_iters(int64_t n, const int64_t *rp, const int32_t *col, const double *val,
-                            int b, int iters, const double *B)
+int lzo_block_lanczos_timed(int64_t n, const int64_t *rp, const int32_t *col, const double *val, int b,
+                            int m, int64_t lc, const double *B, double *q, double *alpha, double *beta,
+                            double *t_each)
 {
-    double t = 0.0;
-    block_lanczos_impl_f64(n, rp, col, val, b, iters + 1, 0, B, NULL, NULL, NULL, 1, &t);
-    return t;
+    return block_lanczos_impl_f64(n, rp, col, val, b, m, lc, B, q, alpha, beta, t_each);
 }
 
 /* ------------------------------------------------- single-vector Lanczos

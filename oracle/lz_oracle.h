@@ -80,10 +80,13 @@ int lzo_fdtd_block(int64_t n, const int64_t *row_ptr, const int32_t *col, const 
                    int b, const double *B, int64_t steps, double T_end, int64_t lc,
                    double *out);
 
-/* Timing helper for the CPU baseline: runs `iters` block-Lanczos iterations of
- * the oracle on (A, B) and returns the wall seconds of the iterations only. */
-double lzo_time_block_iters(int64_t n, const int64_t *row_ptr, const int32_t *col,
-                            const double *val, int b, int iters, const double *B);
+/* lzo_block_lanczos with per-iteration wall times: t_each[j - 1] = seconds of
+ * iteration j (j = 1..m-1; the start-up step is not timed).  bench.py's CPU
+ * baseline (best of the timed iterations) and its parity field (q/alpha/beta
+ * of the same run against the GPU's) both come from one call. */
+int lzo_block_lanczos_timed(int64_t n, const int64_t *row_ptr, const int32_t *col, const double *val,
+                            int b, int m, int64_t lc, const double *B, double *q, double *alpha,
+                            double *beta, double *t_each);
 
 #ifdef __cplusplus
 }

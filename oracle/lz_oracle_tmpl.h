@@ -80,8 +80,7 @@ static void FN(tsmm_rm)(int64_t n, int b, REAL s_w, REAL s_q, const REAL *Q, con
 /* block_lanczos_blas, methods/block_lanczos.hpp:104-166, op for op. */
 static int FN(block_lanczos_impl)(int64_t n, const int64_t *rp, const int32_t *col,
                                   const REAL *val, int b, int m, int64_t lc, const REAL *B,
-                                  REAL *q, REAL *alpha, REAL *beta, int iters_only,
-                                  double *t_iters)
+                                  REAL *q, REAL *alpha, REAL *beta, double *t_each)
 {
     if (b < 1 || b > 64 || m < 1 || n < 1) return -1;
     const size_t nb = (size_t)n * b, bb = (size_t)b * b;
@@ -108,8 +107,9 @@ static int FN(block_lanczos_impl)(int64_t n, const int64_t *rp, const int32_t *c
     /* W = W - Q0*alpha (:128) */
     FN(tsmm_rm)(n, b, 1, -1, Q0, Al, W);
 
-    double t0 = lzo_wtime();
+    /* t_each[j - 1]: wall time of iteration j (the CPU baseline's samples) */
     for (int j = 1; j < m; ++j) {
+        const double t0 = lzo_wtime();
         FN(gram_rm)(n, b, W, W, G);                                /* :137 */
         lzo_sqrtm_pair(b, G, Sq, Si);                              /* :142 */
         if (beta) for (size_t k = 0; k < bb; ++k) beta[j * bb + k] = (REAL)Sq[k];
@@ -124,10 +124,9 @@ static int FN(block_lanczos_impl)(int64_t n, const int64_t *rp, const int32_t *c
         FN(tsmm_rm)(n, b, 1, -1, Q1, Al, W);                       /* :159 */
         { REAL *t = Q0; Q0 = Q1; Q1 = t; }                         /* :162 */
         if (q) for (int c = 0; c < b; ++c) q[j * b + c] = Q0[lc * b + c]; /* :165 */
+        if (t_each) t_each[j - 1] = lzo_wtime() - t0;
     }
-    if (t_iters) *t_iters = lzo_wtime() - t0;
     if (beta) for (size_t k = 0; k < bb; ++k) beta[(size_t)m * bb + k] = (REAL)Si[k];
-    (void)iters_only;
     free(Q0); free(Q1); free(W);
     return 0;
 }

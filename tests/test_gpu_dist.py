@@ -6,9 +6,10 @@ multi-GPU bench is the only place more ranks run).
   all-reduces and the compact-column fused pass, against the oracle
   (methods/block_lanczos.hpp:104-166 op order).
 * lz_block_lanczos_dist (all-gather form) with a one-rank communicator.
-* The wide-address fallbacks: a gather source of >= 2^24 rows / >= 2 GiB
-  (what the all-gather path sees at 2+ ranks of 10M rows) runs the 64-bit
-  addressed fused pass and SpMM kernels; checked against the oracle.
+* Gather sources of >= 2^24 rows / >= 2 GiB (what the all-gather path sees
+  at 2+ ranks of 10M rows, and config C4 on one GPU): the windowed fused pass
+  and SpMM kernels, and the 64-bit fallbacks when columns leave the window;
+  checked against the oracle.
 The decomposition at 2 and 3 ranks is checked on CPU (tests/test_dist_gloo.py).
 """
 import numpy as np
@@ -85,45 +86,77 @@ def test_allgather_dist_single_rank(lz, orc, torch_cuda):
     assert_close_run(lz, m, 16, got, orc.block_lanczos(A, B, m, lc))
 
 
-def test_wide_address_fused_pass(lz, orc, torch_cuda):
-    """n_pad = 2^24 + 64 rows of gather source (2.1 GB): the all-gather form's
-    fused pass takes the 64-bit addressed tile kernel."""
+def _run_dist_wide(lz, h, torch, A, B, m, lc, n_pad):
+    """One-rank all-gather run with a padded gather source of n_pad rows."""
+    kw = dict(dtype=torch.float64, device="cuda")
+    n = A.n
+    Bp = torch.zeros(n_pad, 16, **kw)
+    Bp[:n] = torch.from_numpy(B).cuda()
+    W = torch.zeros(n_pad, 16, **kw)
+    X = torch.zeros(n_pad, 16, **kw)
+    Q0 = torch.zeros(n_pad, 16, **kw)
+    q, al, be = torch.zeros(m * 16, **kw), torch.zeros(m, 16, 16, **kw), torch.zeros(m + 1, 16, 16, **kw)
+    Ad = lz.CsrDevice.from_host(A, n_cols=n_pad)
+    h.block_lanczos_dist(Ad, n_pad, n_pad, Bp, m, lc, 0, q, al, be, Q0, W, X)
+    torch.cuda.synchronize()
+    return q.cpu().numpy(), al.cpu().numpy(), be.cpu().numpy()
+
+
+@pytest.mark.parametrize("far", [False, True])
+def test_wide_address_fused_pass(lz, orc, torch_cuda, far):
+    """n_pad = 2^24 + 64 rows of gather source (2.1 GB, past a 32-bit buffer
+    offset).  far=False: every strip's columns lie in its 2^24-row window, so
+    the windowed k_fused_pp16 runs; far=True: a few columns point 2^24 rows
+    away (padding rows, zero), the window check fails and the 64-bit tile
+    kernel runs.  Both against the oracle."""
     torch = torch_cuda
     A = lz.gen_banded(20011, 10.0, 500, seed=51)
     B = lz.uniform_B(A.n, 16, seed=52)
     m, lc = 5, 4321
-    n, n_pad = A.n, (1 << 24) + 64
-    kw = dict(dtype=torch.float64, device="cuda")
+    n_pad = (1 << 24) + 64
+    Ag = A
+    if far:  # append one far column (a zero padding row of X) to a few rows
+        import scipy.sparse as sp
+        M = sp.csr_matrix((A.val, A.col, A.row_ptr), shape=(A.n, n_pad)).tolil()
+        for r in (3, 9000, A.n - 1):
+            M[r, n_pad - 1] = 0.5
+        M = M.tocsr()
+        M.sort_indices()
+        Ag = lz.CsrHost(A.n, M.indptr.astype(np.int64), M.indices.astype(np.int32), M.data)
     h = lz.Handle(0)
     try:
         h.comm_init(1, 0, lz.comm_unique_id())
-        Bp = torch.zeros(n_pad, 16, **kw)
-        Bp[:n] = torch.from_numpy(B).cuda()
-        W = torch.zeros(n_pad, 16, **kw)
-        X = torch.zeros(n_pad, 16, **kw)
-        q, al, be = torch.zeros(m * 16, **kw), torch.zeros(m, 16, 16, **kw), torch.zeros(m + 1, 16, 16, **kw)
-        Q0 = torch.zeros(n_pad, 16, **kw)
-        Ad = lz.CsrDevice.from_host(A, n_cols=n_pad)
-        h.block_lanczos_dist(Ad, n_pad, n_pad, Bp, m, lc, 0, q, al, be, Q0, W, X)
-        torch.cuda.synchronize()
-        got = (q.cpu().numpy(), al.cpu().numpy(), be.cpu().numpy())
-        del Bp, W, X
+        got = _run_dist_wide(lz, h, torch, Ag, B, m, lc, n_pad)
+        assert h.device_error() == 0
     finally:
         h.close()
     assert_close_run(lz, m, 16, got, orc.block_lanczos(A, B, m, lc))
 
 
-@pytest.mark.parametrize("nx", [50021, (1 << 24) + 5])
-def test_rectangular_and_wide_address_spmm(lz, orc, handle, torch_cuda, nx):
-    """X with more rows than A (n_cols > n_rows); at 2^24 + 5 rows (2.1 GB,
-    b = 16 fp64) the 64-bit addressed kernel runs.  Columns spread over all of X."""
+@pytest.mark.parametrize("nx,layout", [(50021, "random"), ((1 << 24) + 5, "random"), ((1 << 24) + 5, "banded"),
+                                       ((1 << 24) + 5, "mixed")])
+def test_rectangular_and_wide_address_spmm(lz, orc, handle, torch_cuda, nx, layout):
+    """X with more rows than A (n_cols > n_rows).  At 2^24 + 5 rows (2.1 GB,
+    b = 16 fp64) the windowed nnz-split kernel runs: "banded" -- every tile's
+    columns fit one window (buffer-addressed gather based at the tile's
+    smallest column); "random" -- columns spread over all of X, every tile is
+    queued to the 64-bit long-tile kernel; "mixed" -- both kinds of tile."""
     torch = torch_cuda
     rng = np.random.default_rng(5)
     n = 3001
     cnt = rng.integers(0, 20, n)
     rp = np.concatenate([[0], np.cumsum(cnt)]).astype(np.int64)
-    col = rng.integers(0, nx, rp[-1]).astype(np.int32)
-    col[:4] = [0, nx - 1, nx - 2, min(1 << 24, nx - 3)]
+    rows = np.repeat(np.arange(n), cnt)
+    if layout == "random":
+        col = rng.integers(0, nx, rp[-1])
+        col[:4] = [0, nx - 1, nx - 2, min(1 << 24, nx - 3)]
+    else:
+        base = rows * 3000 + rng.integers(0, 2000, rp[-1])  # banded, up to ~9M
+        if layout == "mixed":
+            far = rows >= n // 2
+            base = np.where(far & (rng.random(rp[-1]) < 0.3), nx - 1 - rng.integers(0, 100, rp[-1]), base)
+        col = base
+    col = col.astype(np.int32)
     val = rng.standard_normal(rp[-1])
     A = lz.CsrHost(n, rp, col, val)
     X = torch.zeros(nx, 16, dtype=torch.float64, device="cuda")

@@ -74,7 +74,7 @@ def test_spmm_colmajor_padded_ld(lz, handle, torch_cuda, monkeypatch, direct):
     """The reference's Dense_matrix: leading dimension = padded rows (> n)."""
     torch = torch_cuda
     if direct:
-        monkeypatch.setenv("LZ_SPMM_CM", "direct")  # read once per process: may stay on the first value
+        monkeypatch.setenv("LZ_SPMM_CM", "direct")  # read per call: k_spmm_cm runs
     A = lz.gen_banded(1000, 6.0, 50, seed=4)
     n, b, ld = A.n, 16, 1024 + 7
     rng = np.random.default_rng(2)

@@ -105,16 +105,73 @@ def test_block_bug_compat_operator(lz, orc, handle, torch_cuda, golden):
     assert_close_run(lz, 5, 4, got, orc.block_lanczos(A, B, 5, lc))
 
 
-def test_block_f32_b32_powerlaw(lz, orc, handle, torch_cuda):
-    """C5 shape at small n: fp32, b = 32, power-law rows (load imbalance)."""
-    A = lz.gen_powerlaw(20000, 10.0, 2.1, 2000, seed=5, dtype=np.float32)
+def _f32_checks(lz, m, b, got, ref, rtol):
+    """fp32 run vs the fp32 oracle: alpha/beta/q within rtol relative to the
+    largest entry, Ritz values within rtol of the spectrum's scale."""
+    q, al, be = got
+    qo, ao, bo = ref
+    scale = max(np.abs(ao).max(), np.abs(bo[:m]).max())
+    assert np.max(np.abs(al - ao)) <= rtol * scale, np.max(np.abs(al - ao)) / scale
+    assert np.max(np.abs(be[:m] - bo[:m])) <= rtol * scale, np.max(np.abs(be[:m] - bo[:m])) / scale
+    assert np.max(np.abs(q - qo)) <= rtol * np.abs(qo).max(), np.max(np.abs(q - qo)) / np.abs(qo).max()
+    r_gpu = lz.ritz_values(m, b, al.astype(np.float64), be.astype(np.float64))
+    r_ref = lz.ritz_values(m, b, ao.astype(np.float64), bo.astype(np.float64))
+    assert np.max(np.abs(r_gpu - r_ref)) <= rtol * np.abs(r_ref).max(), np.max(np.abs(r_gpu - r_ref))
+
+
+# fp32 bar: 1e-4 relative (about 800 fp32 ulps at the largest entry, through
+# m steps of a recurrence without re-orthogonalisation and reordered fp32 sums)
+F32_RTOL = 1e-4
+
+
+@pytest.mark.parametrize("n,cap,m", [(20000, 2000, 4), (1_000_003, 100_000, 4)])
+def test_block_f32_b32_powerlaw(lz, orc, handle, torch_cuda, n, cap, m):
+    """C5 shape: fp32, b = 32, power-law rows (load imbalance); at n = 1M with
+    rows up to 1e5 the long-tile queue of the SpMM runs.  alpha, beta, the row
+    probe q and the Ritz values against the fp32 oracle."""
+    A = lz.gen_powerlaw(n, 10.0, 2.1, cap, seed=5, dtype=np.float32)
     B = lz.uniform_B(A.n, 32, seed=6, dtype=np.float32)
-    m, lc = 4, 17
-    q, al, be = gpu_block(lz, handle, torch_cuda, A, B, m, lc)
-    qo, ao, bo = orc.block_lanczos(A, B, m, lc)
-    scale = np.abs(ao).max()
-    assert np.max(np.abs(al - ao)) <= 2e-3 * scale
-    assert np.max(np.abs(be[:m] - bo[:m])) <= 2e-3 * max(scale, np.abs(bo).max())
+    lc = 17
+    got = gpu_block(lz, handle, torch_cuda, A, B, m, lc)
+    _f32_checks(lz, m, 32, got, orc.block_lanczos(A, B, m, lc), F32_RTOL)
+    assert handle.device_error() == 0
+
+
+def test_block_c3_full_size(lz, orc, handle, torch_cuda):
+    """BASELINE config C3 at full size (n = 1e7, nnz = 1e8, half-width 4096,
+    b = 16 fp64; the bench operator): Ritz values within 1e-10 of the oracle."""
+    A = lz.gen_banded(10_000_000, 10.0, 4096, seed=20261015)
+    B = lz.uniform_B(A.n, 16, seed=20261015)
+    m, lc = 4, 84
+    got = gpu_block(lz, handle, torch_cuda, A, B, m, lc)
+    assert handle.device_error() == 0
+    assert_close_run(lz, m, 16, got, orc.block_lanczos(A, B, m, lc))
+
+
+def test_block_b16_c4_density(lz, orc, handle, torch_cuda):
+    """C4's row density (25 nnz/row, half-width 2^16) at small n: pass 1's
+    10-consumer / 4400-entry shape and the SpMM's 1536-entry stage."""
+    A = lz.gen_banded(200_003, 25.0, 1 << 16, seed=44)
+    B = lz.uniform_B(A.n, 16, seed=45)
+    m, lc = 6, 100_000
+    for fused in (True, False):
+        got = gpu_block(lz, handle, torch_cuda, A, B, m, lc, fused=fused)
+        assert_close_run(lz, m, 16, got, orc.block_lanczos(A, B, m, lc))
+    assert handle.device_error() == 0
+
+
+def test_block_b16_window_2e24_rows(lz, orc, handle, torch_cuda):
+    """n = 2^24 + 4099 rows on one GPU (X past 2 GiB: the C4-on-one-GPU
+    regime): the windowed pass-1 and SpMM kernels, fused and unfused, against
+    the oracle.  12 nnz/row, half-width 2^16."""
+    A = lz.gen_banded((1 << 24) + 4099, 12.0, 1 << 16, seed=46)
+    B = lz.uniform_B(A.n, 16, seed=47)
+    m, lc = 3, (1 << 24) + 17
+    ref = orc.block_lanczos(A, B, m, lc)
+    for fused in (True, False):
+        got = gpu_block(lz, handle, torch_cuda, A, B, m, lc, fused=fused)
+        assert_close_run(lz, m, 16, got, ref)
+    assert handle.device_error() == 0
 
 
 def test_vector_lanczos(lz, orc, handle, torch_cuda, golden):
