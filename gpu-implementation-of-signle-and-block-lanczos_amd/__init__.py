@@ -518,8 +518,12 @@ class Handle:
                "lz_block_lanczos")
 
     def vector_lanczos(self, A: CsrDevice, bvec, m: int, lc: int, q, alpha, beta, q0, q1, w):
-        """vector_lanczos (methods/vector_lanczos.hpp:8-67); alpha/beta are device tensors."""
+        """vector_lanczos (methods/vector_lanczos.hpp:8-67); alpha/beta are device tensors.
+        fp64 or fp32: every vector must have A's element type."""
         n = bvec.shape[0]
+        for t in (bvec, q, alpha, beta, q0, q1, w):
+            if t.element_size() != (8 if A.dtype == LZ_F64 else 4):
+                raise ValueError("vector_lanczos: every vector must have A's element type")
         _check(self.L.lz_vector_lanczos(self.ptr, n, A.nnz, _ptr(A.row_ptr), _ptr(A.col), _ptr(A.val), A.dtype,
                                         m, lc, _ptr(bvec), _ptr(q), _ptr(alpha), _ptr(beta), _ptr(q0),
                                         _ptr(q1), _ptr(w)), "lz_vector_lanczos")

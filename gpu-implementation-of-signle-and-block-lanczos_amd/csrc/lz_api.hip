@@ -771,14 +771,17 @@ int lz_vector_lanczos(lz_handle *h, int64_t n, int64_t nnz, const int64_t *rp, c
 {
     LZ_HANDLE_CHECK(h);
     LZ_TRY(check_csr(n, nnz, rp, col, val));
-    LZ_ARG_CHECK(dtype == LZ_F64, "vector Lanczos: fp64 only");
     LZ_ARG_CHECK(n >= 1 && m >= 1 && lc >= 0 && lc < n, "vector Lanczos sizes");
     LZ_ARG_CHECK(bvec && q && alpha && beta && q0 && q1 && w, "NULL buffer");
     LZ_ARG_CHECK(bvec != q0 && bvec != q1 && bvec != w && q0 != q1 && q0 != w && q1 != w,
                  "b, q0, q1, w must be distinct buffers");
-    return vector_lanczos_dev(h, n, nnz, rp, col, (const double *)val, m, lc,
-                              (const double *)bvec, (double *)q, (double *)alpha, (double *)beta,
-                              (double *)q0, (double *)q1, (double *)w);
+    if (dtype == LZ_F64)
+        return vector_lanczos_dev<double>(h, n, nnz, rp, col, (const double *)val, m, lc,
+                                          (const double *)bvec, (double *)q, (double *)alpha,
+                                          (double *)beta, (double *)q0, (double *)q1, (double *)w);
+    return vector_lanczos_dev<float>(h, n, nnz, rp, col, (const float *)val, m, lc, (const float *)bvec,
+                                     (float *)q, (float *)alpha, (float *)beta, (float *)q0, (float *)q1,
+                                     (float *)w);
 }
 
 int lz_fdtd_block(lz_handle *h, int64_t n, int64_t nnz, const int64_t *rp, const int32_t *col,

@@ -18,6 +18,7 @@
 // between the W and Q1 buffers.  All epilogue products run on
 // v_mfma_f64_16x16x4_f64 (see lz_dense.hip for the operand layouts).
 #include <cstring>
+#include <type_traits>
 #include "lz_common.hpp"
 #include "lz_internal.hpp"
 #include "lz_kernels.hpp"
@@ -978,27 +979,41 @@ __device__ __forceinline__ void block_store_slab(double v, double *red, double *
 }
 
 // slabs of x.x (start of the recurrence, ||b||^2)
-__global__ __launch_bounds__(kVlThreads) void k_vl_sq(int64_t n, const double *__restrict__ x,
+template <typename T>
+__global__ __launch_bounds__(kVlThreads) void k_vl_sq(int64_t n, const T *__restrict__ x,
                                                       double *__restrict__ part)
 {
     __shared__ double red[kVlThreads];
     double s = 0.0;
     for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n;
-         i += (int64_t)gridDim.x * blockDim.x)
-        s = fma(x[i], x[i], s);
+         i += (int64_t)gridDim.x * blockDim.x) {
+        const double xi = x[i];
+        s = fma(xi, xi, s);
+    }
     block_store_slab(s, red, part);
 }
 
-template <int LV>
+// beta_j = ||w|| rounded to T, and the scale 1./beta_j the reference multiplies
+// by (`mult_scalar(1./beta[j])`, vector_lanczos.hpp:46-47: a double quotient
+// rounded to T).  For T = double: sqrt and 1/sqrt, as before.
+template <typename T>
+__device__ __forceinline__ void vl_beta(double bsq, T &beta, T &rbeta)
+{
+    beta = (T)sqrt(bsq);
+    rbeta = (T)(1.0 / (double)beta);
+}
+
+template <typename T, int LV>
 __global__ __launch_bounds__(kVlThreads) void k_vl_spmv(
     int64_t n, const int64_t *__restrict__ rp, const int32_t *__restrict__ col,
-    const double *__restrict__ val, const double *__restrict__ w, double *__restrict__ qbuf,
-    double *__restrict__ wn, const double *__restrict__ part_in, int P, int has_prev, int64_t lc,
-    double *__restrict__ qrow, double *__restrict__ beta_out, double *__restrict__ part_out)
+    const T *__restrict__ val, const T *__restrict__ w, T *__restrict__ qbuf,
+    T *__restrict__ wn, const double *__restrict__ part_in, int P, int has_prev, int64_t lc,
+    T *__restrict__ qrow, T *__restrict__ beta_out, double *__restrict__ part_out)
 {
     __shared__ double red[kVlThreads];
     const double bsq = block_sum_slabs(part_in, P, red);
-    const double beta = sqrt(bsq), rbeta = 1.0 / beta;
+    T beta, rbeta;
+    vl_beta(bsq, beta, rbeta);
     if (blockIdx.x == 0 && threadIdx.x == 0) *beta_out = beta;
     constexpr int RB = kVlThreads / LV;
     const int gi = threadIdx.x / LV, p = threadIdx.x % LV;
@@ -1008,11 +1023,11 @@ __global__ __launch_bounds__(kVlThreads) void k_vl_spmv(
         const int64_t row = u * RB + gi;
         const bool valid = row < n;
         const int64_t k0 = valid ? rp[row] : 0, k1 = valid ? rp[row + 1] : 0;
-        double acc = 0.0;
+        T acc = 0;
         int64_t k = k0 + p;
         for (; k + LV < k1; k += 2 * LV) {
             const int c0 = col[k], c1 = col[k + LV];
-            const double v0 = val[k], v1 = val[k + LV];
+            const T v0 = val[k], v1 = val[k + LV];
             acc = fma(v0, w[c0], acc);
             acc = fma(v1, w[c1], acc);
         }
@@ -1020,12 +1035,12 @@ __global__ __launch_bounds__(kVlThreads) void k_vl_spmv(
 #pragma unroll
         for (int off = LV / 2; off > 0; off >>= 1) acc += __shfl_xor(acc, off, 64);
         if (valid && p == 0) {
-            const double qj = w[row] * rbeta;
-            double wv = acc * rbeta;
+            const T qj = w[row] * rbeta;
+            T wv = acc * rbeta;
             if (has_prev) wv = fma(-beta, qbuf[row], wv);
             qbuf[row] = qj;
             wn[row] = wv;
-            dot = fma(wv, qj, dot);
+            dot = fma((double)wv, (double)qj, dot);
             if (row == lc) *qrow = qj;
         }
     }
@@ -1054,7 +1069,8 @@ __global__ __launch_bounds__(NT) void k_vl_spmv_cs(
     __shared__ double yrow[R];
     __shared__ int64_t srp[R + 1];
     const double bsq = block_sum_slabs(part_in, P, red);
-    const double beta = sqrt(bsq), rbeta = 1.0 / beta;
+    double beta, rbeta;
+    vl_beta(bsq, beta, rbeta);
     if (blockIdx.x == 0 && threadIdx.x == 0) *beta_out = beta;
     const int t = threadIdx.x, lane = t & 63, wv = t >> 6;
     double dot = 0.0;
@@ -1176,34 +1192,34 @@ __global__ __launch_bounds__(256) void k_vl_band(int64_t n, const int64_t *__res
 
 // Tile loop of k_vl_spmv_win; WIN selects LDS-ring or global gathers at
 // compile time (a runtime select would make every gather a flat load).
-template <int LV, int NT, int RING, bool WIN>
+template <typename T, int LV, int NT, int RING, bool WIN>
 __device__ __forceinline__ double vl_win_tiles(int64_t n, int64_t c0, int64_t c1, int64_t H,
                                                const int64_t *__restrict__ rp,
                                                const int32_t *__restrict__ col,
-                                               const double *__restrict__ val,
-                                               const double *__restrict__ w, double *__restrict__ qbuf,
-                                               double *__restrict__ wn, int has_prev, int64_t lc,
-                                               double *__restrict__ qrow, double beta, double rbeta,
-                                               double *ring, double *yrow)
+                                               const T *__restrict__ val,
+                                               const T *__restrict__ w, T *__restrict__ qbuf,
+                                               T *__restrict__ wn, int has_prev, int64_t lc,
+                                               T *__restrict__ qrow, T beta, T rbeta,
+                                               T *ring, T *yrow)
 {
     constexpr int R = NT;
     constexpr int RPP = NT / LV, PASSES = R / RPP;  // rows per pass, passes per tile
     const int t = threadIdx.x, g = t / LV, p = t % LV;
     const int64_t base = c0 - H;  // ring slot of w[i]: (i - base) mod RING
     auto slot = [&](int64_t i) -> int { return (int)((uint32_t)(i - base) % (uint32_t)RING); };
-    auto wat = [&](int64_t i) -> double { return WIN ? ring[slot(i)] : w[i]; };
+    auto wat = [&](int64_t i) -> T { return WIN ? ring[slot(i)] : w[i]; };
     double dot = 0.0;
     for (int64_t r0 = c0; r0 < c1; r0 += R) {
         const int rows = (int)(c1 - r0 < R ? c1 - r0 : R);
         // next tile's slab and this thread's epilogue row, issued first
         const int64_t si = r0 + R + H + t;
-        const double slab = (WIN && si < n) ? w[si] : 0.0;
+        const T slab = (WIN && si < n) ? w[si] : T(0);
         const int64_t erow = r0 + t;
-        const double qprev = (t < rows && has_prev) ? qbuf[erow] : 0.0;
+        const T qprev = (t < rows && has_prev) ? qbuf[erow] : T(0);
         // CSR offsets relative to the tile's first entry (a tile's run < 2^31)
         const int64_t kb = rp[r0];
         const int32_t *cb = col + kb;
-        const double *vb = val + kb;
+        const T *vb = val + kb;
         int ks[PASSES], ke[PASSES];
 #pragma unroll
         for (int s = 0; s < PASSES; ++s) {
@@ -1212,18 +1228,18 @@ __device__ __forceinline__ double vl_win_tiles(int64_t n, int64_t c0, int64_t c1
             ke[s] = lr < rows ? (int)(rp[r0 + lr + 1] - kb) : 0;
         }
         int c[PASSES][2];
-        double v[PASSES][2];
+        T v[PASSES][2];
 #pragma unroll
         for (int s = 0; s < PASSES; ++s)
 #pragma unroll
             for (int h2 = 0; h2 < 2; ++h2) {
                 const int k = ks[s] + p + h2 * LV;
                 c[s][h2] = k < ke[s] ? cb[k] : -1;
-                v[s][h2] = k < ke[s] ? vb[k] : 0.0;
+                v[s][h2] = k < ke[s] ? vb[k] : T(0);
             }
 #pragma unroll
         for (int s = 0; s < PASSES; ++s) {
-            double acc = 0.0;
+            T acc = 0;
 #pragma unroll
             for (int h2 = 0; h2 < 2; ++h2)
                 if (c[s][h2] >= 0) acc = fma(v[s][h2], wat(c[s][h2]), acc);
@@ -1234,12 +1250,12 @@ __device__ __forceinline__ double vl_win_tiles(int64_t n, int64_t c0, int64_t c1
         }
         __syncthreads();
         if (t < rows) {
-            const double qj = wat(erow) * rbeta;
-            double wv = yrow[t] * rbeta;
+            const T qj = wat(erow) * rbeta;
+            T wv = yrow[t] * rbeta;
             if (has_prev) wv = fma(-beta, qprev, wv);
             qbuf[erow] = qj;
             wn[erow] = wv;
-            dot = fma(wv, qj, dot);
+            dot = fma((double)wv, (double)qj, dot);
             if (erow == lc) *qrow = qj;
         }
         if (WIN && si < n) ring[slot(si)] = slab;  // disjoint from this tile's window (2H + 2R <= ring)
@@ -1248,31 +1264,33 @@ __device__ __forceinline__ double vl_win_tiles(int64_t n, int64_t c0, int64_t c1
     return dot;
 }
 
-template <int LV, int NT, int RING>
+template <typename T, int LV, int NT, int RING>
 __global__ __launch_bounds__(NT) void k_vl_spmv_win(
     int64_t n, const int64_t *__restrict__ rp, const int32_t *__restrict__ col,
-    const double *__restrict__ val, const double *__restrict__ w, double *__restrict__ qbuf,
-    double *__restrict__ wn, const double *__restrict__ part_in, int P, int has_prev, int64_t lc,
-    double *__restrict__ qrow, double *__restrict__ beta_out, double *__restrict__ part_out,
+    const T *__restrict__ val, const T *__restrict__ w, T *__restrict__ qbuf,
+    T *__restrict__ wn, const double *__restrict__ part_in, int P, int has_prev, int64_t lc,
+    T *__restrict__ qrow, T *__restrict__ beta_out, double *__restrict__ part_out,
     const unsigned long long *__restrict__ band)
 {
     constexpr int R = NT, NI = (RING + NT - 1) / NT;
-    __shared__ double ring[RING];
-    __shared__ double yrow[R];  // also the slab reduction scratch
+    __shared__ T ring[RING];
+    __shared__ double red[R];  // the slab reduction scratch
+    __shared__ T yrow[R];
     const int t = threadIdx.x;
     const int64_t H = (int64_t)*band;
     const bool win = 2 * H + 2 * R <= RING;  // block-uniform
     const int64_t c0 = n * blockIdx.x / gridDim.x, c1 = n * (blockIdx.x + 1) / gridDim.x;
     // first window w[c0 - H, c0 + R + H): all loads in flight, then the slab sum
-    double wi[NI];
+    T wi[NI];
     const int64_t lo = c0 - H < 0 ? 0 : c0 - H, hi = c0 + R + H < n ? c0 + R + H : n;
 #pragma unroll
     for (int k = 0; k < NI; ++k) {
         const int64_t i = lo + t + (int64_t)k * NT;
-        wi[k] = (win && i < hi) ? w[i] : 0.0;
+        wi[k] = (win && i < hi) ? w[i] : T(0);
     }
-    const double bsq = block_sum_slabs(part_in, P, yrow);
-    const double beta = sqrt(bsq), rbeta = 1.0 / beta;
+    const double bsq = block_sum_slabs(part_in, P, red);
+    T beta, rbeta;
+    vl_beta(bsq, beta, rbeta);
     if (blockIdx.x == 0 && t == 0) *beta_out = beta;
 #pragma unroll
     for (int k = 0; k < NI; ++k) {
@@ -1280,36 +1298,40 @@ __global__ __launch_bounds__(NT) void k_vl_spmv_win(
         if (win && i < hi) ring[(int)((uint32_t)(i - (c0 - H)) % (uint32_t)RING)] = wi[k];
     }
     __syncthreads();
-    const double dot = win ? vl_win_tiles<LV, NT, RING, true>(n, c0, c1, H, rp, col, val, w, qbuf, wn, has_prev,
-                                                              lc, qrow, beta, rbeta, ring, yrow)
-                           : vl_win_tiles<LV, NT, RING, false>(n, c0, c1, H, rp, col, val, w, qbuf, wn, has_prev,
-                                                               lc, qrow, beta, rbeta, ring, yrow);
-    block_store_slab(dot, yrow, part_out);
+    const double dot = win ? vl_win_tiles<T, LV, NT, RING, true>(n, c0, c1, H, rp, col, val, w, qbuf, wn, has_prev,
+                                                                 lc, qrow, beta, rbeta, ring, yrow)
+                           : vl_win_tiles<T, LV, NT, RING, false>(n, c0, c1, H, rp, col, val, w, qbuf, wn,
+                                                                  has_prev, lc, qrow, beta, rbeta, ring, yrow);
+    block_store_slab(dot, red, part_out);
 }
 
-__global__ __launch_bounds__(kVlThreads) void k_vl_update(int64_t n, double *__restrict__ wn,
-                                                          const double *__restrict__ q,
+template <typename T>
+__global__ __launch_bounds__(kVlThreads) void k_vl_update(int64_t n, T *__restrict__ wn,
+                                                          const T *__restrict__ q,
                                                           const double *__restrict__ part_in,
-                                                          int P, double *__restrict__ alpha_out,
+                                                          int P, T *__restrict__ alpha_out,
                                                           double *__restrict__ part_out)
 {
     __shared__ double red[kVlThreads];
-    const double alpha = block_sum_slabs(part_in, P, red);
+    const T alpha = (T)block_sum_slabs(part_in, P, red);
     if (blockIdx.x == 0 && threadIdx.x == 0) *alpha_out = alpha;
     double s = 0.0;
     for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n;
          i += (int64_t)gridDim.x * blockDim.x) {
-        const double v = fma(-alpha, q[i], wn[i]);
+        const T v = fma(-alpha, q[i], wn[i]);
         wn[i] = v;
-        s = fma(v, v, s);
+        const double vd = v;
+        s = fma(vd, vd, s);
     }
     block_store_slab(s, red, part_out);
 }
 
+template <typename T>
 int vector_lanczos_dev(lz_handle *h, int64_t n, int64_t nnz, const int64_t *rp, const int32_t *col,
-                       const double *val, int m, int64_t lc, const double *b, double *q,
-                       double *alpha, double *beta, double *q0, double *q1, double *w)
+                       const T *val, int m, int64_t lc, const T *b, T *q, T *alpha, T *beta, T *q0,
+                       T *q1, T *w)
 {
+    constexpr bool F64 = std::is_same<T, double>::value;
     const double mean = n > 0 ? (double)nnz / (double)n : 10.0;
     const int lv = mean <= 5 ? 4 : mean <= 12 ? 8 : mean <= 28 ? 16 : mean <= 60 ? 32 : 64;
     // LZ_VL_KERNEL=cs / cs2: the CSR-stream kernel, 512 / 256-row tiles (needs
@@ -1318,7 +1340,7 @@ int vector_lanczos_dev(lz_handle *h, int64_t n, int64_t nnz, const int64_t *rp, 
     // (measured once per solve: one host sync), else lanes-per-row.
     const char *vk = getenv("LZ_VL_KERNEL");
     const bool al16 = ((uintptr_t)col & 15) == 0 && ((uintptr_t)val & 15) == 0;
-    const int cs = !(vk && al16) ? 0 : !strcmp(vk, "cs") ? 1 : !strcmp(vk, "cs2") ? 2 : 0;
+    const int cs = !(F64 && vk && al16) ? 0 : !strcmp(vk, "cs") ? 1 : !strcmp(vk, "cs2") ? 2 : 0;
     unsigned long long *band = reinterpret_cast<unsigned long long *>(h->partials + 8192);
     int win = 0;  // 1: <512, 9216>, 2: <1024, 16384>
     if (!cs && lv <= 8 && !(vk && !strcmp(vk, "row"))) {
@@ -1345,23 +1367,23 @@ int vector_lanczos_dev(lz_handle *h, int64_t n, int64_t nnz, const int64_t *rp, 
     // slabs: two alternating regions of h->partials
     double *pa = h->partials, *pb = h->partials + 4096;
     const int gsq = gridu;
-    hipLaunchKernelGGL(k_vl_sq, dim3(gsq), dim3(kVlThreads), 0, h->stream, n, b, pa);
+    hipLaunchKernelGGL(k_vl_sq<T>, dim3(gsq), dim3(kVlThreads), 0, h->stream, n, b, pa);
     LZ_LAUNCH_CHECK();
     int P = gsq;
-    const double *wcur = b;
-    double *wbuf[2] = {w, q1};
+    const T *wcur = b;
+    T *wbuf[2] = {w, q1};
     int wi = 0;
     for (int j = 0; j < m; ++j) {
-        double *wnext = wbuf[wi];
+        T *wnext = wbuf[wi];
 #define LZ_VL_CASE(LV)                                                                          \
     case LV:                                                                                    \
-        hipLaunchKernelGGL((k_vl_spmv<LV>), dim3(grid), dim3(kVlThreads), 0, h->stream, n, rp, \
+        hipLaunchKernelGGL((k_vl_spmv<T, LV>), dim3(grid), dim3(kVlThreads), 0, h->stream, n, rp, \
                            col, val, wcur, q0, wnext, pa, P, j > 0 ? 1 : 0, lc, q + j, beta + j, \
                            pb);                                                                 \
         break;
         if (win) {
 #define LZ_VL_WIN(LV, NT, RING)                                                                            \
-    hipLaunchKernelGGL((k_vl_spmv_win<LV, NT, RING>), dim3(grid), dim3(NT), 0, h->stream, n, rp, col, val, \
+    hipLaunchKernelGGL((k_vl_spmv_win<T, LV, NT, RING>), dim3(grid), dim3(NT), 0, h->stream, n, rp, col, val, \
                        wcur, q0, wnext, pa, P, j > 0 ? 1 : 0, lc, q + j, beta + j, pb, band)
             if (win == 1) {
                 if (lv == 4) LZ_VL_WIN(4, 512, 9216); else LZ_VL_WIN(8, 512, 9216);
@@ -1369,12 +1391,17 @@ int vector_lanczos_dev(lz_handle *h, int64_t n, int64_t nnz, const int64_t *rp, 
                 if (lv == 4) LZ_VL_WIN(4, 1024, 16384); else LZ_VL_WIN(8, 1024, 16384);
             }
 #undef LZ_VL_WIN
-        } else if (cs == 1) {
-            hipLaunchKernelGGL((k_vl_spmv_cs<512, 3>), dim3(grid), dim3(512), 0, h->stream, n, nnz, rp,
-                               col, val, wcur, q0, wnext, pa, P, j > 0 ? 1 : 0, lc, q + j, beta + j, pb);
-        } else if (cs == 2) {
-            hipLaunchKernelGGL((k_vl_spmv_cs<256, 3>), dim3(grid), dim3(256), 0, h->stream, n, nnz, rp,
-                               col, val, wcur, q0, wnext, pa, P, j > 0 ? 1 : 0, lc, q + j, beta + j, pb);
+        } else if (cs) {  // fp64 only (cs is 0 otherwise); the casts are no-ops there
+            auto vd = reinterpret_cast<const double *>(val);
+            auto wc = reinterpret_cast<const double *>(wcur);
+            auto qd = reinterpret_cast<double *>(q0), wd = reinterpret_cast<double *>(wnext);
+            auto qr = reinterpret_cast<double *>(q + j), bj = reinterpret_cast<double *>(beta + j);
+            if (cs == 1)
+                hipLaunchKernelGGL((k_vl_spmv_cs<512, 3>), dim3(grid), dim3(512), 0, h->stream, n, nnz, rp,
+                                   col, vd, wc, qd, wd, pa, P, j > 0 ? 1 : 0, lc, qr, bj, pb);
+            else
+                hipLaunchKernelGGL((k_vl_spmv_cs<256, 3>), dim3(grid), dim3(256), 0, h->stream, n, nnz, rp,
+                                   col, vd, wc, qd, wd, pa, P, j > 0 ? 1 : 0, lc, qr, bj, pb);
         } else {
             switch (lv) {
                 LZ_VL_CASE(4)
@@ -1386,7 +1413,7 @@ int vector_lanczos_dev(lz_handle *h, int64_t n, int64_t nnz, const int64_t *rp, 
         }
 #undef LZ_VL_CASE
         LZ_LAUNCH_CHECK();
-        hipLaunchKernelGGL(k_vl_update, dim3(gridu), dim3(kVlThreads), 0, h->stream, n, wnext, q0,
+        hipLaunchKernelGGL(k_vl_update<T>, dim3(gridu), dim3(kVlThreads), 0, h->stream, n, wnext, q0,
                            pb, grid, alpha + j, pa);
         LZ_LAUNCH_CHECK();
         P = gridu;
@@ -1395,5 +1422,12 @@ int vector_lanczos_dev(lz_handle *h, int64_t n, int64_t nnz, const int64_t *rp, 
     }
     return LZ_OK;
 }
+
+template int vector_lanczos_dev<double>(lz_handle *, int64_t, int64_t, const int64_t *, const int32_t *,
+                                        const double *, int, int64_t, const double *, double *, double *,
+                                        double *, double *, double *, double *);
+template int vector_lanczos_dev<float>(lz_handle *, int64_t, int64_t, const int64_t *, const int32_t *,
+                                       const float *, int, int64_t, const float *, float *, float *, float *,
+                                       float *, float *, float *);
 
 }  // namespace lz

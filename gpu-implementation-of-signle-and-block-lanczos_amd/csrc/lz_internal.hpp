@@ -62,8 +62,9 @@ int fused_update16(lz_handle *h, int64_t n, double *Wn, const double *Wcur, cons
 int mm16(lz_handle *h, const double *A, const double *B, double *C);
 
 // fp64 scalar helpers for the vector Lanczos (lz_fused.hip)
+template <typename T>
 int vector_lanczos_dev(lz_handle *h, int64_t n, int64_t nnz, const int64_t *rp, const int32_t *col,
-                       const double *val, int m, int64_t lc, const double *b, double *q,
-                       double *alpha, double *beta, double *q0, double *q1, double *w);
+                       const T *val, int m, int64_t lc, const T *b, T *q, T *alpha, T *beta, T *q0,
+                       T *q1, T *w);
 
 }  // namespace lz

@@ -3,7 +3,7 @@
 // over the C ABI): same CLI (-N grid, -m iterations) and output lines, plus
 // options for the block width, the operator and the validation run.
 //
-//   test_lanczos [-N 10] [-m 5] [--block 4] [--vector] [--unfused]
+//   test_lanczos [-N 10] [-m 5] [--block 4] [--vector [--fp32]] [--unfused]
 //                [--matrix matrix_a|banded|powerlaw|file:PATH] [--n ROWS]
 //                [--nnz-per-row 10] [--halfwidth 4096] [--bug-compat-change-order]
 //                [--fdtd-steps 1000000] [--T-end 1] [--lc ROW] [--device 0]
@@ -59,7 +59,7 @@ static Csr matrix_a(int N, bool bug)
 int main(int argc, char **argv)
 {
     int N = 10, m = 5, b = 4, device = 0;
-    bool vector = false, unfused = false, bug = false;
+    bool vector = false, unfused = false, bug = false, fp32 = false;
     std::string matrix = "matrix_a";
     int64_t nrows = 1000000, halfwidth = 4096, fdtd_steps = 0, lc = -1;
     double npr = 10.0, T_end = 1.0;
@@ -74,6 +74,7 @@ int main(int argc, char **argv)
         else if (o == "--block") b = std::atoi(nxt());
         else if (o == "--vector") vector = true;
         else if (o == "--unfused") unfused = true;
+        else if (o == "--fp32") fp32 = true;  // --vector: test_VectorLanczos<float> (test_lanczos.cu:355)
         else if (o == "--matrix") matrix = nxt();
         else if (o == "--n") nrows = (int64_t)std::stod(nxt());
         else if (o == "--nnz-per-row") npr = std::stod(nxt());
@@ -86,6 +87,7 @@ int main(int argc, char **argv)
         else { std::fprintf(stderr, "unknown option %s\n", o.c_str()); return 2; }
     }
     if (vector) b = 1;
+    if (fp32 && !vector) { std::fprintf(stderr, "--fp32 applies to --vector\n"); return 2; }
     if (lc < 0) lc = lzh_rand_lc(1);  // 1 + rand() % 100, test_lanczos.cu:326
 
     Csr A;
@@ -133,7 +135,25 @@ int main(int argc, char **argv)
     lz::Vector<double> q((int64_t)m * b);
     std::vector<double> alpha, beta;  // host copies, m * b * b and (m + 1) * b * b
     std::vector<double> sol;
-    if (vector) {
+    std::vector<double> qh;
+    if (vector && fp32) {
+        std::vector<float> bvec(n), vf(A.val.begin(), A.val.end());
+        for (int64_t r = 0; r < n; ++r) bvec[r] = (float)B[r];
+        lz::Csr_matrix<float> Af(n, n, A.rp, A.col, vf);
+        lz::Vector<float> bv(bvec), q0(n), q1(n), w(n), qf(m);
+        std::vector<float> al(m), be(m);
+        std::printf(" start Lanczos \n");
+        auto t0 = std::chrono::steady_clock::now();
+        lz::vector_lanczos(Af, bv, m, lc, qf, al.data(), be.data(), q0, q1, w, ctx);
+        auto t1 = std::chrono::steady_clock::now();
+        std::printf(" end Lanczos \n");
+        std::printf("elapsed time: %11.6f\n", std::chrono::duration<double>(t1 - t0).count());
+        alpha.assign(al.begin(), al.end());
+        beta.assign(be.begin(), be.end());
+        beta.push_back(0.0);
+        const std::vector<float> qv = qf.copy_to_host();
+        qh.assign(qv.begin(), qv.end());
+    } else if (vector) {
         std::vector<double> bvec(n);
         for (int64_t r = 0; r < n; ++r) bvec[r] = B[r];
         lz::Vector<double> bv(bvec), q0(n), q1(n), w(n);
@@ -175,7 +195,7 @@ int main(int argc, char **argv)
             beta.insert(beta.end(), v.begin(), v.end());
         }
     }
-    const std::vector<double> qh = q.copy_to_host();
+    if (!(vector && fp32)) qh = q.copy_to_host();
     const std::vector<double> ritz = lz::ritz_values(m, b, alpha, beta);
     sol = lz::block_solution(m, b, T_end, alpha, beta, qh);
     std::printf("Ritz values (%d):", m * b);

@@ -148,7 +148,10 @@ int lz_block_lanczos_unfused(lz_handle *h, int64_t n, int64_t nnz, const int64_t
  * beta, q0, q1, w) (methods/vector_lanczos.hpp:8-67; the correct variant -- the
  * BLAS variant's axpy at :116 is a reference bug not reproduced).  alpha[m],
  * beta[m] are DEVICE arrays here (the reference keeps host arrays; copy them
- * back with one hipMemcpy after the call).  beta[0] = ||b||. */
+ * back with one hipMemcpy after the call).  beta[0] = ||b||.  fp64 or fp32
+ * (test_lanczos.cu:355 instantiates test_VectorLanczos<float>): fp32 storage,
+ * SpMV products and sums in fp32, the dot/norm reductions accumulated in fp64
+ * and rounded to fp32. */
 int lz_vector_lanczos(lz_handle *h, int64_t n, int64_t nnz, const int64_t *row_ptr,
                       const int32_t *col, const void *val, lz_dtype dtype, int m, int64_t lc,
                       const void *bvec, void *q, void *alpha, void *beta, void *q0, void *q1,

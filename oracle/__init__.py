@@ -42,6 +42,8 @@ def lib():
             "lzo_block_lanczos": (_c_int, [_c_i64, _c_vp, _c_vp, _c_vp, _c_int, _c_int, _c_i64, _c_vp, _c_vp, _c_vp, _c_vp]),
             "lzo_block_lanczos_f32": (_c_int, [_c_i64, _c_vp, _c_vp, _c_vp, _c_int, _c_int, _c_i64, _c_vp, _c_vp, _c_vp, _c_vp]),
             "lzo_vector_lanczos": (_c_int, [_c_i64, _c_vp, _c_vp, _c_vp, _c_int, _c_i64, _c_vp, _c_vp, _c_vp, _c_vp]),
+            "lzo_vector_lanczos_f32": (_c_int, [_c_i64, _c_vp, _c_vp, _c_vp, _c_int, _c_i64, _c_vp, _c_vp, _c_vp,
+                                                _c_vp]),
             "lzo_assemble_T": (None, [_c_int, _c_int, _c_vp, _c_vp, _c_vp]),
             "lzo_ritz_values": (_c_int, [_c_int, _c_int, _c_vp, _c_vp, _c_vp]),
             "lzo_block_solution": (_c_int, [_c_int, _c_int, _c_dbl, _c_vp, _c_vp, _c_vp, _c_vp]),
@@ -117,11 +119,14 @@ def block_lanczos(A, B: np.ndarray, m: int, lc: int):
 
 
 def vector_lanczos(A, bvec: np.ndarray, m: int, lc: int):
+    """vector_lanczos restated; fp32 when bvec is float32 (returns float32 arrays)."""
     rp, col, val = _csr(A)
-    bvec = np.ascontiguousarray(bvec, np.float64).ravel()
-    q, alpha, beta = np.zeros(m), np.zeros(m), np.zeros(m)
-    lib().lzo_vector_lanczos(A.n, _p(rp), _p(col), _p(val.astype(np.float64)), m, lc, _p(bvec), _p(q),
-                             _p(alpha), _p(beta))
+    f32 = np.asarray(bvec).dtype == np.float32
+    dt = np.float32 if f32 else np.float64
+    bvec = np.ascontiguousarray(bvec, dt).ravel()
+    q, alpha, beta = np.zeros(m, dt), np.zeros(m, dt), np.zeros(m, dt)
+    fn = lib().lzo_vector_lanczos_f32 if f32 else lib().lzo_vector_lanczos
+    fn(A.n, _p(rp), _p(col), _p(val.astype(dt)), m, lc, _p(bvec), _p(q), _p(alpha), _p(beta))
     return q, alpha, beta
 
 

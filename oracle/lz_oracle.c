@@ -238,6 +238,48 @@ int lzo_vector_lanczos(int64_t n, const int64_t *rp, const int32_t *col, const d
     return 0;
 }
 
+/* vector_lanczos<float> (methods/vector_lanczos.hpp:8-67 at T = float, as
+ * test_lanczos.cu:355 instantiates it): float vectors, float SpMV sums in CSR
+ * order; the norms and dots are accumulated in double and rounded to float
+ * (the product's choice -- the reference's float reductions are device code);
+ * the scale is 1./beta in double rounded to float (`mult_scalar(1./beta[j])`). */
+int lzo_vector_lanczos_f32(int64_t n, const int64_t *rp, const int32_t *col, const float *val, int m,
+                           int64_t lc, const float *bvec, float *q, float *alpha, float *beta)
+{
+    float *q0 = (float *)malloc(n * sizeof(float));
+    float *q1 = (float *)malloc(n * sizeof(float));
+    float *w = (float *)malloc(n * sizeof(float));
+    if (!q0 || !q1 || !w) return -2;
+    double s = 0.0;
+    for (int64_t i = 0; i < n; ++i) s += (double)bvec[i] * bvec[i];
+    beta[0] = (float)sqrt(s);                                          /* :20 */
+    float sc = (float)(1.0 / (double)beta[0]);
+    for (int64_t i = 0; i < n; ++i) q0[i] = bvec[i] * sc;              /* :23 */
+    q[0] = q0[lc];                                                     /* :26 */
+    lzo_csr_spmm_f32(n, rp, col, val, 1, q0, 1, w, 1);                 /* :29 */
+    s = 0.0;
+    for (int64_t i = 0; i < n; ++i) s += (double)w[i] * q0[i];
+    alpha[0] = (float)s;                                               /* :32 */
+    for (int64_t i = 0; i < n; ++i) w[i] -= alpha[0] * q0[i];          /* :35 */
+    for (int j = 1; j < m; ++j) {
+        s = 0.0;
+        for (int64_t i = 0; i < n; ++i) s += (double)w[i] * w[i];
+        beta[j] = (float)sqrt(s);                                      /* :43 */
+        sc = (float)(1.0 / (double)beta[j]);
+        for (int64_t i = 0; i < n; ++i) q1[i] = w[i] * sc;             /* :46-47 */
+        lzo_csr_spmm_f32(n, rp, col, val, 1, q1, 1, w, 1);             /* :50 */
+        for (int64_t i = 0; i < n; ++i) w[i] -= beta[j] * q0[i];       /* :53 */
+        s = 0.0;
+        for (int64_t i = 0; i < n; ++i) s += (double)w[i] * q1[i];
+        alpha[j] = (float)s;                                           /* :56 */
+        for (int64_t i = 0; i < n; ++i) w[i] -= alpha[j] * q1[i];      /* :59 */
+        float *t = q0; q0 = q1; q1 = t;                                /* :61 */
+        q[j] = q0[lc];                                                 /* :64 */
+    }
+    free(q0); free(q1); free(w);
+    return 0;
+}
+
 /* --------------------------------------------------------- T and results */
 void lzo_assemble_T(int m, int b, const double *alpha, const double *beta, double *T)
 {

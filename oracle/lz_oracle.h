@@ -61,6 +61,9 @@ int lzo_block_lanczos_f32(int64_t n, const int64_t *row_ptr, const int32_t *col,
 int lzo_vector_lanczos(int64_t n, const int64_t *row_ptr, const int32_t *col, const double *val,
                        int m, int64_t lc, const double *bvec,
                        double *q, double *alpha, double *beta);
+/* the same at T = float (test_lanczos.cu:355); reductions accumulated in double. */
+int lzo_vector_lanczos_f32(int64_t n, const int64_t *row_ptr, const int32_t *col, const float *val,
+                           int m, int64_t lc, const float *bvec, float *q, float *alpha, float *beta);
 
 /* T = Assemble_T(m, alpha, beta) (objects/tridiagonal_matrix.hpp:90-126, device
  * path): alpha_j on the diagonal, beta_j above (rows j-1, cols j) and beta_j^T

@@ -67,3 +67,17 @@ def test_driver_fdtd(lz, golden):
     _, sol, out = run_driver(lz, "-N", "3", "-m", "8", "--block", "4", "--fdtd-steps", "200000")
     rel = float(out.split("Relative error for block lanczos is")[1].split()[0])
     assert rel < 2e-8, rel  # CPU oracle at 2e5 steps: 4.57e-9 (forward Euler O(dt))
+
+
+def test_driver_vector_fp32(lz, orc, golden):
+    """--vector --fp32: test_VectorLanczos<float> (test_lanczos.cu:355) on the
+    driver's own operator and b, against the oracle's fp32 restatement."""
+    ritz, _, _ = run_driver(lz, "-N", "10", "-m", "10", "--vector", "--fp32")
+    from conftest import golden_csr
+    A = golden_csr(lz, golden, 10)
+    A32 = lz.CsrHost(A.n, A.row_ptr, A.col, A.val.astype(np.float32))
+    bv = lz.rand_B(A.n, 1)[:, 0].astype(np.float32)
+    _, ao, bo = orc.vector_lanczos(A32, bv, 10, int(golden["lc"]))
+    ref = lz.ritz_values(10, 1, ao.astype(np.float64), np.r_[bo, 0].astype(np.float64))
+    assert ritz.size == 10
+    assert np.max(np.abs(ritz - ref)) <= 1e-5 * np.abs(ref).max()

@@ -250,6 +250,40 @@ def test_vector_lanczos_band_window_edge(lz, orc, handle, torch_cuda, monkeypatc
     assert np.allclose(q.cpu().numpy(), qo, rtol=1e-9, atol=1e-14)
 
 
+@pytest.mark.parametrize("op,kernel", [("banded", None), ("banded", "row"), ("powerlaw", None),
+                                       ("banded", "win1024")])
+def test_vector_lanczos_f32(lz, orc, handle, torch_cuda, monkeypatch, op, kernel):
+    """fp32 single-vector Lanczos (test_lanczos.cu:355, test_VectorLanczos<float>)
+    against the oracle's fp32 restatement.  Tolerances are fp32-sized: the
+    oracle itself moves alpha by 1.4e-6 (relative to max|alpha|) when b is
+    perturbed by one ulp in every 7th entry, so 2e-5 is ~15x that and ~1e3x
+    below what an indexing error produces."""
+    torch = torch_cuda
+    if kernel:
+        monkeypatch.setenv("LZ_VL_KERNEL", kernel)
+    else:
+        monkeypatch.delenv("LZ_VL_KERNEL", raising=False)
+    if op == "banded":  # half band 4096: the band-window kernel's ring path by default
+        A = lz.gen_banded(200003, 10.0, 4096, seed=1, dtype=np.float32)
+    else:  # wide band: the window kernel's global-gather instantiation / lanes per row
+        A = lz.gen_powerlaw(60001, 10.0, 1.8, 30000, seed=9, dtype=np.float32)
+    m, lc = 10, 84
+    bv = lz.uniform_B(A.n, 1, seed=3, dtype=np.float32)[:, 0].copy()
+    kw = dict(dtype=torch.float32, device="cuda")
+    q, al, be = torch.zeros(m, **kw), torch.zeros(m, **kw), torch.zeros(m, **kw)
+    ws = [torch.empty(A.n, **kw) for _ in range(3)]
+    handle.vector_lanczos(lz.CsrDevice.from_host(A), torch.from_numpy(bv).cuda(), m, lc, q, al, be, *ws)
+    qo, ao, bo = orc.vector_lanczos(A, bv, m, lc)
+    al, be, q = al.cpu().numpy(), be.cpu().numpy(), q.cpu().numpy()
+    assert np.all(np.isfinite(al)) and np.all(np.isfinite(be))
+    assert np.max(np.abs(al - ao)) <= 2e-5 * np.abs(ao).max()
+    assert np.max(np.abs(be - bo)) <= 2e-5 * np.abs(bo).max()
+    assert np.max(np.abs(q - qo)) <= 2e-5 * np.abs(qo).max()
+    r = lz.ritz_values(m, 1, al.astype(np.float64), np.r_[be, 0].astype(np.float64))
+    ro = lz.ritz_values(m, 1, ao.astype(np.float64), np.r_[bo, 0].astype(np.float64))
+    assert np.max(np.abs(r - ro)) <= 1e-5 * np.abs(ro).max()
+
+
 def test_vector_lanczos_golden(lz, handle, torch_cuda, golden):
     torch = torch_cuda
     A = golden_csr(lz, golden, 10)

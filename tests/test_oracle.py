@@ -96,3 +96,22 @@ def test_oracle_fp32_tracks_fp64(lz, orc):
     A32 = lz.CsrHost(A.n, A.row_ptr, A.col, A.val.astype(np.float32))
     _, al32, _ = orc.block_lanczos(A32, B.astype(np.float32), 4, 0)
     assert np.max(np.abs(al32 - al64)) < 1e-3 * np.abs(al64).max()
+
+
+def test_oracle_vector_f32_tracks_f64(lz, orc, golden):
+    """The fp32 single-vector restatement (test_VectorLanczos<float>) follows the
+    fp64 one on the driver's operator to fp32 accuracy, and reproduces the
+    golden fp64 run's Ritz values to 1e-5 relative."""
+    A = golden_csr(lz, golden, 10)
+    bv = lz.rand_B(A.n, 4)[:, 0].copy()
+    m, lc = 10, int(golden["lc"])
+    q, al, be = orc.vector_lanczos(A, bv, m, lc)
+    A32 = lz.CsrHost(A.n, A.row_ptr, A.col, A.val.astype(np.float32))
+    qf, alf, bef = orc.vector_lanczos(A32, bv.astype(np.float32), m, lc)
+    assert alf.dtype == np.float32 and bef.dtype == np.float32
+    assert np.max(np.abs(alf - al)) <= 1e-5 * np.abs(al).max()
+    assert np.max(np.abs(bef - be)) <= 1e-5 * np.abs(be).max()
+    assert np.max(np.abs(qf - q)) <= 1e-5 * np.abs(q).max()
+    r = orc.ritz_values(m, 1, alf.astype(np.float64), np.r_[bef, 0].astype(np.float64))
+    ref = orc.ritz_values(m, 1, golden["N10_vec_m10_alpha"], np.r_[golden["N10_vec_m10_beta"], 0.0])
+    assert np.max(np.abs(r - ref)) <= 1e-5 * np.abs(ref).max()
