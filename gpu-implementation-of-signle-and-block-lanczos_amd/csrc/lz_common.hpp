@@ -59,6 +59,10 @@ __host__ __device__ inline int64_t ceil_div(int64_t a, int64_t b) { return (a + 
 struct lz_handle {
     int device = 0;
     hipStream_t stream = nullptr;
+    // a second stream for one-workgroup kernels that overlap a streaming pass
+    // (the b = 32 sqrtm beside the next SpMM), joined back by events
+    hipStream_t side = nullptr;
+    hipEvent_t ev_fork = nullptr, ev_join = nullptr;
     int n_cu = 256;
     // device workspace: per-workgroup partial b x b sums (double), b x b
     // scratch matrices and a few scalars.

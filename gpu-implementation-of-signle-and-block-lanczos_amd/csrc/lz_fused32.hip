@@ -1,0 +1,194 @@
+// lz_fused32.hip -- the Q-free block-Lanczos dense passes at b = 32, fp32
+// (BASELINE config C5), on v_mfma_f32_32x32x2_f32, gfx950.
+//
+// The iteration is the b = 16 fp64 one of lz_fused.hip / lz_api.hip
+// (methods/block_lanczos.hpp:131-166 reassociated so Q_j = W_j beta_j^-1 is
+// never stored), with the SpMM kept as its own launch: C5's power-law rows need
+// the nnz-split tile kernel and its long-tile queue (lz_spmm.hip), and its
+// random columns make the gather, not the dense work, the bound.  Per step:
+//   SpMM     Y = A W_j                                         (A + 2 n b s)
+//   pass E   Q_j = W_j beta_j^-1 (registers), W' = Y beta_j^-1 - W_{j-1} P1,
+//            slabs of Q_j^T W', row probe of Q_j               (4 n b s)
+//   finish   alpha_j = 0.5 (M + M^T), P2 = beta_j^-1 alpha_j
+//   pass U   W'' = W' - W_j P2, slabs of W''^T W''              (3 n b s)
+//   sqrtm    beta_{j+1}, beta_{j+1}^-1, P1 = beta_j^-1 beta_{j+1}
+// against the reference order's 7 calls (A + 13 n b s).
+//
+// MFMA layout (32x32x2, f32): lane l supplies A[i = l&31][k] and B[k][j = l&31]
+// at its k (k = 16(l>>5) + s at step s: a lane's A operands are 64 contiguous
+// bytes of one row, four 16-B loads); register v of the result holds row
+// (v&3) + 8(v>>2) + 4(l>>5), column l&31 of the 32 x 32 tile.  That result
+// layout is also both operand layouts of a product contracted over the tile's
+// rows (step v: k = (v&3) + 8(v>>2) + 4(l>>5)), so the Gram slabs take the
+// result registers as they are, with no transpose.
+#include "lz_common.hpp"
+#include "lz_internal.hpp"
+#include "lz_kernels.hpp"
+
+namespace lz {
+
+typedef float f16v_t __attribute__((ext_vector_type(16)));
+
+__device__ __forceinline__ f16v_t mfma32(float a, float b, f16v_t c)
+{
+    return __builtin_amdgcn_mfma_f32_32x32x2f32(a, b, c, 0, 0, 0);
+}
+
+// a[s] = M[row][16 hh + s] for s = 0..15 (zeros past n): four 16-B loads
+__device__ __forceinline__ void aop32(const float *__restrict__ M, int64_t row, bool ok, int hh, float a[16])
+{
+#pragma unroll
+    for (int c = 0; c < 4; ++c) {
+        float4 x = make_float4(0.f, 0.f, 0.f, 0.f);
+        if (ok) x = *reinterpret_cast<const float4 *>(M + row * 32 + 16 * hh + 4 * c);
+        a[4 * c] = x.x; a[4 * c + 1] = x.y; a[4 * c + 2] = x.z; a[4 * c + 3] = x.w;
+    }
+}
+
+// B operand table of a 32 x 32 row-major matrix S in the permuted contraction
+// order: b[s] = sc * S[16 hh + s][jr]
+__device__ __forceinline__ void bop32(const float *__restrict__ S, float sc, int hh, int jr, float b[16])
+{
+#pragma unroll
+    for (int s = 0; s < 16; ++s) b[s] = sc * S[(16 * hh + s) * 32 + jr];
+}
+
+// the block's waves' 32 x 32 Gram accumulators summed in wave order (double)
+// into its slab part[blockIdx.x]
+template <int NW>
+__device__ __forceinline__ void block_slab32(double (*red)[1024], const f16v_t &g, int lane, int w,
+                                             double *__restrict__ part)
+{
+#pragma unroll
+    for (int v = 0; v < 16; ++v) red[w][((v & 3) + 8 * (v >> 2) + 4 * (lane >> 5)) * 32 + (lane & 31)] = (double)g[v];
+    __syncthreads();
+    for (int e = threadIdx.x; e < 1024; e += 64 * NW) {
+        double s = 0.0;
+#pragma unroll
+        for (int ww = 0; ww < NW; ++ww) s += red[ww][e];
+        part[(int64_t)blockIdx.x * 1024 + e] = s;
+    }
+}
+
+constexpr int kF32Waves = 4;  // 4 waves x 32 rows per unit
+
+// Pass E.  Wprev may alias Wn (row r is read into registers before the same
+// wave stores it); P1 == nullptr at j = 0.
+__global__ __launch_bounds__(64 * kF32Waves) void k_fused_e32(int64_t n, const float *__restrict__ Y,
+                                                              const float *__restrict__ Wj, const float *Wprev,
+                                                              float *Wn, const float *__restrict__ binv,
+                                                              const float *__restrict__ P1, int64_t lc,
+                                                              float *__restrict__ qrow, double *__restrict__ part)
+{
+    __shared__ double red[kF32Waves][1024];
+    const int lane = threadIdx.x & 63, w = threadIdx.x >> 6, hh = lane >> 5, jr = lane & 31;
+    const bool has_prev = P1 != nullptr;
+    float bo[16], po[16];
+    bop32(binv, 1.0f, hh, jr, bo);
+    if (has_prev) bop32(P1, -1.0f, hh, jr, po);
+    f16v_t slab;
+#pragma unroll
+    for (int v = 0; v < 16; ++v) slab[v] = 0.0f;
+    XcdSched sch(ceil_div(n, (int64_t)(32 * kF32Waves)));
+    for (int64_t u = sch.begin; u < sch.end; u += sch.step) {
+        const int64_t r0 = u * (32 * kF32Waves) + 32 * w;
+        const int64_t row = r0 + jr;
+        const bool ok = row < n;
+        float wa[16], ya[16], pa[16];
+        aop32(Wj, row, ok, hh, wa);
+        aop32(Y, row, ok, hh, ya);
+        if (has_prev) aop32(Wprev, row, ok, hh, pa);
+        f16v_t q, wn;
+#pragma unroll
+        for (int v = 0; v < 16; ++v) q[v] = wn[v] = 0.0f;
+#pragma unroll
+        for (int s = 0; s < 16; ++s) q = mfma32(wa[s], bo[s], q);     // Q_j = W_j beta^-1
+#pragma unroll
+        for (int s = 0; s < 16; ++s) wn = mfma32(ya[s], bo[s], wn);   // Y beta^-1
+        if (has_prev) {
+#pragma unroll
+            for (int s = 0; s < 16; ++s) wn = mfma32(pa[s], po[s], wn);  // - W_{j-1} P1
+        }
+#pragma unroll
+        for (int v = 0; v < 16; ++v) {
+            const int64_t rr = r0 + (v & 3) + 8 * (v >> 2) + 4 * hh;
+            if (rr < n) {
+                Wn[rr * 32 + jr] = wn[v];
+                if (rr == lc) qrow[jr] = q[v];
+            }
+        }
+#pragma unroll
+        for (int v = 0; v < 16; ++v) slab = mfma32(q[v], wn[v], slab);  // Q_j^T W' (rows past n: 0)
+    }
+    block_slab32<kF32Waves>(red, slab, lane, w, part);
+}
+
+// Pass U: Wn <- Wn - Wj P2, slabs of Wn^T Wn.
+__global__ __launch_bounds__(64 * kF32Waves) void k_fused_u32(int64_t n, float *__restrict__ Wn,
+                                                              const float *__restrict__ Wj,
+                                                              const float *__restrict__ P2,
+                                                              double *__restrict__ part)
+{
+    __shared__ double red[kF32Waves][1024];
+    const int lane = threadIdx.x & 63, w = threadIdx.x >> 6, hh = lane >> 5, jr = lane & 31;
+    float bo[16];
+    bop32(P2, -1.0f, hh, jr, bo);
+    f16v_t g;
+#pragma unroll
+    for (int v = 0; v < 16; ++v) g[v] = 0.0f;
+    XcdSched sch(ceil_div(n, (int64_t)(32 * kF32Waves)));
+    for (int64_t u = sch.begin; u < sch.end; u += sch.step) {
+        const int64_t r0 = u * (32 * kF32Waves) + 32 * w;
+        float wa[16];
+        aop32(Wj, r0 + jr, r0 + jr < n, hh, wa);
+        f16v_t acc;  // W' in result layout: two 128-B rows per load instruction
+#pragma unroll
+        for (int v = 0; v < 16; ++v) {
+            const int64_t rr = r0 + (v & 3) + 8 * (v >> 2) + 4 * hh;
+            acc[v] = rr < n ? Wn[rr * 32 + jr] : 0.0f;
+        }
+#pragma unroll
+        for (int s = 0; s < 16; ++s) acc = mfma32(wa[s], bo[s], acc);
+#pragma unroll
+        for (int v = 0; v < 16; ++v) {
+            const int64_t rr = r0 + (v & 3) + 8 * (v >> 2) + 4 * hh;
+            if (rr < n) Wn[rr * 32 + jr] = acc[v];
+        }
+#pragma unroll
+        for (int v = 0; v < 16; ++v) g = mfma32(acc[v], acc[v], g);
+    }
+    block_slab32<kF32Waves>(red, g, lane, w, part);
+}
+
+static int f32_grid(lz_handle *h, int64_t n)
+{
+    return (int)std::max<int64_t>(1, std::min<int64_t>(ceil_div(n, (int64_t)(32 * kF32Waves)), (int64_t)h->n_cu * 2));
+}
+
+int fused_e32(lz_handle *h, int64_t n, const float *Y, const float *Wj, const float *Wprev, float *Wn,
+              const float *binv, const float *P1, int64_t lc, float *qrow, int *nparts)
+{
+    const int grid = f32_grid(h, n);
+    LZ_TRY(ensure_partials(h, (size_t)grid * 1024));
+    const int ev = prof_begin(h, PROF_SPMM_PASS);
+    hipLaunchKernelGGL(k_fused_e32, dim3(grid), dim3(64 * kF32Waves), 0, h->stream, n, Y, Wj, Wprev, Wn, binv, P1,
+                       lc, qrow, h->partials);
+    prof_end(h, ev);
+    LZ_LAUNCH_CHECK();
+    *nparts = grid;
+    return LZ_OK;
+}
+
+int fused_u32(lz_handle *h, int64_t n, float *Wn, const float *Wj, const float *P2, int *nparts)
+{
+    const int grid = f32_grid(h, n);
+    LZ_TRY(ensure_partials(h, (size_t)grid * 1024));
+    const int ev = prof_begin(h, PROF_UPDATE_PASS);
+    hipLaunchKernelGGL(k_fused_u32, dim3(grid), dim3(64 * kF32Waves), 0, h->stream, n, Wn, Wj, P2, h->partials);
+    prof_end(h, ev);
+    LZ_LAUNCH_CHECK();
+    *nparts = grid;
+    return LZ_OK;
+}
+
+}  // namespace lz

@@ -61,6 +61,15 @@ int fused_update16(lz_handle *h, int64_t n, double *Wn, const double *Wcur, cons
 // C = A*B, 16 x 16 row-major fp64, on the stream
 int mm16(lz_handle *h, const double *A, const double *B, double *C);
 
+// ---- Q-free dense passes, b = 32 fp32 (lz_fused32.hip), around a separate SpMM Y = A W_j
+// pass E: Q_j = Wj binv (registers); Wn = Y binv - Wprev P1 (P1 == null: no
+// Wprev term); slabs (32 x 32 doubles, one per block, *nparts <= 2 n_cu) of
+// Q_j^T Wn in h->partials; row probe.  Wprev may alias Wn.
+int fused_e32(lz_handle *h, int64_t n, const float *Y, const float *Wj, const float *Wprev, float *Wn,
+              const float *binv, const float *P1, int64_t lc, float *qrow, int *nparts);
+// pass U: Wn <- Wn - Wj P2; slabs of Wn^T Wn
+int fused_u32(lz_handle *h, int64_t n, float *Wn, const float *Wj, const float *P2, int *nparts);
+
 // fp64 scalar helpers for the vector Lanczos (lz_fused.hip)
 template <typename T>
 int vector_lanczos_dev(lz_handle *h, int64_t n, int64_t nnz, const int64_t *rp, const int32_t *col,

@@ -124,15 +124,29 @@ def _f32_checks(lz, m, b, got, ref, rtol):
 F32_RTOL = 1e-4
 
 
-@pytest.mark.parametrize("n,cap,m", [(20000, 2000, 4), (1_000_003, 100_000, 4)])
-def test_block_f32_b32_powerlaw(lz, orc, handle, torch_cuda, n, cap, m):
+@pytest.mark.parametrize("fused", [True, False])
+@pytest.mark.parametrize("n,cap,m", [(20000, 2000, 4), (1_000_003, 100_000, 4), (20011, 2000, 8)])
+def test_block_f32_b32_powerlaw(lz, orc, handle, torch_cuda, n, cap, m, fused):
     """C5 shape: fp32, b = 32, power-law rows (load imbalance); at n = 1M with
     rows up to 1e5 the long-tile queue of the SpMM runs.  alpha, beta, the row
-    probe q and the Ritz values against the fp32 oracle."""
+    probe q and the Ritz values against the fp32 oracle; the Q-free fused
+    passes (lz_fused32.hip) and the reference op order."""
     A = lz.gen_powerlaw(n, 10.0, 2.1, cap, seed=5, dtype=np.float32)
     B = lz.uniform_B(A.n, 32, seed=6, dtype=np.float32)
     lc = 17
-    got = gpu_block(lz, handle, torch_cuda, A, B, m, lc)
+    got = gpu_block(lz, handle, torch_cuda, A, B, m, lc, fused=fused)
+    _f32_checks(lz, m, 32, got, orc.block_lanczos(A, B, m, lc), F32_RTOL)
+    assert handle.device_error() == 0
+
+
+@pytest.mark.parametrize("n,lc,m", [(33, 32, 1), (127, 100, 3), (4099, 4098, 5), (300_007, 300_000, 5)])
+def test_block_f32_b32_fused_shapes(lz, orc, handle, torch_cuda, n, lc, m):
+    """The b = 32 fp32 Q-free passes at ragged sizes: fewer rows than one 32-row
+    tile or one 128-row unit, the row probe in the last partial tile, a banded
+    operator (C3 generator) in fp32.  m b <= n keeps the Krylov block full rank."""
+    A = lz.gen_banded(n, 10.0, 300, seed=n, dtype=np.float32)
+    B = lz.uniform_B(A.n, 32, seed=7, dtype=np.float32)
+    got = gpu_block(lz, handle, torch_cuda, A, B, m, lc, fused=True)
     _f32_checks(lz, m, 32, got, orc.block_lanczos(A, B, m, lc), F32_RTOL)
     assert handle.device_error() == 0
 
