@@ -1,4 +1,4 @@
-"""Multi-GPU decomposition on CPU: world_size 2 over gloo.
+"""Multi-GPU decomposition on CPU: world_size 2-4 over gloo.
 
 lz_block_lanczos_dist (csrc/lz_api.hip) runs, per rank: all-gather of the
 residual slab into a padded full block, the fused pass on the rank's rows with
@@ -96,11 +96,13 @@ def _worker(rank, world, port, n, b, m, hw, seed):
         dist.destroy_process_group()
 
 
-@pytest.mark.parametrize("b", [4, 16])
-def test_row_partitioned_block_lanczos_gloo(b):
+@pytest.mark.parametrize("world,b,hw", [(2, 4, 300), (2, 16, 300), (4, 16, 900)])
+def test_row_partitioned_block_lanczos_gloo(world, b, hw):
+    """All-gather form at 2 and 4 ranks (4 ranks: uneven nnz-balanced slabs,
+    every slab padded, halos reaching past the neighbouring rank)."""
     import torch.multiprocessing as mp
 
-    mp.spawn(_worker, args=(2, _free_port(), 3001, b, 6, 300, 77), nprocs=2, join=True)
+    mp.spawn(_worker, args=(world, _free_port(), 3001, b, 6, hw, 77), nprocs=world, join=True)
 
 
 def _halo_worker(rank, world, port, n, b, m, hw, seed):
