@@ -7,7 +7,8 @@ namespace lz {
 // ---- sparse (lz_spmm.hip)
 template <typename T>
 int spmm_rm(lz_handle *h, int64_t n, int64_t nnz, const int64_t *rp, const int32_t *col, const T *val, int b,
-            const T *X, int64_t ldx, int64_t nx, T *Y, int64_t ldy);  // nx: rows of X
+            const T *X, int64_t ldx, int64_t nx, T *Y, int64_t ldy,
+            bool ycm = false);  // nx: rows of X; ycm: Y column-major (leading dimension ldy), b >= 2
 template <typename T>
 int spmm_cm(lz_handle *h, int64_t n, int64_t nnz, const int64_t *rp, const int32_t *col, const T *val, int b,
             const T *X, int64_t ldx, int64_t nx, T *Y, int64_t ldy);  // nx: rows of X

@@ -28,6 +28,37 @@ struct SpmmShape {
     static constexpr int RB = 256 / LPR; // rows per workgroup pass
 };
 
+// Store a finished nr x b Y tile (element (r, c) = get(r, c), in LDS) into a
+// column-major Y (element (r, c) at r + c*ldy): nr contiguous elements per
+// column, 16 B per lane where Y + r0 + c*ldy is 16-B aligned for every column
+// (ldy and r0 multiples of 16 B / sizeof(T), Y aligned), else one element per lane.
+template <typename T, typename Get>
+__device__ __forceinline__ void store_tile_cm(T *__restrict__ Y, int64_t r0, int nr, int b, int64_t ldy, Get get)
+{
+    constexpr int EPV = 16 / (int)sizeof(T);
+    const bool vec = ((reinterpret_cast<uintptr_t>(Y) & 15) == 0) && (ldy % EPV == 0) && (r0 % EPV == 0);
+    if (vec) {
+        const int nq = (nr + EPV - 1) / EPV;
+        for (int idx = threadIdx.x; idx < b * nq; idx += blockDim.x) {
+            const int c = idx / nq, r = (idx - c * nq) * EPV;
+            T *dst = Y + r0 + r + (int64_t)c * ldy;
+            if (r + EPV <= nr) {
+                Vec<T, EPV> v;
+#pragma unroll
+                for (int e = 0; e < EPV; ++e) v.v[e] = get(r + e, c);
+                stv<T, EPV>(dst, v);
+            } else {
+                for (int e = 0; r + e < nr; ++e) dst[e] = get(r + e, c);
+            }
+        }
+    } else {
+        for (int idx = threadIdx.x; idx < b * nr; idx += blockDim.x) {
+            const int c = idx / nr, r = idx - c * nr;
+            Y[(r0 + r) + (int64_t)c * ldy] = get(r, c);
+        }
+    }
+}
+
 // Tile-per-block SpMM (fallback for X >= 2 GiB or n >= 2^24).  A block owns a tile of
 // RB*RPG consecutive rows; group gi (LPR lanes) owns rows gi + RB*j, j < RPG.
 // The block stages the tile's (col, val) range into LDS with coalesced loads
@@ -36,7 +67,7 @@ struct SpmmShape {
 // per lane in flight), reading (col, val) from LDS.  One tile per block with
 // the XCD remap keeps each XCD's in-flight tiles contiguous (L2-resident X
 // window).  Tiles with more than CAP nnz are staged in CAP-sized chunks.
-template <typename T, int B, int CAP, int RPG>
+template <typename T, int B, int CAP, int RPG, bool YCM = false>
 __global__ __launch_bounds__(256) void k_spmm_lds(int64_t n, const int64_t *__restrict__ rp,
                                                   const int32_t *__restrict__ col,
                                                   const T *__restrict__ val,
@@ -45,7 +76,7 @@ __global__ __launch_bounds__(256) void k_spmm_lds(int64_t n, const int64_t *__re
 {
     using S = SpmmShape<T, B>;
     constexpr int VEC = S::VEC, LPR = S::LPR, RB = S::RB, UNR = 8, TR = RB * RPG;
-    __shared__ int32_t cs[CAP];
+    __shared__ __align__(16) int32_t cs[CAP];
     __shared__ T vs[CAP];
     const int tid = threadIdx.x;
     const int gi = tid / LPR, p = tid % LPR;
@@ -98,6 +129,26 @@ __global__ __launch_bounds__(256) void k_spmm_lds(int64_t n, const int64_t *__re
             }
         }
     }
+    if constexpr (YCM) {  // column-major Y: the tile through LDS (over the staged run, so
+                          // the kernel's LDS and occupancy stay as they are), TR
+                          // contiguous elements per column
+        constexpr bool ALIAS = sizeof(T) * B * (TR + 1) <= sizeof(int32_t) * CAP;
+        T(*yt)[TR + 1];
+        if constexpr (ALIAS) {
+            __syncthreads();  // every wave is done with cs
+            yt = reinterpret_cast<T(*)[TR + 1]>(cs);
+        } else {
+            __shared__ T ytb[B][TR + 1];
+            yt = ytb;
+        }
+#pragma unroll
+        for (int j = 0; j < RPG; ++j)
+#pragma unroll
+            for (int i = 0; i < VEC; ++i) yt[p * VEC + i][gi + RB * j] = acc[j][i];
+        __syncthreads();
+        store_tile_cm<T>(Y, r0, (int)(rend - r0), B, ldy, [&](int r, int c) { return yt[c][r]; });
+        return;
+    }
 #pragma unroll
     for (int j = 0; j < RPG; ++j) {
         const int64_t row = r0 + gi + RB * j;
@@ -141,7 +192,7 @@ __device__ __forceinline__ Vec<T, VEC> ldbuf(__amdgpu_buffer_rsrc_t r, uint32_t 
     return v;
 }
 
-template <typename T, int B, int CAP, int RPG, int UNR = 8>
+template <typename T, int B, int CAP, int RPG, int UNR = 8, bool YCM = false>
 __global__ __launch_bounds__(256) void k_spmm_buf(int64_t n, const int64_t *__restrict__ rp,
                                                   const int32_t *__restrict__ col,
                                                   const T *__restrict__ val,
@@ -265,6 +316,16 @@ __global__ __launch_bounds__(256) void k_spmm_buf(int64_t n, const int64_t *__re
             }
         }
     }
+    if constexpr (YCM) {  // column-major Y: the tile through LDS, TR contiguous elements per column
+        __shared__ T yt[B][TR + 1];
+#pragma unroll
+        for (int j = 0; j < RPG; ++j)
+#pragma unroll
+            for (int i = 0; i < VEC; ++i) yt[p * VEC + i][gi + RB * j] = acc[j][i];
+        __syncthreads();
+        store_tile_cm<T>(Y, r0, (int)(rend - r0), B, ldy, [&](int r, int c) { return yt[c][r]; });
+        return;
+    }
 #pragma unroll
     for (int j = 0; j < RPG; ++j) {
         const int64_t row = r0 + gi + RB * j;
@@ -295,7 +356,10 @@ __global__ __launch_bounds__(256) void k_spmm_buf(int64_t n, const int64_t *__re
 // window goes to the long-tile queue, whose kernel then gathers with 64-bit
 // addresses.  Banded operators of any size keep the buffer-addressed gather
 // (BASELINE config C4: 40M rows on one GPU).
-template <typename T, int B, int TR, int CAP, bool WIN, int MODE>
+// YCM: Y is column-major (element (r, c) at r + c*ldy, the reference's
+// Dense_matrix layout): the finished Y tile leaves column by column, nrows
+// contiguous elements per column (the caller transposed X in).
+template <typename T, int B, int TR, int CAP, bool WIN, int MODE, bool YCM = false>
 __global__ __launch_bounds__(256) void k_spmm_seg(int64_t n, const int64_t *__restrict__ rp,
                                                   const int32_t *__restrict__ col,
                                                   const T *__restrict__ val,
@@ -424,8 +488,12 @@ __global__ __launch_bounds__(256) void k_spmm_seg(int64_t n, const int64_t *__re
                 }
             }
             __syncthreads();
-            for (int idx = tid; idx < nrows * LPR; idx += 256)
-                stv<T, VEC>(Y + (r0 + idx / LPR) * ldy + (idx % LPR) * VEC, yt[idx / LPR][idx % LPR]);
+            if constexpr (YCM) {
+                store_tile_cm<T>(Y, r0, nrows, B, ldy, [&](int r, int c) { return yt[r][c / VEC].v[c % VEC]; });
+            } else {
+                for (int idx = tid; idx < nrows * LPR; idx += 256)
+                    stv<T, VEC>(Y + (r0 + idx / LPR) * ldy + (idx % LPR) * VEC, yt[idx / LPR][idx % LPR]);
+            }
         }
         return;
     } else {
@@ -601,6 +669,10 @@ __global__ __launch_bounds__(256) void k_spmm_seg(int64_t n, const int64_t *__re
         yt[r][p] = sum;
     }
     __syncthreads();
+    if constexpr (YCM) {
+        store_tile_cm<T>(Y, r0, nrows, B, ldy, [&](int r, int c) { return yt[r][c / VEC].v[c % VEC]; });
+        return;
+    }
     for (int idx = tid; idx < nrows * LPR; idx += 256) {
         T *dst = Y + (r0 + idx / LPR) * ldy + (idx % LPR) * VEC;
         if constexpr (sizeof(T) * VEC == 16) {
@@ -666,7 +738,7 @@ __global__ __launch_bounds__(256) void k_spmv(int64_t n, const int64_t *__restri
 
 // nnz-split SpMM with the long-tile queue: the main kernel, then a persistent
 // kernel over the queued tiles (an empty queue costs one short launch).
-template <typename T, int B, int TR, int CAP, bool WIN>
+template <typename T, int B, int TR, int CAP, bool WIN, bool YCM = false>
 static int launch_seg(lz_handle *h, int64_t n, const int64_t *rp, const int32_t *col, const T *val, const T *X,
                       int64_t ldx, int64_t nx, T *Y, int64_t ldy)
 {
@@ -680,10 +752,10 @@ static int launch_seg(lz_handle *h, int64_t n, const int64_t *rp, const int32_t 
         h->longq_cap = (size_t)st + 1;
     }
     LZ_HIP_TRY(hipMemsetAsync(h->longq, 0, sizeof(int), h->stream));
-    hipLaunchKernelGGL((k_spmm_seg<T, B, TR, CAP, WIN, 0>), dim3((unsigned)st), dim3(256), 0, h->stream, n, rp, col,
+    hipLaunchKernelGGL((k_spmm_seg<T, B, TR, CAP, WIN, 0, YCM>), dim3((unsigned)st), dim3(256), 0, h->stream, n, rp, col,
                        val, X, ldx, nx, Y, ldy, h->longq);
     const int g2 = (int)std::max<int64_t>(1, std::min<int64_t>(st, (int64_t)h->n_cu * 4));
-    hipLaunchKernelGGL((k_spmm_seg<T, B, TR, CAP, WIN, 1>), dim3(g2), dim3(256), 0, h->stream, n, rp, col, val, X,
+    hipLaunchKernelGGL((k_spmm_seg<T, B, TR, CAP, WIN, 1, YCM>), dim3(g2), dim3(256), 0, h->stream, n, rp, col, val, X,
                        ldx, nx, Y, ldy, h->longq);
     return LZ_OK;
 }
@@ -693,9 +765,10 @@ static int launch_seg(lz_handle *h, int64_t n, const int64_t *rp, const int32_t 
 // C3) or 1536 entries (C4: 25 nnz/row), windowed past 2^24 rows / 2 GiB of X.
 // Other shapes: the row-per-group k_spmm_buf, or the 64-bit k_spmm_lds past
 // 2 GiB / 2^24 rows.
+// ycm (128-B rows only): Y column-major with leading dimension ldy.
 template <typename T, int B>
 static int launch_spmm_rm(lz_handle *h, int64_t n, int64_t nnz, const int64_t *rp, const int32_t *col,
-                          const T *val, const T *X, int64_t ldx, int64_t nx, T *Y, int64_t ldy)
+                          const T *val, const T *X, int64_t ldx, int64_t nx, T *Y, int64_t ldy, bool ycm = false)
 {
     using S = SpmmShape<T, B>;
     if (n <= 0) return LZ_OK;
@@ -705,7 +778,12 @@ static int launch_spmm_rm(lz_handle *h, int64_t n, int64_t nnz, const int64_t *r
     int rc = LZ_OK;
     if constexpr (S::LPR == 8) {
         const bool wide = (double)nnz > 13.0 * (double)n;
-        if (buf_ok && !wide) rc = launch_seg<T, B, 48, 768, false>(h, n, rp, col, val, X, ldx, nx, Y, ldy);
+        if (ycm) {
+            if (buf_ok && !wide) rc = launch_seg<T, B, 48, 768, false, true>(h, n, rp, col, val, X, ldx, nx, Y, ldy);
+            else if (buf_ok) rc = launch_seg<T, B, 48, 1536, false, true>(h, n, rp, col, val, X, ldx, nx, Y, ldy);
+            else if (!wide) rc = launch_seg<T, B, 48, 768, true, true>(h, n, rp, col, val, X, ldx, nx, Y, ldy);
+            else rc = launch_seg<T, B, 48, 1536, true, true>(h, n, rp, col, val, X, ldx, nx, Y, ldy);
+        } else if (buf_ok && !wide) rc = launch_seg<T, B, 48, 768, false>(h, n, rp, col, val, X, ldx, nx, Y, ldy);
         else if (buf_ok) rc = launch_seg<T, B, 48, 1536, false>(h, n, rp, col, val, X, ldx, nx, Y, ldy);
         else if (!wide) rc = launch_seg<T, B, 48, 768, true>(h, n, rp, col, val, X, ldx, nx, Y, ldy);
         else rc = launch_seg<T, B, 48, 1536, true>(h, n, rp, col, val, X, ldx, nx, Y, ldy);
@@ -714,7 +792,13 @@ static int launch_spmm_rm(lz_handle *h, int64_t n, int64_t nnz, const int64_t *r
         LZ_ARG_CHECK(tiles < (1LL << 31), "too many row tiles");
         constexpr int CAP = S::RB * 32 < 1024 ? 1024 : (S::RB * 32 > 4096 ? 4096 : S::RB * 32);
         constexpr int CAP2 = CAP * 2 < 4096 ? CAP * 2 : 4096;
-        if (buf_ok)
+        if (ycm && buf_ok)
+            hipLaunchKernelGGL((k_spmm_buf<T, B, 1024, 2, 8, true>), dim3((unsigned)tiles), dim3(256), 0, h->stream, n,
+                               rp, col, val, X, ldx, nx, Y, ldy);
+        else if (ycm)
+            hipLaunchKernelGGL((k_spmm_lds<T, B, CAP2, 2, true>), dim3((unsigned)tiles), dim3(256), 0, h->stream, n,
+                               rp, col, val, X, ldx, nx, Y, ldy);
+        else if (buf_ok)
             hipLaunchKernelGGL((k_spmm_buf<T, B, 1024, 2>), dim3((unsigned)tiles), dim3(256), 0, h->stream, n, rp,
                                col, val, X, ldx, nx, Y, ldy);
         else
@@ -729,58 +813,69 @@ static int launch_spmm_rm(lz_handle *h, int64_t n, int64_t nnz, const int64_t *r
 
 template <typename T>
 int spmm_rm(lz_handle *h, int64_t n, int64_t nnz, const int64_t *rp, const int32_t *col, const T *val, int b,
-            const T *X, int64_t ldx, int64_t nx, T *Y, int64_t ldy)
+            const T *X, int64_t ldx, int64_t nx, T *Y, int64_t ldy, bool ycm)
 {
+    LZ_ARG_CHECK(!(ycm && b == 1), "column-major Y store: b >= 2");
     switch (b) {
     case 1:
         LZ_ARG_CHECK(ldx == 1 && ldy == 1, "b = 1 row-major needs ldx = ldy = 1");
         return spmv<T>(h, n, rp, col, val, X, Y, nnz);
-    case 2: return launch_spmm_rm<T, 2>(h, n, nnz, rp, col, val, X, ldx, nx, Y, ldy);
-    case 4: return launch_spmm_rm<T, 4>(h, n, nnz, rp, col, val, X, ldx, nx, Y, ldy);
-    case 8: return launch_spmm_rm<T, 8>(h, n, nnz, rp, col, val, X, ldx, nx, Y, ldy);
-    case 16: return launch_spmm_rm<T, 16>(h, n, nnz, rp, col, val, X, ldx, nx, Y, ldy);
-    case 32: return launch_spmm_rm<T, 32>(h, n, nnz, rp, col, val, X, ldx, nx, Y, ldy);
-    case 64: return launch_spmm_rm<T, 64>(h, n, nnz, rp, col, val, X, ldx, nx, Y, ldy);
+    case 2: return launch_spmm_rm<T, 2>(h, n, nnz, rp, col, val, X, ldx, nx, Y, ldy, ycm);
+    case 4: return launch_spmm_rm<T, 4>(h, n, nnz, rp, col, val, X, ldx, nx, Y, ldy, ycm);
+    case 8: return launch_spmm_rm<T, 8>(h, n, nnz, rp, col, val, X, ldx, nx, Y, ldy, ycm);
+    case 16: return launch_spmm_rm<T, 16>(h, n, nnz, rp, col, val, X, ldx, nx, Y, ldy, ycm);
+    case 32: return launch_spmm_rm<T, 32>(h, n, nnz, rp, col, val, X, ldx, nx, Y, ldy, ycm);
+    case 64: return launch_spmm_rm<T, 64>(h, n, nnz, rp, col, val, X, ldx, nx, Y, ldy, ycm);
     default:
         set_error("row-major SpMM supports b in {1,2,4,8,16,32,64}, got %d", b);
         return LZ_E_ARG;
     }
 }
 
-// Layout change between a column-major block (b columns, leading dimension
-// ld) and a row-major one (ld = b), kCmRows rows per workgroup through LDS:
-// both the column reads and the row writes are coalesced.  IN: col -> row
-// (src = column-major, ld = its leading dimension); !IN: row -> col.
+// Column-major block (b columns, leading dimension ld) -> row-major (ld = b),
+// kCmRows rows per workgroup through LDS: the column reads and the row writes
+// are both coalesced.
 constexpr int kCmRows = 128;
 
-template <typename T, bool IN>
+template <typename T>
 __global__ __launch_bounds__(256) void k_cm_transpose(int64_t rows, int b, const T *__restrict__ src,
                                                       int64_t ld, T *__restrict__ dst)
 {
+    constexpr int EPV = 16 / (int)sizeof(T);
     extern __shared__ __align__(16) unsigned char cm_lds[];  // b * (kCmRows + 1) elements
     T *tile = reinterpret_cast<T *>(cm_lds);
     const int64_t r0 = (int64_t)blockIdx.x * kCmRows;
     const int nr = (int)(rows - r0 < kCmRows ? rows - r0 : kCmRows);
-    const int tot = nr * b;
-    if constexpr (IN) {
+    // column pieces of EPV rows (16 B) where every column start is 16-B aligned
+    if (((reinterpret_cast<uintptr_t>(src) & 15) == 0) && ld % EPV == 0 && nr == kCmRows) {
+        constexpr int NQ = kCmRows / EPV;
+        for (int i = threadIdx.x; i < NQ * b; i += blockDim.x) {
+            const int c = i / NQ, r = (i - c * NQ) * EPV;
+            const Vec<T, EPV> v = ldv<T, EPV>(src + (int64_t)c * ld + r0 + r);
+#pragma unroll
+            for (int e = 0; e < EPV; ++e) tile[c * (kCmRows + 1) + r + e] = v.v[e];
+        }
+    } else {
         for (int i = threadIdx.x; i < kCmRows * b; i += blockDim.x) {
             const int c = i / kCmRows, r = i % kCmRows;
             if (r < nr) tile[c * (kCmRows + 1) + r] = src[(int64_t)c * ld + r0 + r];
         }
-        __syncthreads();
-        for (int i = threadIdx.x; i < tot; i += blockDim.x) {
-            const int r = i / b, c = i % b;
-            dst[r0 * b + i] = tile[c * (kCmRows + 1) + r];
+    }
+    __syncthreads();
+    // row pieces of EPV columns (b is a power of two >= 2; dst rows are b * sizeof(T) bytes)
+    if (b % EPV == 0) {
+        const int nb = b / EPV;
+        for (int i = threadIdx.x; i < nr * nb; i += blockDim.x) {
+            const int r = i / nb, c = (i - r * nb) * EPV;
+            Vec<T, EPV> v;
+#pragma unroll
+            for (int e = 0; e < EPV; ++e) v.v[e] = tile[(c + e) * (kCmRows + 1) + r];
+            stv<T, EPV>(dst + (r0 + r) * b + c, v);
         }
     } else {
-        for (int i = threadIdx.x; i < tot; i += blockDim.x) {
+        for (int i = threadIdx.x; i < nr * b; i += blockDim.x) {
             const int r = i / b, c = i % b;
-            tile[c * (kCmRows + 1) + r] = src[r0 * b + i];
-        }
-        __syncthreads();
-        for (int i = threadIdx.x; i < kCmRows * b; i += blockDim.x) {
-            const int c = i / kCmRows, r = i % kCmRows;
-            if (r < nr) dst[(int64_t)c * ld + r0 + r] = tile[c * (kCmRows + 1) + r];
+            dst[r0 * b + i] = tile[c * (kCmRows + 1) + r];
         }
     }
 }
@@ -790,13 +885,15 @@ int spmm_cm(lz_handle *h, int64_t n, int64_t nnz, const int64_t *rp, const int32
             const T *X, int64_t ldx, int64_t nx, T *Y, int64_t ldy)
 {
     if (n <= 0) return LZ_OK;
-    // b = 2..64 (powers of two): a column-major gather touches b lines per nonzero, the row-major
-    // kernel one; transposing X in and Y out (read + write of each block once)
-    // costs less (Yee N=160, b=16 fp32: 3.69 ms direct).  LZ_SPMM_CM=direct: the
-    // one-pass kernel.
+    // b = 2..64 (powers of two): a column-major gather touches b lines per
+    // nonzero, the row-major kernel one, so X is transposed in once (read +
+    // write) and the row-major SpMM kernels store their finished Y tiles column
+    // by column themselves (TR contiguous elements per column).  Yee N=160, b=16
+    // fp32: 3.69 ms direct, 2.61 ms with a separate Y transpose pass.
+    // LZ_SPMM_CM=direct: the one-pass kernel.
     const char *cm_env = getenv("LZ_SPMM_CM");  // read per call (tests switch it)
     if (b >= 2 && (b & (b - 1)) == 0 && !(cm_env && cm_env[0] == 'd')) {  // the row-major kernel's b
-        const size_t need = sizeof(T) * (size_t)b * (size_t)(nx + n);
+        const size_t need = sizeof(T) * (size_t)b * (size_t)nx;
         if (need > h->cm_cap) {
             LZ_HIP_TRY(hipStreamSynchronize(h->stream));
             (void)hipFree(h->cm_buf);
@@ -805,16 +902,12 @@ int spmm_cm(lz_handle *h, int64_t n, int64_t nnz, const int64_t *rp, const int32
             LZ_HIP_TRY(hipMalloc(&h->cm_buf, need));
             h->cm_cap = need;
         }
-        T *Xr = static_cast<T *>(h->cm_buf), *Yr = Xr + (size_t)b * nx;
+        T *Xr = static_cast<T *>(h->cm_buf);
         const size_t lds = sizeof(T) * (size_t)b * (kCmRows + 1);
-        hipLaunchKernelGGL((k_cm_transpose<T, true>), dim3((unsigned)ceil_div(nx, (int64_t)kCmRows)), dim3(256), lds,
+        hipLaunchKernelGGL((k_cm_transpose<T>), dim3((unsigned)ceil_div(nx, (int64_t)kCmRows)), dim3(256), lds,
                            h->stream, nx, b, X, ldx, Xr);
         LZ_LAUNCH_CHECK();
-        LZ_TRY(spmm_rm<T>(h, n, nnz, rp, col, val, b, Xr, b, nx, Yr, b));
-        hipLaunchKernelGGL((k_cm_transpose<T, false>), dim3((unsigned)ceil_div(n, (int64_t)kCmRows)), dim3(256), lds,
-                           h->stream, n, b, Yr, ldy, Y);
-        LZ_LAUNCH_CHECK();
-        return LZ_OK;
+        return spmm_rm<T>(h, n, nnz, rp, col, val, b, Xr, b, nx, Y, ldy, true);
     }
     const int grid = (int)std::min<int64_t>(ceil_div(n, 256), (int64_t)h->n_cu * 8);
     if (grid <= 0) return LZ_OK;
@@ -853,9 +946,9 @@ int spmv(lz_handle *h, int64_t n, const int64_t *rp, const int32_t *col, const T
 }
 
 template int spmm_rm<double>(lz_handle *, int64_t, int64_t, const int64_t *, const int32_t *,
-                             const double *, int, const double *, int64_t, int64_t, double *, int64_t);
+                             const double *, int, const double *, int64_t, int64_t, double *, int64_t, bool);
 template int spmm_rm<float>(lz_handle *, int64_t, int64_t, const int64_t *, const int32_t *, const float *,
-                            int, const float *, int64_t, int64_t, float *, int64_t);
+                            int, const float *, int64_t, int64_t, float *, int64_t, bool);
 template int spmm_cm<double>(lz_handle *, int64_t, int64_t, const int64_t *, const int32_t *,
                              const double *, int, const double *, int64_t, int64_t, double *, int64_t);
 template int spmm_cm<float>(lz_handle *, int64_t, int64_t, const int64_t *, const int32_t *, const float *,

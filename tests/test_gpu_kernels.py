@@ -61,11 +61,26 @@ def test_spmm_rowmajor_f32(lz, orc, handle, torch_cuda, b):
     check_spmm(lz, orc, handle, torch_cuda, A, b, np.float32)
 
 
-@pytest.mark.parametrize("b", [1, 4, 5, 16, 32, 64])
+@pytest.mark.parametrize("n", [3001, 3072])
+@pytest.mark.parametrize("b", [1, 2, 4, 5, 16, 32, 64])
 @pytest.mark.parametrize("dtype", [np.float64, np.float32])
-def test_spmm_colmajor(lz, orc, handle, torch_cuda, b, dtype):
-    """Column-major X/Y (b >= 2: transposed in and out around the row-major kernel)."""
-    A = lz.gen_banded(3001, 8.0, 100, seed=9)
+def test_spmm_colmajor(lz, orc, handle, torch_cuda, b, dtype, n):
+    """Column-major X/Y (b >= 2: X transposed in, the row-major kernels store
+    their Y tiles column by column; n = 3072: the 16-B column pieces)."""
+    A = lz.gen_banded(n, 8.0, 100, seed=9)
+    check_spmm(lz, orc, handle, torch_cuda, A, b, dtype, layout="col")
+
+
+@pytest.mark.parametrize("n", [20011, 20016])
+@pytest.mark.parametrize("b,dtype", [(16, np.float64), (32, np.float32)])
+def test_spmm_colmajor_long_tiles(lz, orc, handle, torch_cuda, b, dtype, n):
+    """128-B rows in the column-major layout: the nnz-split kernel stores its Y
+    tile column by column, in both its tile pass and its long-tile pass
+    (power-law rows longer than the 768-entry stage), n not a multiple of the
+    48-row tile."""
+    A = lz.gen_powerlaw(n, 10.0, 1.3, 8000, seed=8, dtype=np.float64)
+    tiles = np.diff(A.row_ptr[np.minimum(np.arange(0, A.n + 48, 48), A.n)])
+    assert (tiles > 768).sum() > 10 and np.diff(A.row_ptr).max() > 768  # long tiles, and a row longer than the stage
     check_spmm(lz, orc, handle, torch_cuda, A, b, dtype, layout="col")
 
 
