@@ -15,9 +15,10 @@ HBM.
   all-gathers the block (`--exchange allgather`); `value` counts
   slab-iterations/s summed over ranks.
 --config c4: BASELINE config C4, strong scaling -- n = 4e7 rows in total,
-  25 nnz/row (nnz = 1e9), half width 2^16, split over the N ranks.  At N > 1
-  the line reports the halo exchange as `value` and the north star's RCCL
-  all-gather form beside it (extra.c4_allgather).
+  25 nnz/row (nnz = 1e9), half width 2^16, split over the N ranks.
+At N > 1 (either config) the line reports the `--exchange` form (halo by
+default) as `value` and times the other form (the north star's RCCL
+all-gather) beside it on the same partition (extra.other_exchange).
 
 After the timed region the run checks itself: the device error word must be
 0 (no persistent kernel abandoned a bounded spin) and, on one GPU, the first
@@ -131,7 +132,7 @@ def parse_args():
     ap.add_argument("--exchange", choices=["halo", "allgather"], default="halo",
                     help="multi-GPU Krylov-block exchange (N > 1, or with --dist at N = 1)")
     ap.add_argument("--no-second-exchange", action="store_true",
-                    help="c4, N > 1: do not time the other exchange form beside the headline one")
+                    help="N > 1: do not time the other exchange form beside the headline one")
     ap.add_argument("--dist", action="store_true",
                     help="run the distributed entry point even at N = 1 (rehearsal of the N > 1 path)")
     args = ap.parse_args()
@@ -274,9 +275,9 @@ def main():
     small_ms, _ = prof[h.PROF_SMALL]
     gram_ms, _ = prof[h.PROF_GRAM]
 
-    # ---- c4, N > 1: the other exchange form on the same partition
+    # ---- N > 1: the other exchange form (halo <-> the north star's all-gather) on the same partition
     other = None
-    if c4 and world > 1 and not args.no_second_exchange:
+    if world > 1 and not args.no_second_exchange:
         ex2 = "allgather" if args.exchange == "halo" else "halo"
         del run, Ad
         torch.cuda.empty_cache()
@@ -496,7 +497,7 @@ def main():
             "mfma": mfma,
             "extra": {
                 "plain_spmm": plain,
-                "c4_other_exchange": other,
+                "other_exchange": other,
                 "c2_vector_lanczos": c2,
                 "c5_block32_f32_powerlaw": c5,
                 "c3_random_columns_stress": c3r,
@@ -510,6 +511,9 @@ def main():
                 "iteration_qfree_bytes": a_bytes + 6 * n * b * 8,
                 "iteration_bytes_note": "min_bytes: SURVEY.md 8(d) convention A + 8nbs (fixed); qfree_bytes: "
                                         "A + 6nbs, what the implemented Q-free iteration moves",
+                # the gather-bound pass's natural unit: nonzeros (one 128-B X row gathered each) per second,
+                # comparable across C3 (10 nnz/row) and C4 (25 nnz/row)
+                "nnz_per_s_per_gpu": round(A.nnz * K / elapsed, 1),
             },
         }
         os.write(json_fd, (json.dumps(out) + "\n").encode())
