@@ -323,11 +323,17 @@ def test_fdtd_block(lz, orc, handle, torch_cuda, golden):
     assert np.allclose(out.cpu().numpy(), orc.fdtd_block(A, B, 2000, 1.0, lc), rtol=1e-12)
 
 
-@pytest.mark.parametrize("n,b,steps", [(3001, 3, 1001), (3001, 16, 513), ((1 << 18) + 1, 4, 3)])
-def test_fdtd_block_shapes(lz, orc, handle, torch_cuda, n, b, steps):
+@pytest.mark.parametrize("n,b,steps,graph", [(3001, 3, 1001, None), (3001, 16, 513, None), (3001, 16, 513, "0"),
+                                             ((1 << 18) + 1, 4, 3, None)])
+def test_fdtd_block_shapes(lz, orc, handle, torch_cuda, monkeypatch, n, b, steps, graph):
     """Odd step counts (final state in the ping-pong buffer), b not a power of
-    two, a graph replay count with eager remainder, and the unfused large-n path."""
+    two, a graph replay count with eager remainder, the eager loop
+    (LZ_FDTD_GRAPH=0, read per call), and the unfused large-n path."""
     torch = torch_cuda
+    if graph is None:
+        monkeypatch.delenv("LZ_FDTD_GRAPH", raising=False)
+    else:
+        monkeypatch.setenv("LZ_FDTD_GRAPH", graph)
     A = lz.gen_banded(n, 6.0, 200, seed=n)
     A = lz.CsrHost(A.n, A.row_ptr, A.col, A.val * 0.05)
     B = lz.uniform_B(n, b, seed=7)
