@@ -197,42 +197,45 @@ static int block_lanczos_fused16(lz_handle *h, int64_t n, int64_t nnz, const int
     return LZ_OK;
 }
 
-// Q-free iteration at b = 32 fp32 (BASELINE config C5; lz_fused32.hip): the
-// b = 16 fp64 scheme above with the SpMM as its own launch (the nnz-split tile
-// kernel + long-tile queue that power-law rows need) writing Y into the API's
-// Q0 buffer, then pass E and pass U.  A + 9 n b s bytes per step against the
-// reference order's A + 13 n b s; the residual buffers rotate as in
-// block_lanczos_fused16 (B = W_0 read only, then W, Q1, in place).
-static int block_lanczos_fused32(lz_handle *h, int64_t n, int64_t nnz, const int64_t *rp, const int32_t *col,
-                                 const float *val, int m, int64_t lc, const float *B, float *q, float *alpha,
-                                 float *beta, float *Q0, float *Q1, float *W)
+// Q-free iteration with the SpMM as its own launch (lz_fused32.hip): b = 32
+// fp32 (BASELINE config C5) on MFMA passes, every other b <= 32 except 16-fp64
+// (e.g. the reference driver's default N_COL = 4) on VALU passes.  The b = 16
+// fp64 scheme above with the SpMM (the nnz-split tile kernel + long-tile queue
+// that power-law rows need) writing Y into the API's Q0 buffer, then pass E
+// and pass U: A + 9 n b s bytes per step against the reference order's
+// A + 13 n b s.  The residual buffers rotate as in block_lanczos_fused16
+// (B = W_0 read only, then W, Q1, in place).
+template <typename T>
+static int block_lanczos_sep(lz_handle *h, int64_t n, int64_t nnz, const int64_t *rp, const int32_t *col,
+                             const T *val, int b, int m, int64_t lc, const T *B, T *q, T *alpha, T *beta, T *Q0,
+                             T *Q1, T *W)
 {
-    constexpr int64_t bb = 1024;
-    float *sc = reinterpret_cast<float *>(h->scratch + 4 * kMaxB * kMaxB);
-    float *binv[2] = {sc, sc + bb}, *P = sc + 2 * bb;
-    float *Y = Q0;
+    const int64_t bb = (int64_t)b * b;
+    T *sc = reinterpret_cast<T *>(h->scratch + 4 * kMaxB * kMaxB);
+    T *binv[2] = {sc, sc + bb}, *P = sc + 2 * bb;
+    T *Y = Q0;
     int np = 0;
-    LZ_TRY(gram_partials<float>(h, n, 32, B, B, 32, &np));
-    LZ_TRY(sqrtm_pair<float>(h, 32, nullptr, np, beta, binv[0], nullptr));
-    const float *in = B, *prev = nullptr;
+    LZ_TRY(gram_partials<T>(h, n, b, B, B, b, &np));
+    LZ_TRY(sqrtm_pair<T>(h, b, nullptr, np, beta, binv[0], nullptr));
+    const T *in = B, *prev = nullptr;
     for (int j = 0; j < m; ++j) {
-        float *out = j == 0 ? W : j == 1 ? Q1 : const_cast<float *>(prev);
-        const float *bi = binv[j & 1];
+        T *out = j == 0 ? W : j == 1 ? Q1 : const_cast<T *>(prev);
+        const T *bi = binv[j & 1];
         // the SpMM gathers the unnormalised W_j: it needs no beta, so step j-1's
         // sqrtm runs beside it on the side stream; pass E waits for it
-        LZ_TRY(spmm_rm<float>(h, n, nnz, rp, col, val, 32, in, 32, n, Y, 32));
+        LZ_TRY(spmm_rm<T>(h, n, nnz, rp, col, val, b, in, b, n, Y, b));
         if (j > 0) LZ_HIP_TRY(hipStreamWaitEvent(h->stream, h->ev_join, 0));
-        LZ_TRY(fused_e32(h, n, Y, in, prev, out, bi, j ? P : nullptr, lc, q + j * 32, &np));
+        LZ_TRY(fused_e_sep<T>(h, n, b, Y, in, prev, out, bi, j ? P : nullptr, lc, q + (int64_t)j * b, &np));
         // alpha_j and P2 = beta_j^-1 alpha_j (this step's P1 is consumed)
-        LZ_TRY(gram_finish<float>(h, 32, np, 1, alpha + j * bb, h->partials, bi, P));
-        LZ_TRY(fused_u32(h, n, out, in, P, &np));
+        LZ_TRY(gram_finish<T>(h, b, np, 1, alpha + j * bb, h->partials, bi, P));
+        LZ_TRY(fused_u_sep<T>(h, n, b, out, in, P, &np));
         if (j + 1 < m) {  // beta_{j+1}, its inverse and P1 = beta_j^-1 beta_{j+1}, on the side stream
             LZ_HIP_TRY(hipEventRecord(h->ev_fork, h->stream));
             LZ_HIP_TRY(hipStreamWaitEvent(h->side, h->ev_fork, 0));
             hipStream_t main = h->stream;
             h->stream = h->side;
-            const int rc = sqrtm_pair<float>(h, 32, nullptr, np, beta + (j + 1) * bb, binv[(j + 1) & 1], nullptr,
-                                             nullptr, bi, P);
+            const int rc = sqrtm_pair<T>(h, b, nullptr, np, beta + (j + 1) * bb, binv[(j + 1) & 1], nullptr, nullptr,
+                                         bi, P);
             h->stream = main;
             LZ_TRY(rc);
             LZ_HIP_TRY(hipEventRecord(h->ev_join, h->side));
@@ -240,8 +243,7 @@ static int block_lanczos_fused32(lz_handle *h, int64_t n, int64_t nnz, const int
         prev = in;
         in = out;
     }
-    LZ_HIP_TRY(hipMemcpyAsync(beta + m * bb, binv[(m - 1) & 1], sizeof(float) * bb, hipMemcpyDeviceToDevice,
-                              h->stream));
+    LZ_HIP_TRY(hipMemcpyAsync(beta + m * bb, binv[(m - 1) & 1], sizeof(T) * bb, hipMemcpyDeviceToDevice, h->stream));
     return LZ_OK;
 }
 
@@ -815,11 +817,12 @@ int lz_block_lanczos(lz_handle *h, int64_t n, int64_t nnz, const int64_t *rp, co
         return block_lanczos_fused16(h, n, nnz, rp, col, (const double *)val, m, lc,
                                      (const double *)B, (double *)q, (double *)alpha,
                                      (double *)beta, (double *)Q0, (double *)Q1, (double *)W);
-    if (dtype == LZ_F32 && b == 32)
-        return block_lanczos_fused32(h, n, nnz, rp, col, (const float *)val, m, lc, (const float *)B, (float *)q,
-                                     (float *)alpha, (float *)beta, (float *)Q0, (float *)Q1, (float *)W);
-    return lz_block_lanczos_unfused(h, n, nnz, rp, col, val, dtype, b, m, lc, B, q, alpha, beta,
-                                    Q0, Q1, W);
+    if (dtype == LZ_F64)
+        return block_lanczos_sep<double>(h, n, nnz, rp, col, (const double *)val, b, m, lc, (const double *)B,
+                                         (double *)q, (double *)alpha, (double *)beta, (double *)Q0, (double *)Q1,
+                                         (double *)W);
+    return block_lanczos_sep<float>(h, n, nnz, rp, col, (const float *)val, b, m, lc, (const float *)B, (float *)q,
+                                    (float *)alpha, (float *)beta, (float *)Q0, (float *)Q1, (float *)W);
 }
 
 int lz_vector_lanczos(lz_handle *h, int64_t n, int64_t nnz, const int64_t *rp, const int32_t *col,

@@ -342,7 +342,8 @@ template <typename T>
 __global__ __launch_bounds__(kRedThreads) void k_sqrtm(int b, const T *__restrict__ Gin,
                                                        const double *__restrict__ part, int P,
                                                        T *__restrict__ beta, T *__restrict__ binv,
-                                                       T *__restrict__ eig)
+                                                       T *__restrict__ eig, const T *__restrict__ L,
+                                                       T *__restrict__ LB)
 {
     constexpr int MB = 32;
     __shared__ double Abuf[2][MB * MB], Vbuf[2][MB * MB];
@@ -436,6 +437,16 @@ __global__ __launch_bounds__(kRedThreads) void k_sqrtm(int b, const T *__restric
         }
         if (beta) beta[e] = (T)s1;
         if (binv) binv[e] = (T)s2;
+        if (L) An[e] = s1;  // An is dead: park beta for LB
+    }
+    if (L) {  // LB = L * beta (the Q-free iteration's P1 = beta_{j-1}^-1 beta_j)
+        __syncthreads();
+        for (int e = tid; e < bb; e += NT) {
+            const int i = e / b, j = e % b;
+            double s = 0.0;
+            for (int k = 0; k < b; ++k) s = fma((double)L[i * b + k], An[k * b + j], s);
+            LB[e] = (T)s;
+        }
     }
     if (eig && tid < b) {
         const double lk = A[tid * b + tid];
@@ -751,7 +762,6 @@ int sqrtm_pair(lz_handle *h, int b, const T *G, int nparts, T *beta, T *beta_inv
                const double *slabs, const T *L, T *LB)
 {
     LZ_ARG_CHECK(b >= 1 && b <= 32, "sqrtm supports b <= 32");
-    LZ_ARG_CHECK(!L || b == 8 || b == 16 || b == 32, "sqrtm_pair L*beta: b in {8, 16, 32}");
     {
     const int ev_ = prof_begin(h, PROF_SMALL);
     const double *sl = slabs ? slabs : h->partials;
@@ -764,7 +774,7 @@ int sqrtm_pair(lz_handle *h, int b, const T *G, int nparts, T *beta, T *beta_inv
         LZ_SQRTM_B(8) LZ_SQRTM_B(16) LZ_SQRTM_B(32)
     default:
         hipLaunchKernelGGL((k_sqrtm<T>), dim3(1), dim3(kRedThreads), 0, h->stream, b, G, sl,
-                           nparts, beta, beta_inv, eig);
+                           nparts, beta, beta_inv, eig, L, LB);
     }
 #undef LZ_SQRTM_B
     prof_end(h, ev_);

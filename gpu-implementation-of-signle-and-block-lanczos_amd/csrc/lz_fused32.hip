@@ -1,5 +1,7 @@
-// lz_fused32.hip -- the Q-free block-Lanczos dense passes at b = 32, fp32
-// (BASELINE config C5), on v_mfma_f32_32x32x2_f32, gfx950.
+// lz_fused32.hip -- the Q-free block-Lanczos dense passes that run around a
+// separate SpMM launch: b = 32 fp32 (BASELINE config C5) on
+// v_mfma_f32_32x32x2_f32, and every other block width b <= 32 (fp64 or fp32,
+// e.g. the reference driver's default N_COL = 4) on the VALU; gfx950.
 //
 // The iteration is the b = 16 fp64 one of lz_fused.hip / lz_api.hip
 // (methods/block_lanczos.hpp:131-166 reassociated so Q_j = W_j beta_j^-1 is
@@ -21,6 +23,7 @@
 // layout is also both operand layouts of a product contracted over the tile's
 // rows (step v: k = (v&3) + 8(v>>2) + 4(l>>5)), so the Gram slabs take the
 // result registers as they are, with no transpose.
+#include <type_traits>
 #include "lz_common.hpp"
 #include "lz_internal.hpp"
 #include "lz_kernels.hpp"
@@ -192,5 +195,158 @@ int fused_u32(lz_handle *h, int64_t n, float *Wn, const float *Wj, const float *
     *nparts = grid;
     return LZ_OK;
 }
+
+// ---------------------------------------------------------------------------
+// Any b <= 32, fp64 or fp32 (VALU): 32-row tiles through LDS in fp64, every
+// product accumulated in fp64 and rounded to T once (the MFMA path rounds in
+// fp32 at b = 32).  Thread t owns slab entries t, t + 256, ... of the b x b slab.
+constexpr int kGenRows = 32;
+
+template <typename T>
+__global__ __launch_bounds__(256) void k_fused_e_gen(int64_t n, int b, const T *__restrict__ Y,
+                                                     const T *__restrict__ Wj, const T *Wprev, T *Wn,
+                                                     const T *__restrict__ binv, const T *__restrict__ P1,
+                                                     int64_t lc, T *__restrict__ qrow, double *__restrict__ part)
+{
+    constexpr int TR = kGenRows, MB = 32;
+    __shared__ double sb[MB * MB], sp[MB * MB], tj[TR * MB], ty[TR * MB], tp[TR * MB], tq[TR * MB], tw[TR * MB];
+    const int t = threadIdx.x, bb = b * b;
+    const bool hp = P1 != nullptr;
+    for (int e = t; e < bb; e += 256) {
+        sb[e] = (double)binv[e];
+        sp[e] = hp ? (double)P1[e] : 0.0;
+    }
+    double acc[4] = {0.0, 0.0, 0.0, 0.0};
+    XcdSched sch(ceil_div(n, (int64_t)TR));
+    for (int64_t u = sch.begin; u < sch.end; u += sch.step) {
+        const int64_t r0 = u * TR;
+        const int nr = (int)(n - r0 < TR ? n - r0 : TR), ne = nr * b;
+        __syncthreads();  // the previous tile's tq / tw reads are done (and sb, sp written)
+        for (int e = t; e < ne; e += 256) {
+            tj[e] = (double)Wj[r0 * b + e];
+            ty[e] = (double)Y[r0 * b + e];
+            tp[e] = hp ? (double)Wprev[r0 * b + e] : 0.0;  // Wprev may be Wn: read before any store
+        }
+        __syncthreads();
+        for (int e = t; e < ne; e += 256) {
+            const int r = e / b, c = e - r * b;
+            double q = 0.0, w = 0.0;
+            for (int k = 0; k < b; ++k) {
+                q = fma(tj[r * b + k], sb[k * b + c], q);
+                w = fma(ty[r * b + k], sb[k * b + c], w);
+            }
+            for (int k = 0; hp && k < b; ++k) w = fma(-tp[r * b + k], sp[k * b + c], w);
+            const T qT = (T)q, wT = (T)w;
+            tq[e] = (double)qT;
+            tw[e] = (double)wT;
+            Wn[r0 * b + e] = wT;
+            if (r0 + r == lc) qrow[c] = qT;
+        }
+        __syncthreads();
+#pragma unroll
+        for (int kk = 0; kk < 4; ++kk) {
+            const int e = t + 256 * kk;
+            if (e < bb) {
+                const int i = e / b, j = e - i * b;
+                for (int r = 0; r < nr; ++r) acc[kk] = fma(tq[r * b + i], tw[r * b + j], acc[kk]);
+            }
+        }
+    }
+#pragma unroll
+    for (int kk = 0; kk < 4; ++kk)
+        if (t + 256 * kk < bb) part[(int64_t)blockIdx.x * bb + t + 256 * kk] = acc[kk];
+}
+
+template <typename T>
+__global__ __launch_bounds__(256) void k_fused_u_gen(int64_t n, int b, T *__restrict__ Wn, const T *__restrict__ Wj,
+                                                     const T *__restrict__ P2, double *__restrict__ part)
+{
+    constexpr int TR = kGenRows, MB = 32;
+    __shared__ double sp[MB * MB], tj[TR * MB], tw[TR * MB];
+    const int t = threadIdx.x, bb = b * b;
+    for (int e = t; e < bb; e += 256) sp[e] = (double)P2[e];
+    double acc[4] = {0.0, 0.0, 0.0, 0.0};
+    XcdSched sch(ceil_div(n, (int64_t)TR));
+    for (int64_t u = sch.begin; u < sch.end; u += sch.step) {
+        const int64_t r0 = u * TR;
+        const int nr = (int)(n - r0 < TR ? n - r0 : TR), ne = nr * b;
+        __syncthreads();
+        for (int e = t; e < ne; e += 256) {
+            tj[e] = (double)Wj[r0 * b + e];
+            tw[e] = (double)Wn[r0 * b + e];
+        }
+        __syncthreads();
+        double v[4];
+#pragma unroll
+        for (int kk = 0; kk < 4; ++kk) {  // W'' = W' - Wj P2 (ne <= 1024 = 4 per thread)
+            const int e = t + 256 * kk;
+            if (e < ne) {
+                const int r = e / b, c = e - r * b;
+                double x = tw[e];
+                for (int k = 0; k < b; ++k) x = fma(-tj[r * b + k], sp[k * b + c], x);
+                const T xT = (T)x;
+                Wn[r0 * b + e] = xT;
+                v[kk] = (double)xT;
+            }
+        }
+        __syncthreads();  // every thread's reads of tw are done
+#pragma unroll
+        for (int kk = 0; kk < 4; ++kk)
+            if (t + 256 * kk < ne) tw[t + 256 * kk] = v[kk];
+        __syncthreads();
+#pragma unroll
+        for (int kk = 0; kk < 4; ++kk) {
+            const int e = t + 256 * kk;
+            if (e < bb) {
+                const int i = e / b, j = e - i * b;
+                for (int r = 0; r < nr; ++r) acc[kk] = fma(tw[r * b + i], tw[r * b + j], acc[kk]);
+            }
+        }
+    }
+#pragma unroll
+    for (int kk = 0; kk < 4; ++kk)
+        if (t + 256 * kk < bb) part[(int64_t)blockIdx.x * bb + t + 256 * kk] = acc[kk];
+}
+
+template <typename T>
+int fused_e_sep(lz_handle *h, int64_t n, int b, const T *Y, const T *Wj, const T *Wprev, T *Wn, const T *binv,
+                const T *P1, int64_t lc, T *qrow, int *nparts)
+{
+    if constexpr (std::is_same<T, float>::value)
+        if (b == 32) return fused_e32(h, n, Y, Wj, Wprev, Wn, binv, P1, lc, qrow, nparts);
+    LZ_ARG_CHECK(b >= 1 && b <= 32, "fused pass E: 1 <= b <= 32");
+    const int grid = (int)std::max<int64_t>(1, std::min<int64_t>(ceil_div(n, (int64_t)kGenRows), (int64_t)h->n_cu * 2));
+    LZ_TRY(ensure_partials(h, (size_t)grid * b * b));
+    const int ev = prof_begin(h, PROF_SPMM_PASS);
+    hipLaunchKernelGGL((k_fused_e_gen<T>), dim3(grid), dim3(256), 0, h->stream, n, b, Y, Wj, Wprev, Wn, binv, P1, lc,
+                       qrow, h->partials);
+    prof_end(h, ev);
+    LZ_LAUNCH_CHECK();
+    *nparts = grid;
+    return LZ_OK;
+}
+
+template <typename T>
+int fused_u_sep(lz_handle *h, int64_t n, int b, T *Wn, const T *Wj, const T *P2, int *nparts)
+{
+    if constexpr (std::is_same<T, float>::value)
+        if (b == 32) return fused_u32(h, n, Wn, Wj, P2, nparts);
+    LZ_ARG_CHECK(b >= 1 && b <= 32, "fused pass U: 1 <= b <= 32");
+    const int grid = (int)std::max<int64_t>(1, std::min<int64_t>(ceil_div(n, (int64_t)kGenRows), (int64_t)h->n_cu * 2));
+    LZ_TRY(ensure_partials(h, (size_t)grid * b * b));
+    const int ev = prof_begin(h, PROF_UPDATE_PASS);
+    hipLaunchKernelGGL((k_fused_u_gen<T>), dim3(grid), dim3(256), 0, h->stream, n, b, Wn, Wj, P2, h->partials);
+    prof_end(h, ev);
+    LZ_LAUNCH_CHECK();
+    *nparts = grid;
+    return LZ_OK;
+}
+
+template int fused_e_sep<double>(lz_handle *, int64_t, int, const double *, const double *, const double *, double *,
+                                 const double *, const double *, int64_t, double *, int *);
+template int fused_e_sep<float>(lz_handle *, int64_t, int, const float *, const float *, const float *, float *,
+                                const float *, const float *, int64_t, float *, int *);
+template int fused_u_sep<double>(lz_handle *, int64_t, int, double *, const double *, const double *, int *);
+template int fused_u_sep<float>(lz_handle *, int64_t, int, float *, const float *, const float *, int *);
 
 }  // namespace lz

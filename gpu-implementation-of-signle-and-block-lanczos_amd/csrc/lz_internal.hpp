@@ -70,6 +70,13 @@ int fused_e32(lz_handle *h, int64_t n, const float *Y, const float *Wj, const fl
               const float *binv, const float *P1, int64_t lc, float *qrow, int *nparts);
 // pass U: Wn <- Wn - Wj P2; slabs of Wn^T Wn
 int fused_u32(lz_handle *h, int64_t n, float *Wn, const float *Wj, const float *P2, int *nparts);
+// the same two passes at any b <= 32, fp64 or fp32 (b = 32 fp32: the MFMA kernels above;
+// otherwise VALU kernels); slabs of b x b doubles in h->partials
+template <typename T>
+int fused_e_sep(lz_handle *h, int64_t n, int b, const T *Y, const T *Wj, const T *Wprev, T *Wn, const T *binv,
+                const T *P1, int64_t lc, T *qrow, int *nparts);
+template <typename T>
+int fused_u_sep(lz_handle *h, int64_t n, int b, T *Wn, const T *Wj, const T *P2, int *nparts);
 
 // fp64 scalar helpers for the vector Lanczos (lz_fused.hip)
 template <typename T>

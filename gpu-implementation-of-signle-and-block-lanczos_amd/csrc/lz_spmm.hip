@@ -687,6 +687,24 @@ __global__ __launch_bounds__(256) void k_spmm_seg(int64_t n, const int64_t *__re
     }  // MODE 0
 }
 
+// Row-major SpMM at a block width off the tuned set (b not a power of two):
+// thread (r, c) sums row r in CSR order; the b threads of a row read the same
+// (col, val) line and b contiguous elements of each gathered X row.
+template <typename T>
+__global__ __launch_bounds__(256) void k_spmm_any_b(int64_t n, int b, const int64_t *__restrict__ rp,
+                                                    const int32_t *__restrict__ col, const T *__restrict__ val,
+                                                    const T *__restrict__ X, int64_t ldx, T *__restrict__ Y,
+                                                    int64_t ldy)
+{
+    for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n * b; i += (int64_t)gridDim.x * blockDim.x) {
+        const int64_t r = i / b;
+        const int c = (int)(i - r * b);
+        T acc = T(0);
+        for (int64_t k = rp[r], e = rp[r + 1]; k < e; ++k) acc = fma(val[k], X[(int64_t)col[k] * ldx + c], acc);
+        Y[r * ldy + c] = acc;
+    }
+}
+
 // Column-major compatibility path (the reference's Dense_matrix layout,
 // element (r,c) at r + c*ld).  One thread per row; any b.
 template <typename T>
@@ -826,9 +844,17 @@ int spmm_rm(lz_handle *h, int64_t n, int64_t nnz, const int64_t *rp, const int32
     case 16: return launch_spmm_rm<T, 16>(h, n, nnz, rp, col, val, X, ldx, nx, Y, ldy, ycm);
     case 32: return launch_spmm_rm<T, 32>(h, n, nnz, rp, col, val, X, ldx, nx, Y, ldy, ycm);
     case 64: return launch_spmm_rm<T, 64>(h, n, nnz, rp, col, val, X, ldx, nx, Y, ldy, ycm);
-    default:
-        set_error("row-major SpMM supports b in {1,2,4,8,16,32,64}, got %d", b);
-        return LZ_E_ARG;
+    default: {  // any other b <= 64: one thread per (row, column), CSR order (block widths off the tuned set)
+        LZ_ARG_CHECK(b >= 1 && b <= 64, "row-major SpMM: 1 <= b <= 64");
+        LZ_ARG_CHECK(!ycm, "column-major Y store: b a power of two");
+        const int64_t nb = n * b;
+        const int grid = (int)std::max<int64_t>(1, std::min<int64_t>(ceil_div(nb, (int64_t)256), (int64_t)h->n_cu * 16));
+        const int ev = prof_begin(h, PROF_SPMM);
+        hipLaunchKernelGGL((k_spmm_any_b<T>), dim3(grid), dim3(256), 0, h->stream, n, b, rp, col, val, X, ldx, Y, ldy);
+        prof_end(h, ev);
+        LZ_LAUNCH_CHECK();
+        return LZ_OK;
+    }
     }
 }
 

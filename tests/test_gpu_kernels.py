@@ -49,7 +49,7 @@ def check_spmm(lz, orc, h, torch, A, b, dtype, layout="row"):
         assert np.all(np.abs(Y - Yo) <= tol)
 
 
-@pytest.mark.parametrize("b", [1, 2, 4, 8, 16, 32])
+@pytest.mark.parametrize("b", [1, 2, 3, 4, 5, 8, 16, 32])
 def test_spmm_rowmajor_f64(lz, orc, handle, torch_cuda, b):
     A = lz.gen_banded(20011, 10.0, 500, seed=3)
     check_spmm(lz, orc, handle, torch_cuda, A, b, np.float64)
@@ -269,6 +269,6 @@ def test_errors_are_loud(lz, handle, torch_cuda):
     with pytest.raises(lz.LanczosError):
         handle.sqrtm(torch.zeros(40, 40, dtype=torch.float64, device="cuda"), W, W)
     A = lz.CsrDevice.from_host(lz.gen_banded(100, 5.0, 10))
-    with pytest.raises(lz.LanczosError):
-        handle.spmm(A, torch.zeros(100, 3, dtype=torch.float64, device="cuda"),
-                    torch.zeros(100, 3, dtype=torch.float64, device="cuda"))
+    with pytest.raises(lz.LanczosError):  # b = 65 > the 64-column limit
+        handle.spmm(A, torch.zeros(100, 65, dtype=torch.float64, device="cuda"),
+                    torch.zeros(100, 65, dtype=torch.float64, device="cuda"))

@@ -139,6 +139,32 @@ def test_block_f32_b32_powerlaw(lz, orc, handle, torch_cuda, n, cap, m, fused):
     assert handle.device_error() == 0
 
 
+@pytest.mark.parametrize("b", [1, 3, 4, 5, 8, 32])
+def test_block_fused_any_b_f64(lz, orc, handle, torch_cuda, b):
+    """The Q-free iteration at every block width but 16 (separate SpMM + VALU
+    passes E and U, lz_fused32.hip; b = 4 is the reference driver's N_COL):
+    fused and unfused against the oracle, Ritz within 1e-10."""
+    A = lz.gen_banded(20011, 10.0, 600, seed=b)
+    B = lz.uniform_B(A.n, b, seed=b + 1)
+    m, lc = 6, 20010
+    ref = orc.block_lanczos(A, B, m, lc)
+    for fused in (True, False):
+        got = gpu_block(lz, handle, torch_cuda, A, B, m, lc, fused=fused)
+        assert_close_run(lz, m, b, got, ref)
+    assert handle.device_error() == 0
+
+
+@pytest.mark.parametrize("b", [4, 16])
+def test_block_fused_any_b_f32(lz, orc, handle, torch_cuda, b):
+    """fp32 at b != 32 (VALU passes, fp64 accumulation rounded to fp32 once)."""
+    A = lz.gen_banded(20011, 10.0, 600, seed=b, dtype=np.float32)
+    B = lz.uniform_B(A.n, b, seed=b + 1, dtype=np.float32)
+    m, lc = 5, 77
+    got = gpu_block(lz, handle, torch_cuda, A, B, m, lc, fused=True)
+    _f32_checks(lz, m, b, got, orc.block_lanczos(A, B, m, lc), F32_RTOL)
+    assert handle.device_error() == 0
+
+
 @pytest.mark.parametrize("n,lc,m", [(33, 32, 1), (127, 100, 3), (4099, 4098, 5), (300_007, 300_000, 5)])
 def test_block_f32_b32_fused_shapes(lz, orc, handle, torch_cuda, n, lc, m):
     """The b = 32 fp32 Q-free passes at ragged sizes: fewer rows than one 32-row
