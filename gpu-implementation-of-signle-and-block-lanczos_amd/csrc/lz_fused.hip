@@ -311,25 +311,16 @@ __global__ __launch_bounds__(256) void k_slab_reduce1(const double *__restrict__
 }
 
 // Fold P slabs of bb (<= 256) doubles to <= 256 slabs at h->partials2 in one
-// or two fixed-order levels (the first level writes <= 4096 slabs past the
-// first 256*256 doubles of partials2).  Returns the folded count.
+// fixed-order level: block q sums slabs [q P / G, (q + 1) P / G) in order
+// (G = min(P, 256); at C3 3,584 pass-1 slabs, 14 per block).  Returns the
+// folded count.  (A copy-only first level of <= 4096 blocks was measured
+// here before: one launch and 7 MB more per step for nothing.)
 static int fold_slabs(lz_handle *h, const double *part, int64_t P, int bb, int *nout)
 {
-    double *final_ = h->partials2;
-    double *lvl1 = h->partials2 + 256 * 256;
+    const int g = (int)std::min<int64_t>(P, 256);
     const int ev = prof_begin(h, PROF_SMALL);
-    if (P <= 256) {
-        hipLaunchKernelGGL(k_slab_reduce1, dim3((unsigned)P), dim3(256), 0, h->stream, part, P, bb,
-                           final_);
-        *nout = (int)P;
-    } else {
-        const int g1 = (int)std::min<int64_t>(P, 4096);
-        hipLaunchKernelGGL(k_slab_reduce1, dim3(g1), dim3(256), 0, h->stream, part, P, bb, lvl1);
-        const int g2 = std::min(g1, 256);
-        hipLaunchKernelGGL(k_slab_reduce1, dim3(g2), dim3(256), 0, h->stream, lvl1, (int64_t)g1,
-                           bb, final_);
-        *nout = g2;
-    }
+    hipLaunchKernelGGL(k_slab_reduce1, dim3((unsigned)g), dim3(256), 0, h->stream, part, P, bb, h->partials2);
+    *nout = g;
     prof_end(h, ev);
     LZ_LAUNCH_CHECK();
     return LZ_OK;
