@@ -30,7 +30,8 @@ import numpy as np
 
 PKG_DIR = os.path.dirname(os.path.abspath(__file__))
 LIB_DIR = os.path.join(PKG_DIR, "lib")
-HIP_LIB = os.path.join(LIB_DIR, "liblz_hip.so")
+# LZ_HIP_LIB: another build of the same library (A/B of kernel versions in scripts/)
+HIP_LIB = os.environ.get("LZ_HIP_LIB") or os.path.join(LIB_DIR, "liblz_hip.so")
 HOST_LIB = os.path.join(LIB_DIR, "liblz_host.so")
 
 LZ_F64, LZ_F32 = 0, 1
