@@ -1191,7 +1191,7 @@ __device__ __forceinline__ double vl_win_tiles(int64_t n, int64_t c0, int64_t c1
                                                const T *__restrict__ w, T *__restrict__ qbuf,
                                                T *__restrict__ wn, int has_prev, int64_t lc,
                                                T *__restrict__ qrow, T beta, T rbeta,
-                                               T *ring, T *yrow)
+                                               T *ring, T *yrow, int32_t *rps)
 {
     constexpr int R = NT;
     constexpr int RPP = NT / LV, PASSES = R / RPP;  // rows per pass, passes per tile
@@ -1200,23 +1200,44 @@ __device__ __forceinline__ double vl_win_tiles(int64_t n, int64_t c0, int64_t c1
     auto slot = [&](int64_t i) -> int { return (int)((uint32_t)(i - base) % (uint32_t)RING); };
     auto wat = [&](int64_t i) -> T { return WIN ? ring[slot(i)] : w[i]; };
     double dot = 0.0;
+    // the first tile's row pointers; later tiles' are loaded one tile ahead
+    auto rows_at = [&](int64_t r) { return (int)(c1 - r < R ? c1 - r : R); };
+    int64_t nkb = 0, nke = 0, nrp = 0;
+    if (c0 < c1) {
+        const int rw = rows_at(c0);
+        nkb = rp[c0];
+        nke = rp[c0 + rw];
+        nrp = t < rw ? rp[c0 + t] : 0;
+    }
     for (int64_t r0 = c0; r0 < c1; r0 += R) {
-        const int rows = (int)(c1 - r0 < R ? c1 - r0 : R);
+        const int rows = rows_at(r0);
         // next tile's slab and this thread's epilogue row, issued first
         const int64_t si = r0 + R + H + t;
         const T slab = (WIN && si < n) ? w[si] : T(0);
         const int64_t erow = r0 + t;
         const T qprev = (t < rows && has_prev) ? qbuf[erow] : T(0);
-        // CSR offsets relative to the tile's first entry (a tile's run < 2^31)
-        const int64_t kb = rp[r0];
+        // CSR offsets relative to the tile's first entry (a tile's run < 2^31).
+        // The tile's row pointers come in one coalesced load per thread and
+        // go through LDS: read per row by each lane group they were PASSES x 2
+        // dependent-address loads, which the compiler issued one at a time
+        // (one VGPR, vmcnt(0) after each).
+        const int64_t kb = nkb, kend = nke;
+        if (t < rows) rps[t] = (int)(nrp - kb);
+        __syncthreads();
+        if (r0 + R < c1) {  // the next tile's row pointers, in flight behind this tile
+            const int rw = rows_at(r0 + R);
+            nkb = kend;
+            nke = rp[r0 + R + rw];
+            nrp = t < rw ? rp[r0 + R + t] : 0;
+        }
         const int32_t *cb = col + kb;
         const T *vb = val + kb;
         int ks[PASSES], ke[PASSES];
 #pragma unroll
         for (int s = 0; s < PASSES; ++s) {
             const int lr = s * RPP + g;
-            ks[s] = lr < rows ? (int)(rp[r0 + lr] - kb) : 0;
-            ke[s] = lr < rows ? (int)(rp[r0 + lr + 1] - kb) : 0;
+            ks[s] = lr < rows ? rps[lr] : 0;
+            ke[s] = lr < rows ? (lr + 1 < rows ? rps[lr + 1] : (int)(kend - kb)) : 0;
         }
         int c[PASSES][2];
         T v[PASSES][2];
@@ -1289,10 +1310,13 @@ __global__ __launch_bounds__(NT) void k_vl_spmv_win(
         if (win && i < hi) ring[(int)((uint32_t)(i - (c0 - H)) % (uint32_t)RING)] = wi[k];
     }
     __syncthreads();
+    // red (the slab scratch) is free during the tiles: it holds each tile's row pointers
+    int32_t *rps = reinterpret_cast<int32_t *>(red);
+    static_assert(sizeof(red) >= NT * sizeof(int32_t), "row pointers of a tile fit the slab scratch");
     const double dot = win ? vl_win_tiles<T, LV, NT, RING, true>(n, c0, c1, H, rp, col, val, w, qbuf, wn, has_prev,
-                                                                 lc, qrow, beta, rbeta, ring, yrow)
+                                                                 lc, qrow, beta, rbeta, ring, yrow, rps)
                            : vl_win_tiles<T, LV, NT, RING, false>(n, c0, c1, H, rp, col, val, w, qbuf, wn,
-                                                                  has_prev, lc, qrow, beta, rbeta, ring, yrow);
+                                                                  has_prev, lc, qrow, beta, rbeta, ring, yrow, rps);
     block_store_slab(dot, red, part_out);
 }
 
