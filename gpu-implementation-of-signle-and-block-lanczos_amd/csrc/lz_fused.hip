@@ -457,10 +457,14 @@ __global__ __launch_bounds__(256) void k_strip_pairs(int64_t n, const int64_t *_
          st += (int64_t)gridDim.x * blockDim.x) {
         uint32_t key[16];
         const int64_t r0 = st * 16;
+        // the strip's 17 row pointers first, all in flight at once (clamped
+        // indices: no per-load branch for the compiler to serialise on)
+        int64_t rv[17];
+#pragma unroll
+        for (int i = 0; i < 17; ++i) rv[i] = rp[r0 + i < n ? r0 + i : n];
 #pragma unroll
         for (int i = 0; i < 16; ++i) {
-            const int64_t r = r0 + i;
-            const int64_t len = r < n ? rp[r + 1] - rp[r] : 0;
+            const int64_t len = r0 + i < n ? rv[i + 1] - rv[i] : 0;
             key[i] = ((uint32_t)(len < (1 << 27) ? len : (1 << 27)) << 4) | (uint32_t)i;
         }
 #pragma unroll
