@@ -60,6 +60,7 @@ HIP_SYMBOLS = [
     ("lz_device_error", _c_int, [_c_vp, ctypes.POINTER(_c_int)]),
     ("lz_debug_poison_lds", _c_int, [_c_vp, ctypes.c_uint32]),
     ("lz_prof_enable", _c_int, [_c_vp, _c_int]),
+    ("lz_prof_enable_mask", _c_int, [_c_vp, ctypes.c_uint]),
     ("lz_prof_read", _c_int, [_c_vp, _c_int, ctypes.POINTER(_c_dbl), ctypes.POINTER(_c_int)]),
     ("lz_csr_spmm", _c_int, [_c_vp, _c_i64, _c_i64, _c_i64, _c_vp, _c_vp, _c_vp, _c_int, _c_int,
                              _c_vp, _c_i64, _c_int, _c_vp, _c_i64]),
@@ -548,8 +549,15 @@ class Handle:
         """Fill every CU's LDS with `pattern` (test support: stale-LDS reads show as NaN)."""
         _check(self.L.lz_debug_poison_lds(self._h, pattern), "lz_debug_poison_lds")
 
-    def prof_enable(self, on: bool = True):
-        _check(self.L.lz_prof_enable(self._h, int(on)), "lz_prof_enable")
+    def prof_enable(self, on: bool = True, classes=None):
+        """Record kernel-class timings (all classes, or only `classes`)."""
+        if classes is None:
+            _check(self.L.lz_prof_enable(self._h, int(on)), "lz_prof_enable")
+        else:
+            mask = 0
+            for c in classes:
+                mask |= 1 << int(c)
+            _check(self.L.lz_prof_enable_mask(self._h, mask if on else 0), "lz_prof_enable_mask")
 
     def prof_read(self, cls: int):
         """(total ms, launches) of a kernel class since prof_enable."""

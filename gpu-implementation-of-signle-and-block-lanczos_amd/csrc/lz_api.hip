@@ -18,7 +18,7 @@ static thread_local char g_err[1024] = "";
 
 int prof_begin(lz_handle *h, int cls)
 {
-    if (!h->prof || h->ev_used + 2 > h->ev_cap) return -1;
+    if (!h->prof || !((h->prof_mask >> cls) & 1u) || h->ev_used + 2 > h->ev_cap) return -1;
     const int idx = h->ev_used;
     if (hipEventRecord(h->ev_pool[idx], h->stream) != hipSuccess) return -1;
     h->ev_class[idx / 2] = cls;
@@ -637,18 +637,21 @@ int lz_debug_poison_lds(lz_handle *h, uint32_t pattern)
     return LZ_OK;
 }
 
-int lz_prof_enable(lz_handle *h, int on)
+int lz_prof_enable_mask(lz_handle *h, unsigned class_mask)
 {
     LZ_HANDLE_CHECK(h);
-    if (on && !h->ev_pool) {
+    if (class_mask && !h->ev_pool) {
         h->ev_cap = 8192;
         h->ev_pool = new hipEvent_t[h->ev_cap];
         for (int i = 0; i < h->ev_cap; ++i) LZ_HIP_TRY(hipEventCreate(&h->ev_pool[i]));
     }
-    h->prof = on != 0;
+    h->prof = class_mask != 0;
+    h->prof_mask = class_mask;
     h->ev_used = 0;
     return LZ_OK;
 }
+
+int lz_prof_enable(lz_handle *h, int on) { return lz_prof_enable_mask(h, on ? ~0u : 0u); }
 
 int lz_prof_read(lz_handle *h, int cls, double *ms_total, int *count)
 {

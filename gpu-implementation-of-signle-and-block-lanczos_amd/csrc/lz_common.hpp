@@ -84,6 +84,7 @@ struct lz_handle {
     // (lz_prof_enable / lz_prof_read): events recorded around each launch of
     // the class, elapsed times summed at read time.
     bool prof = false;
+    unsigned prof_mask = ~0u;     // classes recorded while prof is on
     hipEvent_t *ev_pool = nullptr;
     int ev_cap = 0, ev_used = 0;
     int ev_class[4096];

@@ -71,6 +71,11 @@ int lz_debug_poison_lds(lz_handle *h, uint32_t pattern);
 /* (LZ_POISON=1 in the environment: lz_init fills the new handle's workspaces with 0xFF.) */
 
 int lz_prof_enable(lz_handle *h, int on);
+/* As lz_prof_enable, recording only the classes whose bit is set in
+ * class_mask (1 << class; 0 = off).  Each recorded launch adds two event
+ * records to the stream (~3.5 us per launch on MI355X), so a timed run records
+ * only the class it reports. */
+int lz_prof_enable_mask(lz_handle *h, unsigned class_mask);
 int lz_prof_read(lz_handle *h, int kernel_class, double *ms_total, int *count);
 
 /* ----------------------------------------------------------- sparse kernels */
