@@ -541,13 +541,14 @@ __global__ __launch_bounds__(64 * (NC + NL)) void k_fused_pp16(
     __shared__ typename C::Stage st[K];
     __shared__ double scr[NC][256];  // per consumer: the parked Y tile (swizzled)
     __shared__ double ops[2][256];      // beta^-1, -beta in MFMA B-operand order
-    __shared__ int ready[K], done[K];
+    __shared__ int ready[K], done[K], slabs_in;
     const int lane = threadIdx.x & 63, w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
     const bool has_prev = beta != nullptr;
     if (threadIdx.x < K) {
         ready[threadIdx.x] = -1;
         done[threadIdx.x] = 0;
     }
+    if (threadIdx.x == 0) slabs_in = 0;
     // B operands in a permuted contraction order: MFMA step kc, lane l contracts
     // over k = 4 (l >> 4) + kc (not 4 kc + (l >> 4)), so every A operand a lane
     // needs is 4 contiguous doubles of one row -- two 16-B loads instead of
@@ -805,9 +806,28 @@ __global__ __launch_bounds__(64 * (NC + NL)) void k_fused_pp16(
     if (cw == 0 && lane == 0) lz_ws_probe[8 * blockIdx.x + 7] = nt;
 #endif
     if (s0p >= 0) epilogue();
-    double *slab = part + ((int64_t)blockIdx.x * NC + cw) * 256;
+    // the block's NC consumer slabs folded into one at part[blockIdx.x] by the
+    // last consumer to finish (an LDS counter; the loaders have exited), in
+    // k_slab_reduce1's order for NC slabs -- the launch that folded them is gone
 #pragma unroll
-    for (int r = 0; r < 4; ++r) slab[((lane >> 4) + 4 * r) * 16 + (lane & 15)] = macc[r];
+    for (int r = 0; r < 4; ++r) S0[((lane >> 4) + 4 * r) * 16 + (lane & 15)] = macc[r];
+    int arrived = 0;
+    if (lane == 0) arrived = __hip_atomic_fetch_add(&slabs_in, 1, __ATOMIC_ACQ_REL, __HIP_MEMORY_SCOPE_WORKGROUP);
+    arrived = __shfl(arrived, 0, 64);
+    if (arrived == NC - 1) {
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
+        double *slab = part + (int64_t)blockIdx.x * 256;
+        for (int e = lane; e < 256; e += 64) {
+            double a[8] = {0.0, 0.0, 0.0, 0.0, 0.0, 0.0, 0.0, 0.0};
+            int sl = 0;
+            for (; sl + 7 < NC; sl += 8) {
+#pragma unroll
+                for (int i = 0; i < 8; ++i) a[i] += scr[sl + i][e];
+            }
+            for (; sl < NC; ++sl) a[0] += scr[sl][e];
+            slab[e] = ((a[0] + a[1]) + (a[2] + a[3])) + ((a[4] + a[5]) + (a[6] + a[7]));
+        }
+    }
 }
 
 // C = A * B, 16 x 16 row-major fp64 (the per-step P1 = beta_{j-1}^-1 beta_j and
@@ -893,11 +913,11 @@ int fused_spmm16(lz_handle *h, int64_t n, const int64_t *rp, const int32_t *col,
         const int nc = wide ? 10 : 14;
         static_assert(14 <= kPairPad, "row orders must cover the last tile's strips");
         const int grid = (int)std::max<int64_t>(1, std::min<int64_t>(ceil_div(n, (int64_t)16 * nc), h->n_cu));
-        LZ_TRY(ensure_partials(h, (size_t)grid * nc * 256));
+        static_assert(kMaxB * kMaxB >= 256, "h->partials2 holds one 16 x 16 slab per pass-1 block");
         const int ev = prof_begin(h, PROF_SPMM_PASS);
-        auto go = [&](auto kern) {
+        auto go = [&](auto kern) {  // one folded slab per block, at h->partials2
             hipLaunchKernelGGL(kern, dim3(grid), dim3(64 * (nc + 2)), 0, h->stream, n, rp, col, val, Wg, nx, Wown,
-                               Qbuf, Wn, binv, beta, lc, qrow, h->partials, h->err_flag, pairs, row_off);
+                               Qbuf, Wn, binv, beta, lc, qrow, h->partials2, h->err_flag, pairs, row_off);
         };
         if (!wide && buf) go(k_fused_pp16<14, 2376, 3, 2, false>);
         else if (!wide) go(k_fused_pp16<14, 2376, 3, 2, true>);
@@ -905,7 +925,8 @@ int fused_spmm16(lz_handle *h, int64_t n, const int64_t *rp, const int32_t *col,
         else go(k_fused_pp16<10, 4400, 2, 2, true>);
         prof_end(h, ev);
         LZ_LAUNCH_CHECK();
-        return fold_slabs(h, h->partials, (int64_t)grid * nc, 256, nparts);
+        *nparts = grid;
+        return LZ_OK;
     }
     LZ_TRY(ensure_partials(h, tiles * 256));
     const int ev = prof_begin(h, PROF_SPMM_PASS);
