@@ -400,3 +400,28 @@ def test_block_b16_long_runs(lz, orc, handle, torch_cuda):
     assert_close_run(lz, m, 16, got, orc.block_lanczos(A, B, m, lc))
     # the persistent pass-1 kernels' bounded spins never timed out
     assert handle.device_error() == 0
+
+
+def test_prof_class_mask(lz, handle, torch_cuda):
+    """lz_prof_enable_mask records only the selected kernel classes (the bench's
+    timed region records pass 1 alone); lz_prof_enable(1) records all of them;
+    results do not depend on what is recorded."""
+    torch = torch_cuda
+    A = lz.gen_banded(20011, 10.0, 1024, seed=5)
+    B = lz.uniform_B(A.n, 16, seed=6)
+    Ad = lz.CsrDevice.from_host(A)
+    Bd = torch.from_numpy(B).cuda()
+    m = 3
+    outs = []
+    for classes in ([handle.PROF_SPMM_PASS], None):
+        handle.prof_enable(True, classes=classes)
+        q, al, be = lz.run_block_lanczos(handle, Ad, Bd, m, 84)
+        torch.cuda.synchronize()
+        ms1, c1 = handle.prof_read(handle.PROF_SPMM_PASS)
+        ms2, c2 = handle.prof_read(handle.PROF_UPDATE_PASS)
+        handle.prof_enable(False)
+        assert c1 == m and ms1 > 0.0
+        assert (c2 == 0) if classes else (c2 == m)
+        outs.append((q.cpu().numpy(), al.cpu().numpy(), be.cpu().numpy()))
+    assert all(np.array_equal(x, y) for x, y in zip(outs[0], outs[1]))
+    assert handle.device_error() == 0
