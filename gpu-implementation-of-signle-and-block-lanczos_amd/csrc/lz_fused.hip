@@ -3,14 +3,19 @@
 //
 // The reference iteration (methods/block_lanczos.hpp:131-166) is seven
 // library calls per step, moving ~A + 13 n*b*8 bytes.  Here one step is two
-// streaming passes plus two one-workgroup kernels:
+// streaming passes plus two one-workgroup kernels (the Q-free form: the
+// residual blocks W_j are kept unnormalised, Q_j is never stored):
 //
-//   pass 1  k_fused_spmm16   Y = A*W (gather),  Q_j[r] = W[r]*beta_j^-1,
-//                            W'[r] = Y[r]*beta_j^-1 - Q_{j-1}[r]*beta_j,
-//                            slabs of Q_j^T W'            (A + ~5 n*b*8 bytes)
-//   finish  k_gram_finish    alpha_j = 0.5 (M + M^T)
-//   pass 2  k_fused_update16 W' -= Q_j*alpha_j, slabs of W'^T W'   (3 n*b*8)
-//   finish  k_sqrtm          beta_{j+1}, beta_{j+1}^-1 = sqrtm(W'^T W')
+//   pass 1  k_fused_pp16     Y = A*W_j (gather),  Q_j[r] = W_j[r]*beta_j^-1,
+//                            W'[r] = Y[r]*beta_j^-1 - W_{j-1}[r]*P1,
+//                            slabs of Q_j^T W' (folded per block in LDS),
+//                            row probe                     (A + 3 n*b*8 bytes)
+//   finish  k_gram_finish    alpha_j = 0.5 (M + M^T), P2 = beta_j^-1 alpha_j
+//   pass 2  k_fused_update16 W' -= W_j*P2, slabs of W'^T W'        (3 n*b*8)
+//   finish  k_sqrtm_b        beta_{j+1}, beta_{j+1}^-1 = sqrtm(W'^T W'),
+//                            P1 = beta_j^-1 beta_{j+1}
+// (k_fused_spmm16, one 128-row tile per block, is the 64-bit-addressed
+// fallback for gather sources no 32-bit window covers.)
 //
 // using A*(W*beta^-1) = (A*W)*beta^-1, so the normalised block Q_j is formed
 // in the SpMM epilogue instead of in its own pass.  Q_j overwrites Q_{j-1} in
