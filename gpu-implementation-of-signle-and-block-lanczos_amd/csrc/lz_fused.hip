@@ -17,11 +17,11 @@
 // (k_fused_spmm16, one 128-row tile per block, is the 64-bit-addressed
 // fallback for gather sources no 32-bit window covers.)
 //
-// using A*(W*beta^-1) = (A*W)*beta^-1, so the normalised block Q_j is formed
-// in the SpMM epilogue instead of in its own pass.  Q_j overwrites Q_{j-1} in
-// place (row r is read and written by the same wave), the residual alternates
-// between the W and Q1 buffers.  All epilogue products run on
-// v_mfma_f64_16x16x4_f64 (see lz_dense.hip for the operand layouts).
+// using A*(W*beta^-1) = (A*W)*beta^-1, so Q_j exists only in registers of the
+// SpMM epilogue.  W' overwrites W_{j-1} in place (row r is read and written by
+// the same wave); the residual alternates between the W and Q1 buffers.  All
+// epilogue products run on v_mfma_f64_16x16x4_f64 (see lz_dense.hip for the
+// operand layouts).
 #include <cstring>
 #include <type_traits>
 #include "lz_common.hpp"
