@@ -96,7 +96,7 @@ def _worker(rank, world, port, n, b, m, hw, seed):
         dist.destroy_process_group()
 
 
-@pytest.mark.parametrize("world,b,hw", [(2, 4, 300), (2, 16, 300), (4, 16, 900)])
+@pytest.mark.parametrize("world,b,hw", [(2, 4, 300), (2, 16, 300), (4, 16, 900), (8, 16, 700)])
 def test_row_partitioned_block_lanczos_gloo(world, b, hw):
     """All-gather form at 2 and 4 ranks (4 ranks: uneven nnz-balanced slabs,
     every slab padded, halos reaching past the neighbouring rank)."""
@@ -197,7 +197,7 @@ def _halo_worker(rank, world, port, n, b, m, hw, seed):
         dist.destroy_process_group()
 
 
-@pytest.mark.parametrize("world,hw", [(2, 300), (3, 5000)])
+@pytest.mark.parametrize("world,hw", [(2, 300), (3, 5000), (8, 700)])
 def test_halo_partitioned_block_lanczos_gloo(world, hw):
     """hw=5000 > rows per rank: every rank's halo spans both neighbours and beyond."""
     import torch.multiprocessing as mp
