@@ -75,8 +75,9 @@ struct lz_handle {
     int nranks = 1, rank = 0;
     void *halo = nullptr;         // lz::HaloPlan when lz_halo_init was called
     uint64_t *pairs = nullptr;    // per-16-row-strip row order by length (k_strip_pairs)
-    int *longq = nullptr;         // k_spmm_seg long-tile queue: [0] count, [1..] tile ids
+    int *longq = nullptr;         // k_spmm_seg long-tile queue: [0], [1] counts (alternate calls), [2..] tile ids
     size_t longq_cap = 0;         // ints
+    int longq_parity = 0;         // the count slot of the next call
     size_t pairs_cap = 0;         // entries
     void *cm_buf = nullptr;       // column-major SpMM: row-major copies of X and Y
     size_t cm_cap = 0;            // bytes

@@ -364,7 +364,8 @@ __global__ __launch_bounds__(256) void k_spmm_seg(int64_t n, const int64_t *__re
                                                   const int32_t *__restrict__ col,
                                                   const T *__restrict__ val,
                                                   const T *__restrict__ X, int64_t ldx, int64_t nx,
-                                                  T *__restrict__ Y, int64_t ldy, int *__restrict__ longq)
+                                                  T *__restrict__ Y, int64_t ldy, int *__restrict__ longq,
+                                                  int parity)
 {
     // MODE 0: tiles whose run exceeds the stage (or, WIN, whose columns exceed
     //         the window) are queued (longq[0] = count, longq[1..] = tile ids)
@@ -404,9 +405,12 @@ __global__ __launch_bounds__(256) void k_spmm_seg(int64_t n, const int64_t *__re
                 }
             }
         };
-        const int cnt = longq[0];
+        // this launch's count slot; the other slot is zeroed for the next launch
+        // (no memset per call: the queue counts alternate between longq[0] / [1])
+        const int cnt = longq[parity];
+        if (blockIdx.x == 0 && threadIdx.x == 0) longq[parity ^ 1] = 0;
         for (int qi = blockIdx.x; qi < cnt; qi += gridDim.x) {
-            const int64_t r0 = (int64_t)longq[1 + qi] * TR;
+            const int64_t r0 = (int64_t)longq[2 + qi] * TR;
             const int nrows = (int)((n - r0) < TR ? (n - r0) : TR);
             const int64_t kA = rp[r0];
             __syncthreads();  // the previous tile is done with rel / yt
@@ -509,7 +513,7 @@ __global__ __launch_bounds__(256) void k_spmm_seg(int64_t n, const int64_t *__re
     }
     const int64_t N64 = rp[r0 + nrows] - kA;
     if (N64 > CAP) {  // block-uniform
-        if (tid == 0) longq[1 + atomicAdd(&longq[0], 1)] = (int)(r0 / TR);
+        if (tid == 0) longq[2 + atomicAdd(&longq[parity], 1)] = (int)(r0 / TR);
         return;
     }
     const int N = (int)N64;
@@ -601,7 +605,7 @@ __global__ __launch_bounds__(256) void k_spmm_seg(int64_t n, const int64_t *__re
         const int64_t lo = N > 0 ? cmin : 0, span = N > 0 ? (int64_t)cmax - cmin + 1 : 0;
         const int64_t wrows = (int64_t)(0x7fffffff / rowb) < kWinRows ? (int64_t)(0x7fffffff / rowb) : kWinRows;
         if (span > wrows) {  // block-uniform: columns too far apart for one window
-            if (tid == 0) longq[1 + atomicAdd(&longq[0], 1)] = (int)(r0 / TR);
+            if (tid == 0) longq[2 + atomicAdd(&longq[parity], 1)] = (int)(r0 / TR);
             return;
         }
         wb = (uint32_t)lo;
@@ -762,19 +766,22 @@ static int launch_seg(lz_handle *h, int64_t n, const int64_t *rp, const int32_t 
 {
     const int64_t st = ceil_div(n, (int64_t)TR);
     LZ_ARG_CHECK(st < (1LL << 31), "too many row tiles");
-    if ((size_t)st + 1 > h->longq_cap) {
+    if ((size_t)st + 2 > h->longq_cap) {
         LZ_HIP_TRY(hipStreamSynchronize(h->stream));
         (void)hipFree(h->longq);
         h->longq = nullptr;
-        LZ_HIP_TRY(hipMalloc(&h->longq, sizeof(int) * ((size_t)st + 1)));
-        h->longq_cap = (size_t)st + 1;
+        LZ_HIP_TRY(hipMalloc(&h->longq, sizeof(int) * ((size_t)st + 2)));
+        LZ_HIP_TRY(hipMemset(h->longq, 0, 2 * sizeof(int)));  // both count slots
+        h->longq_cap = (size_t)st + 2;
+        h->longq_parity = 0;
     }
-    LZ_HIP_TRY(hipMemsetAsync(h->longq, 0, sizeof(int), h->stream));
+    const int parity = h->longq_parity;
+    h->longq_parity ^= 1;
     hipLaunchKernelGGL((k_spmm_seg<T, B, TR, CAP, WIN, 0, YCM>), dim3((unsigned)st), dim3(256), 0, h->stream, n, rp, col,
-                       val, X, ldx, nx, Y, ldy, h->longq);
+                       val, X, ldx, nx, Y, ldy, h->longq, parity);
     const int g2 = (int)std::max<int64_t>(1, std::min<int64_t>(st, (int64_t)h->n_cu * 4));
     hipLaunchKernelGGL((k_spmm_seg<T, B, TR, CAP, WIN, 1, YCM>), dim3(g2), dim3(256), 0, h->stream, n, rp, col, val, X,
-                       ldx, nx, Y, ldy, h->longq);
+                       ldx, nx, Y, ldy, h->longq, parity);
     return LZ_OK;
 }
 
