@@ -391,7 +391,7 @@ def main():
               "iters_per_s": round(k5 / dt5, 2), "ms_per_iter": round(dt5 / k5 * 1e3, 3),
               "finite": bool(torch.isfinite(al5).all())}
         # MFMA utilisation of the C5 dense step (v_mfma_f32_32x32x2_f32), committed PMC passes
-        for kern in ("k_fused_e32", "k_fused_u32"):
+        for kern in ("k_fused_el32", "k_fused_ub32"):  # the beta^2 form's passes (the default at b = 32)
             d, src = pmc_record("mfma", kern, n5, A5.nnz, 0)
             if d:
                 c5.setdefault("mfma", {})[kern] = {"pmc_MfmaUtil_pct": d.get("MfmaUtil_pct"),

@@ -8,6 +8,7 @@
 #include <utility>
 #include <vector>
 
+#include <type_traits>
 #include "lz_common.hpp"
 #include "lz_internal.hpp"
 #include "lz_kernels.hpp"
@@ -205,11 +206,65 @@ static int block_lanczos_fused16(lz_handle *h, int64_t n, int64_t nnz, const int
 // and pass U: A + 9 n b s bytes per step against the reference order's
 // A + 13 n b s.  The residual buffers rotate as in block_lanczos_fused16
 // (B = W_0 read only, then W, Q1, in place).
+// The b = 32 fp32 step in its beta^2 form (default; LZ_C5_B2=0 selects the
+// pass-E form below): the SpMM's
+// epilogue stores U = W' beta_j = A W_j - W_{j-1} M_j with M_j =
+// beta_{j-1}^-1 G_j (G_j = W_j^T W_j, known before the step's sqrtm), so pass E
+// shrinks to the slabs W_j^T U; alpha_j = sym(beta_j^-1 (W_j^T U) beta_j^-1),
+// W'' = U beta_j^-1 - W_j beta_j^-1 alpha_j.  The sqrtm of G_{j+1} runs on the
+// side stream beside the next SpMM, which needs only M_{j+1}.
+static int block_lanczos_b2_32(lz_handle *h, int64_t n, int64_t nnz, const int64_t *rp, const int32_t *col,
+                               const float *val, int m, int64_t lc, const float *B, float *q, float *alpha,
+                               float *beta, float *Q0, float *Q1, float *W)
+{
+    constexpr int b = 32;
+    const int64_t bb = (int64_t)b * b;
+    float *sc = reinterpret_cast<float *>(h->scratch + 4 * kMaxB * kMaxB);
+    float *binv[2] = {sc, sc + bb}, *P2 = sc + 2 * bb, *M = sc + 3 * bb;
+    float *U = Q0;
+    int np = 0;
+    LZ_TRY(gram_partials<float>(h, n, b, B, B, b, &np));
+    LZ_TRY(sqrtm_pair<float>(h, b, nullptr, np, beta, binv[0], nullptr));
+    const float *in = B, *prev = nullptr;
+    for (int j = 0; j < m; ++j) {
+        float *out = j == 0 ? W : j == 1 ? Q1 : const_cast<float *>(prev);
+        const float *bi = binv[j & 1];
+        LZ_TRY(spmm_rm_b2(h, n, nnz, rp, col, val, in, n, U, prev, j ? M : nullptr));
+        if (j > 0) LZ_HIP_TRY(hipStreamWaitEvent(h->stream, h->ev_join, 0));
+        LZ_TRY(fused_el32(h, n, in, U, &np));
+        // the one-workgroup kernels read 32 folded slabs, not the passes' 1024
+        const int nf = fold_slabs_g(h, h->partials, np, (int)bb, 32);
+        LZ_TRY(alpha_b2(h, h->partials2, nf, bi, alpha + j * bb, P2, in, lc, n, q + (int64_t)j * b));
+        LZ_TRY(fused_ub32(h, n, U, in, bi, P2, out, &np));
+        if (j + 1 < m) {
+            const int ng = fold_slabs_g(h, h->partials, np, (int)bb, 32);
+            LZ_TRY(m_b2(h, h->partials2, ng, bi, M));  // M_{j+1} = beta_j^-1 G_{j+1}
+            LZ_HIP_TRY(hipEventRecord(h->ev_fork, h->stream));
+            LZ_HIP_TRY(hipStreamWaitEvent(h->side, h->ev_fork, 0));
+            hipStream_t main = h->stream;
+            h->stream = h->side;
+            const int rc = sqrtm_pair<float>(h, b, nullptr, np, beta + (j + 1) * bb, binv[(j + 1) & 1], nullptr);
+            h->stream = main;
+            LZ_TRY(rc);
+            LZ_HIP_TRY(hipEventRecord(h->ev_join, h->side));
+        }
+        prev = in;
+        in = out;
+    }
+    LZ_HIP_TRY(hipMemcpyAsync(beta + m * bb, binv[(m - 1) & 1], sizeof(float) * bb, hipMemcpyDeviceToDevice, h->stream));
+    return LZ_OK;
+}
+
 template <typename T>
 static int block_lanczos_sep(lz_handle *h, int64_t n, int64_t nnz, const int64_t *rp, const int32_t *col,
                              const T *val, int b, int m, int64_t lc, const T *B, T *q, T *alpha, T *beta, T *Q0,
                              T *Q1, T *W)
 {
+    if constexpr (std::is_same<T, float>::value) {  // default at b = 32; LZ_C5_B2=0: the form below
+        const char *e = getenv("LZ_C5_B2");
+        if (b == 32 && !(e && atoi(e) == 0) && spmm_b2_ok(n, nnz, n))
+            return block_lanczos_b2_32(h, n, nnz, rp, col, val, m, lc, B, q, alpha, beta, Q0, Q1, W);
+    }
     const int64_t bb = (int64_t)b * b;
     T *sc = reinterpret_cast<T *>(h->scratch + 4 * kMaxB * kMaxB);
     T *binv[2] = {sc, sc + bb}, *P = sc + 2 * bb;

@@ -226,6 +226,82 @@ __global__ __launch_bounds__(kRedThreads) void k_gram_finish(int b, const double
     }
 }
 
+// C5 beta^2 step (b = 32, fp32 storage, fp64 arithmetic), one workgroup each:
+// k_alpha_b2  X = sum slabs (W_j^T U), Z = beta^-1 X beta^-1, alpha = (Z + Z^T)/2,
+//             P2 = beta^-1 alpha, row probe q_j = W_j[lc] beta^-1
+// k_m_b2      G = sum slabs (W''^T W''), M = beta^-1 G (the next SpMM's epilogue)
+__global__ __launch_bounds__(kRedThreads) void k_alpha_b2(const double *__restrict__ part, int P,
+                                                          const float *__restrict__ binv, float *__restrict__ alpha,
+                                                          float *__restrict__ P2, const float *__restrict__ Wj,
+                                                          int64_t lc_row, float *__restrict__ qrow)
+{
+    constexpr int B = 32, BB = B * B;
+    __shared__ double x[BB], bi[BB], t1[BB];
+    __shared__ double scratch[kRedThreads];
+    const int t = threadIdx.x;
+    reduce_slabs(part, P, BB, x, scratch);
+    bi[t] = (double)binv[t];
+    __syncthreads();
+    const int i = t / B, j = t % B;
+    double s = 0.0;  // t1 = beta^-1 X
+    for (int k = 0; k < B; ++k) s = fma(bi[i * B + k], x[k * B + j], s);
+    t1[t] = s;
+    __syncthreads();
+    s = 0.0;  // Z = t1 beta^-1
+    for (int k = 0; k < B; ++k) s = fma(t1[i * B + k], bi[k * B + j], s);
+    x[t] = s;  // each thread reads only t1 and bi here
+    __syncthreads();
+    const float a = (float)(0.5 * (x[i * B + j] + x[j * B + i]));
+    __syncthreads();
+    alpha[t] = a;
+    t1[t] = (double)a;
+    __syncthreads();
+    s = 0.0;  // P2 = beta^-1 alpha
+    for (int k = 0; k < B; ++k) s = fma(bi[i * B + k], t1[k * B + j], s);
+    P2[t] = (float)s;
+    if (lc_row >= 0 && t < B) {
+        double q = 0.0;
+        for (int k = 0; k < B; ++k) q = fma((double)Wj[lc_row * B + k], bi[k * B + t], q);
+        qrow[t] = (float)q;
+    }
+}
+
+__global__ __launch_bounds__(kRedThreads) void k_m_b2(const double *__restrict__ part, int P,
+                                                      const float *__restrict__ binv, float *__restrict__ M)
+{
+    constexpr int B = 32, BB = B * B;
+    __shared__ double g[BB], bi[BB];
+    __shared__ double scratch[kRedThreads];
+    const int t = threadIdx.x;
+    reduce_slabs(part, P, BB, g, scratch);
+    bi[t] = (double)binv[t];
+    __syncthreads();
+    const int i = t / B, j = t % B;
+    double s = 0.0;
+    for (int k = 0; k < B; ++k) s = fma(bi[i * B + k], g[k * B + j], s);
+    M[t] = (float)s;
+}
+
+int alpha_b2(lz_handle *h, const double *part, int P, const float *binv, float *alpha, float *P2, const float *Wj,
+             int64_t lc, int64_t n, float *qrow)
+{
+    const int ev = prof_begin(h, PROF_SMALL);
+    hipLaunchKernelGGL(k_alpha_b2, dim3(1), dim3(kRedThreads), 0, h->stream, part, P, binv, alpha, P2, Wj,
+                       (lc >= 0 && lc < n) ? lc : (int64_t)-1, qrow);
+    prof_end(h, ev);
+    LZ_LAUNCH_CHECK();
+    return LZ_OK;
+}
+
+int m_b2(lz_handle *h, const double *part, int P, const float *binv, float *M)
+{
+    const int ev = prof_begin(h, PROF_SMALL);
+    hipLaunchKernelGGL(k_m_b2, dim3(1), dim3(kRedThreads), 0, h->stream, part, P, binv, M);
+    prof_end(h, ev);
+    LZ_LAUNCH_CHECK();
+    return LZ_OK;
+}
+
 // ------------------------------------------ b = 32 fp32 on v_mfma_f32_32x32x2_f32
 // (BASELINE config 5: block 32, fp32).  Lane l of a 32x32x2 MFMA supplies
 // A[i = l&31][k = l>>5] and B[k = l>>5][j = l&31]; C/D element (row

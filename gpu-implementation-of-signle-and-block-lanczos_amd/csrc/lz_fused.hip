@@ -315,6 +315,19 @@ __global__ __launch_bounds__(256) void k_slab_reduce1(const double *__restrict__
     }
 }
 
+// Fold P slabs of bb doubles to G slabs at h->partials2 (block q sums slabs
+// [q P / G, (q + 1) P / G) in order): the C5 beta^2 step's 1024 pass slabs
+// to 32 before a one-workgroup kernel reads them.
+int fold_slabs_g(lz_handle *h, const double *part, int64_t P, int bb, int G)
+{
+    const int g = (int)std::min<int64_t>(P, G);
+    const int ev = prof_begin(h, PROF_SMALL);
+    hipLaunchKernelGGL(k_slab_reduce1, dim3((unsigned)g), dim3(256), 0, h->stream, part, P, bb, h->partials2);
+    prof_end(h, ev);
+    LZ_LAUNCH_CHECK();
+    return g;
+}
+
 // Fold P slabs of bb (<= 256) doubles to <= 256 slabs at h->partials2 in one
 // fixed-order level: block q sums slabs [q P / G, (q + 1) P / G) in order
 // (G = min(P, 256); at C3 3,584 pass-1 slabs, 14 per block).  Returns the

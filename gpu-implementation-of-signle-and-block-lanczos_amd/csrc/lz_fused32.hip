@@ -163,6 +163,78 @@ __global__ __launch_bounds__(64 * kF32Waves) void k_fused_u32(int64_t n, float *
     block_slab32<kF32Waves>(red, g, lane, w, part);
 }
 
+// The beta^2 form of the step (C5; the SpMM's epilogue stores U = W' beta_j =
+// A W_j - W_{j-1} beta_{j-1}^-1 G_j, so pass E shrinks to the slabs W_j^T U):
+//   pass EL  slabs of W_j^T U                                   (2 n b s, reads only)
+//   pass UB  W'' = U beta_j^-1 - W_j P2 (P2 = beta_j^-1 alpha_j), slabs of W''^T W''
+__global__ __launch_bounds__(64 * kF32Waves) void k_fused_el32(int64_t n, const float *__restrict__ Wj,
+                                                               const float *__restrict__ U,
+                                                               double *__restrict__ part)
+{
+    __shared__ double red[kF32Waves][1024];
+    const int lane = threadIdx.x & 63, w = threadIdx.x >> 6, hh = lane >> 5, jr = lane & 31;
+    f16v_t g;
+#pragma unroll
+    for (int v = 0; v < 16; ++v) g[v] = 0.0f;
+    XcdSched sch(ceil_div(n, (int64_t)(32 * kF32Waves)));
+    for (int64_t u = sch.begin; u < sch.end; u += sch.step) {
+        const int64_t r0 = u * (32 * kF32Waves) + 32 * w;
+        float wv[16], uv[16];
+#pragma unroll
+        for (int v = 0; v < 16; ++v) {
+            const int64_t rr = r0 + (v & 3) + 8 * (v >> 2) + 4 * hh;
+            wv[v] = rr < n ? Wj[rr * 32 + jr] : 0.0f;
+            uv[v] = rr < n ? U[rr * 32 + jr] : 0.0f;
+        }
+#pragma unroll
+        for (int v = 0; v < 16; ++v) g = mfma32(wv[v], uv[v], g);
+    }
+    block_slab32<kF32Waves>(red, g, lane, w, part);
+}
+
+__global__ __launch_bounds__(64 * kF32Waves) void k_fused_ub32(int64_t n, const float *__restrict__ U,
+                                                               const float *__restrict__ Wj,
+                                                               const float *__restrict__ binv,
+                                                               const float *__restrict__ P2, float *__restrict__ Wn,
+                                                               double *__restrict__ part)
+{
+    __shared__ double red[kF32Waves][1024];
+    const int lane = threadIdx.x & 63, w = threadIdx.x >> 6, hh = lane >> 5, jr = lane & 31;
+    float bo[16], po[16];
+    bop32(binv, 1.0f, hh, jr, bo);
+    bop32(P2, -1.0f, hh, jr, po);
+    f16v_t g;
+#pragma unroll
+    for (int v = 0; v < 16; ++v) g[v] = 0.0f;
+    XcdSched sch(ceil_div(n, (int64_t)(32 * kF32Waves)));
+    for (int64_t u = sch.begin; u < sch.end; u += sch.step) {
+        const int64_t r0 = u * (32 * kF32Waves) + 32 * w;
+        const int64_t row = r0 + jr;
+        const bool ok = row < n;
+        float ua[16], wa[16];
+        aop32(U, row, ok, hh, ua);
+        aop32(Wj, row, ok, hh, wa);
+        f16v_t acc, acc2;  // two independent chains (each MFMA waits on its predecessor)
+#pragma unroll
+        for (int v = 0; v < 16; ++v) acc[v] = acc2[v] = 0.0f;
+#pragma unroll
+        for (int s2 = 0; s2 < 16; ++s2) {
+            acc = mfma32(ua[s2], bo[s2], acc);    // U beta^-1
+            acc2 = mfma32(wa[s2], po[s2], acc2);  // - W_j P2
+        }
+#pragma unroll
+        for (int v = 0; v < 16; ++v) acc[v] += acc2[v];
+#pragma unroll
+        for (int v = 0; v < 16; ++v) {
+            const int64_t rr = r0 + (v & 3) + 8 * (v >> 2) + 4 * hh;
+            if (rr < n) Wn[rr * 32 + jr] = acc[v];
+        }
+#pragma unroll
+        for (int v = 0; v < 16; ++v) g = mfma32(acc[v], acc[v], g);  // rows past n: 0
+    }
+    block_slab32<kF32Waves>(red, g, lane, w, part);
+}
+
 // blocks per CU: pass E (190 registers: 2 waves per SIMD) 2; pass U 4.
 // Measured at C5 (ms, E / U): grid 1x 1.12 / 0.91, 2x 0.96 / 0.78, 3x 1.20 / 0.78, 4x - / 0.76.
 static int f32_grid(lz_handle *h, int64_t n, int mult)
@@ -178,6 +250,32 @@ int fused_e32(lz_handle *h, int64_t n, const float *Y, const float *Wj, const fl
     const int ev = prof_begin(h, PROF_SPMM_PASS);
     hipLaunchKernelGGL(k_fused_e32, dim3(grid), dim3(64 * kF32Waves), 0, h->stream, n, Y, Wj, Wprev, Wn, binv, P1,
                        lc, qrow, h->partials);
+    prof_end(h, ev);
+    LZ_LAUNCH_CHECK();
+    *nparts = grid;
+    return LZ_OK;
+}
+
+int fused_el32(lz_handle *h, int64_t n, const float *Wj, const float *U, int *nparts)
+{
+    const int grid = f32_grid(h, n, 4);
+    LZ_TRY(ensure_partials(h, (size_t)grid * 1024));
+    const int ev = prof_begin(h, PROF_SPMM_PASS);
+    hipLaunchKernelGGL(k_fused_el32, dim3(grid), dim3(64 * kF32Waves), 0, h->stream, n, Wj, U, h->partials);
+    prof_end(h, ev);
+    LZ_LAUNCH_CHECK();
+    *nparts = grid;
+    return LZ_OK;
+}
+
+int fused_ub32(lz_handle *h, int64_t n, const float *U, const float *Wj, const float *binv, const float *P2,
+               float *Wn, int *nparts)
+{
+    const int grid = f32_grid(h, n, 4);
+    LZ_TRY(ensure_partials(h, (size_t)grid * 1024));
+    const int ev = prof_begin(h, PROF_UPDATE_PASS);
+    hipLaunchKernelGGL(k_fused_ub32, dim3(grid), dim3(64 * kF32Waves), 0, h->stream, n, U, Wj, binv, P2, Wn,
+                       h->partials);
     prof_end(h, ev);
     LZ_LAUNCH_CHECK();
     *nparts = grid;

@@ -70,6 +70,17 @@ int fused_e32(lz_handle *h, int64_t n, const float *Y, const float *Wj, const fl
               const float *binv, const float *P1, int64_t lc, float *qrow, int *nparts);
 // pass U: Wn <- Wn - Wj P2; slabs of Wn^T Wn
 int fused_u32(lz_handle *h, int64_t n, float *Wn, const float *Wj, const float *P2, int *nparts);
+// C5 beta^2 step (lz_fused32.hip, lz_dense.hip, lz_spmm.hip)
+int fused_el32(lz_handle *h, int64_t n, const float *Wj, const float *U, int *nparts);
+int fused_ub32(lz_handle *h, int64_t n, const float *U, const float *Wj, const float *binv, const float *P2,
+               float *Wn, int *nparts);
+int alpha_b2(lz_handle *h, const double *part, int P, const float *binv, float *alpha, float *P2, const float *Wj,
+             int64_t lc, int64_t n, float *qrow);
+int m_b2(lz_handle *h, const double *part, int P, const float *binv, float *M);
+bool spmm_b2_ok(int64_t n, int64_t nnz, int64_t nx);
+int fold_slabs_g(lz_handle *h, const double *part, int64_t P, int bb, int G);  // -> slab count at h->partials2
+int spmm_rm_b2(lz_handle *h, int64_t n, int64_t nnz, const int64_t *rp, const int32_t *col, const float *val,
+               const float *X, int64_t nx, float *Y, const float *Wp, const float *Mm);
 // the same two passes at any b <= 32, fp64 or fp32 (b = 32 fp32: the MFMA kernels above;
 // otherwise VALU kernels); slabs of b x b doubles in h->partials
 template <typename T>

@@ -359,13 +359,31 @@ __global__ __launch_bounds__(256) void k_spmm_buf(int64_t n, const int64_t *__re
 // YCM: Y is column-major (element (r, c) at r + c*ldy, the reference's
 // Dense_matrix layout): the finished Y tile leaves column by column, nrows
 // contiguous elements per column (the caller transposed X in).
-template <typename T, int B, int TR, int CAP, bool WIN, int MODE, bool YCM = false>
+// U row piece = Y piece - Wp[row] . M[:, piece] (k in order, one fma chain per
+// element): the C5 beta^2 epilogue of k_spmm_seg (EPI).
+template <typename T, int B, int VEC>
+__device__ __forceinline__ Vec<T, VEC> epi_piece(Vec<T, VEC> y, const T *__restrict__ wrow, const T *Ms, int pc)
+{
+#pragma unroll
+    for (int k4 = 0; k4 < B / 4; ++k4) {
+        T w[4];
+        const auto u = *reinterpret_cast<const float4 *>(wrow + 4 * k4);
+        __builtin_memcpy(w, &u, 16);
+#pragma unroll
+        for (int e = 0; e < 4; ++e)
+#pragma unroll
+            for (int i = 0; i < VEC; ++i) y.v[i] = fma(-w[e], Ms[(4 * k4 + e) * B + pc * VEC + i], y.v[i]);
+    }
+    return y;
+}
+
+template <typename T, int B, int TR, int CAP, bool WIN, int MODE, bool YCM = false, bool EPI = false>
 __global__ __launch_bounds__(256) void k_spmm_seg(int64_t n, const int64_t *__restrict__ rp,
                                                   const int32_t *__restrict__ col,
                                                   const T *__restrict__ val,
                                                   const T *__restrict__ X, int64_t ldx, int64_t nx,
                                                   T *__restrict__ Y, int64_t ldy, int *__restrict__ longq,
-                                                  int parity)
+                                                  int parity, const T *__restrict__ Wp, const T *__restrict__ Mm)
 {
     // MODE 0: tiles whose run exceeds the stage (or, WIN, whose columns exceed
     //         the window) are queued (longq[0] = count, longq[1..] = tile ids)
@@ -385,7 +403,13 @@ __global__ __launch_bounds__(256) void k_spmm_seg(int64_t n, const int64_t *__re
     __shared__ Vec<T, VEC> yt[TR][LPR];      // the tile's finished rows
     __shared__ Vec<T, VEC> head[G][LPR];     // a group's piece of a row begun in an earlier slice
     __shared__ int32_t cmin, cmax;           // WIN: the tile's column range
+    // EPI (b = 32 fp32, the C5 Q-free step in its beta^2 form): the stored row
+    // is U = Y - Wp M (Wp: W_{j-1}, M = beta_{j-1}^-1 G_j, 32 x 32 in LDS)
+    __shared__ T Ms[EPI ? B * B : 1];
     const int tid = threadIdx.x;
+    const bool epi = EPI && Wp != nullptr;
+    if (epi)
+        for (int e = tid; e < B * B; e += 256) Ms[e] = Mm[e];  // visible after the staging barriers
     const int gi = tid / LPR, p = tid % LPR;
     const uint32_t rowb = (uint32_t)(ldx * sizeof(T)), lane_off = p * VEC * sizeof(T);
     Vec<T, VEC> zero;
@@ -495,8 +519,12 @@ __global__ __launch_bounds__(256) void k_spmm_seg(int64_t n, const int64_t *__re
             if constexpr (YCM) {
                 store_tile_cm<T>(Y, r0, nrows, B, ldy, [&](int r, int c) { return yt[r][c / VEC].v[c % VEC]; });
             } else {
-                for (int idx = tid; idx < nrows * LPR; idx += 256)
-                    stv<T, VEC>(Y + (r0 + idx / LPR) * ldy + (idx % LPR) * VEC, yt[idx / LPR][idx % LPR]);
+                for (int idx = tid; idx < nrows * LPR; idx += 256) {
+                    Vec<T, VEC> y = yt[idx / LPR][idx % LPR];
+                    if constexpr (EPI)
+                        if (epi) y = epi_piece<T, B, VEC>(y, Wp + (r0 + idx / LPR) * B, Ms, idx % LPR);
+                    stv<T, VEC>(Y + (r0 + idx / LPR) * ldy + (idx % LPR) * VEC, y);
+                }
             }
         }
         return;
@@ -679,13 +707,16 @@ __global__ __launch_bounds__(256) void k_spmm_seg(int64_t n, const int64_t *__re
     }
     for (int idx = tid; idx < nrows * LPR; idx += 256) {
         T *dst = Y + (r0 + idx / LPR) * ldy + (idx % LPR) * VEC;
+        Vec<T, VEC> y = yt[idx / LPR][idx % LPR];
+        if constexpr (EPI)
+            if (epi) y = epi_piece<T, B, VEC>(y, Wp + (r0 + idx / LPR) * B, Ms, idx % LPR);
         if constexpr (sizeof(T) * VEC == 16) {
             typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
             u32x4 u;
-            __builtin_memcpy(&u, &yt[idx / LPR][idx % LPR], 16);
+            __builtin_memcpy(&u, &y, 16);
             __builtin_nontemporal_store(u, reinterpret_cast<u32x4 *>(dst));
         } else {
-            stv<T, VEC>(dst, yt[idx / LPR][idx % LPR]);
+            stv<T, VEC>(dst, y);
         }
     }
     }  // MODE 0
@@ -760,9 +791,9 @@ __global__ __launch_bounds__(256) void k_spmv(int64_t n, const int64_t *__restri
 
 // nnz-split SpMM with the long-tile queue: the main kernel, then a persistent
 // kernel over the queued tiles (an empty queue costs one short launch).
-template <typename T, int B, int TR, int CAP, bool WIN, bool YCM = false>
+template <typename T, int B, int TR, int CAP, bool WIN, bool YCM = false, bool EPI = false>
 static int launch_seg(lz_handle *h, int64_t n, const int64_t *rp, const int32_t *col, const T *val, const T *X,
-                      int64_t ldx, int64_t nx, T *Y, int64_t ldy)
+                      int64_t ldx, int64_t nx, T *Y, int64_t ldy, const T *Wp = nullptr, const T *Mm = nullptr)
 {
     const int64_t st = ceil_div(n, (int64_t)TR);
     LZ_ARG_CHECK(st < (1LL << 31), "too many row tiles");
@@ -777,11 +808,11 @@ static int launch_seg(lz_handle *h, int64_t n, const int64_t *rp, const int32_t 
     }
     const int parity = h->longq_parity;
     h->longq_parity ^= 1;
-    hipLaunchKernelGGL((k_spmm_seg<T, B, TR, CAP, WIN, 0, YCM>), dim3((unsigned)st), dim3(256), 0, h->stream, n, rp, col,
-                       val, X, ldx, nx, Y, ldy, h->longq, parity);
+    hipLaunchKernelGGL((k_spmm_seg<T, B, TR, CAP, WIN, 0, YCM, EPI>), dim3((unsigned)st), dim3(256), 0, h->stream, n, rp,
+                       col, val, X, ldx, nx, Y, ldy, h->longq, parity, Wp, Mm);
     const int g2 = (int)std::max<int64_t>(1, std::min<int64_t>(st, (int64_t)h->n_cu * 4));
-    hipLaunchKernelGGL((k_spmm_seg<T, B, TR, CAP, WIN, 1, YCM>), dim3(g2), dim3(256), 0, h->stream, n, rp, col, val, X,
-                       ldx, nx, Y, ldy, h->longq, parity);
+    hipLaunchKernelGGL((k_spmm_seg<T, B, TR, CAP, WIN, 1, YCM, EPI>), dim3(g2), dim3(256), 0, h->stream, n, rp, col, val,
+                       X, ldx, nx, Y, ldy, h->longq, parity, Wp, Mm);
     return LZ_OK;
 }
 
@@ -830,6 +861,27 @@ static int launch_spmm_rm(lz_handle *h, int64_t n, int64_t nnz, const int64_t *r
             hipLaunchKernelGGL((k_spmm_lds<T, B, CAP2, 2>), dim3((unsigned)tiles), dim3(256), 0, h->stream, n, rp,
                                col, val, X, ldx, nx, Y, ldy);
     }
+    prof_end(h, ev);
+    LZ_TRY(rc);
+    LZ_LAUNCH_CHECK();
+    return LZ_OK;
+}
+
+// C5 beta^2 step: U = A X - Wp M at b = 32 fp32, row-major, X < 2 GiB, <= 13
+// nnz per row (the shapes k_spmm_seg<..., 768, false> covers); returns
+// LZ_E_ARG otherwise so the caller keeps the separate pass E.
+bool spmm_b2_ok(int64_t n, int64_t nnz, int64_t nx)
+{
+    return nx * 32 * (int64_t)sizeof(float) < (1LL << 31) && nx < (1 << 24) && (double)nnz <= 13.0 * (double)n;
+}
+
+int spmm_rm_b2(lz_handle *h, int64_t n, int64_t nnz, const int64_t *rp, const int32_t *col, const float *val,
+               const float *X, int64_t nx, float *Y, const float *Wp, const float *Mm)
+{
+    LZ_ARG_CHECK(spmm_b2_ok(n, nnz, nx), "beta^2 SpMM epilogue: shape not covered");
+    if (n <= 0) return LZ_OK;
+    const int ev = prof_begin(h, PROF_SPMM);
+    const int rc = launch_seg<float, 32, 48, 768, false, false, true>(h, n, rp, col, val, X, 32, nx, Y, 32, Wp, Mm);
     prof_end(h, ev);
     LZ_TRY(rc);
     LZ_LAUNCH_CHECK();

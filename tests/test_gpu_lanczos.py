@@ -124,13 +124,19 @@ def _f32_checks(lz, m, b, got, ref, rtol):
 F32_RTOL = 1e-4
 
 
-@pytest.mark.parametrize("fused", [True, False])
+@pytest.mark.parametrize("form", ["b2", "e", "unfused"])
 @pytest.mark.parametrize("n,cap,m", [(20000, 2000, 4), (1_000_003, 100_000, 4), (20011, 2000, 8)])
-def test_block_f32_b32_powerlaw(lz, orc, handle, torch_cuda, n, cap, m, fused):
+def test_block_f32_b32_powerlaw(lz, orc, handle, torch_cuda, monkeypatch, n, cap, m, form):
     """C5 shape: fp32, b = 32, power-law rows (load imbalance); at n = 1M with
     rows up to 1e5 the long-tile queue of the SpMM runs.  alpha, beta, the row
-    probe q and the Ritz values against the fp32 oracle; the Q-free fused
-    passes (lz_fused32.hip) and the reference op order."""
+    probe q and the Ritz values against the fp32 oracle for the Q-free step in
+    its beta^2 form (default: U = A W_j - W_{j-1} M from the SpMM epilogue), in
+    its pass-E form (LZ_C5_B2=0), and the reference op order."""
+    fused = form != "unfused"
+    if form == "e":
+        monkeypatch.setenv("LZ_C5_B2", "0")
+    else:
+        monkeypatch.delenv("LZ_C5_B2", raising=False)
     A = lz.gen_powerlaw(n, 10.0, 2.1, cap, seed=5, dtype=np.float32)
     B = lz.uniform_B(A.n, 32, seed=6, dtype=np.float32)
     lc = 17
