@@ -361,14 +361,18 @@ __global__ __launch_bounds__(256) void k_spmm_buf(int64_t n, const int64_t *__re
 // contiguous elements per column (the caller transposed X in).
 // U row piece = Y piece - Wp[row] . M[:, piece] (k in order, one fma chain per
 // element): the C5 beta^2 epilogue of k_spmm_seg (EPI).
+// The B / VEC = 8 lanes of a row (consecutive lanes) each load one 16-B piece
+// of the row and pass it round by lane shuffles: one load per piece, not B / 4.
 template <typename T, int B, int VEC>
 __device__ __forceinline__ Vec<T, VEC> epi_piece(Vec<T, VEC> y, const T *__restrict__ wrow, const T *Ms, int pc)
 {
+    static_assert(B / 4 == 8 && VEC == 4, "b = 32 fp32 rows: 8 lanes of 4 values");
+    const float4 mine = *reinterpret_cast<const float4 *>(wrow + 4 * pc);
+    const int base = (int)(threadIdx.x & 63) & ~7;
 #pragma unroll
     for (int k4 = 0; k4 < B / 4; ++k4) {
-        T w[4];
-        const auto u = *reinterpret_cast<const float4 *>(wrow + 4 * k4);
-        __builtin_memcpy(w, &u, 16);
+        const T w[4] = {__shfl(mine.x, base + k4, 64), __shfl(mine.y, base + k4, 64), __shfl(mine.z, base + k4, 64),
+                        __shfl(mine.w, base + k4, 64)};
 #pragma unroll
         for (int e = 0; e < 4; ++e)
 #pragma unroll
