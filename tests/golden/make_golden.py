@@ -81,8 +81,6 @@ def main():
             out[f"N{N}_b{b}_B_head"] = Bc[:64].copy()
             out[f"N{N}_b{b}_B_sum"] = np.float64(Bc.sum())
             for m in ((5, 8) if N == 3 else (5, 20)):
-                if b == 16 and m == 20 and N == 10:
-                    continue
                 q, al, be = oracle.block_lanczos(A, B, m, lc)
                 qn, aln, ben = numpy_block_lanczos(A, B, m, lc)
                 assert np.allclose(q, qn, rtol=1e-9, atol=1e-12), "oracle vs numpy: q"

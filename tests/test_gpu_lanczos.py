@@ -79,8 +79,6 @@ def test_block_b16_tail_rows(lz, orc, handle, torch_cuda):
 @pytest.mark.parametrize("m", [5, 20])
 def test_block_matrix_a_golden(lz, orc, handle, torch_cuda, golden, b, m):
     """C1: the reference's own Yee operator (N=10) and glibc-rand B, golden vectors."""
-    if b == 16 and m == 20:
-        pytest.skip("no golden vector for this pair")
     A = golden_csr(lz, golden, 10)
     n = A.n
     B = lz.rand_B(n, b)

@@ -84,7 +84,7 @@ def test_sym_eig_vs_numpy(lz):
         assert np.allclose(V.T @ V, np.eye(k), atol=1e-12)
 
 
-@pytest.mark.parametrize("key", ["N10_b4_m5", "N10_b4_m20", "N10_b16_m5", "N3_b4_m8"])
+@pytest.mark.parametrize("key", ["N10_b4_m5", "N10_b4_m20", "N10_b16_m5", "N10_b16_m20", "N3_b4_m8"])
 def test_ritz_and_solution_from_golden(lz, golden, key):
     """Host eigensolver (tred2/tql2) vs the oracle's Jacobi on the golden alpha/beta."""
     m = int(key.split("_m")[1])

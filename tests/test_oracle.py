@@ -15,7 +15,8 @@ from make_golden import numpy_block_lanczos  # noqa: E402
 
 
 @pytest.mark.parametrize("key,N,b,m", [("N10_b4_m5", 10, 4, 5), ("N10_b4_m20", 10, 4, 20),
-                                       ("N10_b16_m5", 10, 16, 5), ("N3_b4_m8", 3, 4, 8)])
+                                       ("N10_b16_m5", 10, 16, 5), ("N10_b16_m20", 10, 16, 20),
+                                       ("N3_b4_m8", 3, 4, 8)])
 def test_oracle_reproduces_golden(lz, orc, golden, key, N, b, m):
     A = golden_csr(lz, golden, N)
     B = lz.rand_B(A.n, b)
