@@ -397,20 +397,22 @@ static ncclComm_t comm_of(lz_handle *h) { return reinterpret_cast<ncclComm_t>(h-
     } while (0)
 
 // b = 16 fp64 row-partitioned iteration (Q-free, as block_lanczos_fused16).
-// Per step: ncclAllGather of the residual slab into X_full, the fused pass on
-// local rows, two b x b ncclAllReduce (alpha and Gram partial sums), sqrtm
-// redundantly on every rank.  Local residual slabs (n_pad rows): W at step 0,
-// Q0 at step 1, then in place over the previous step's slab.
+// Per step: the fused pass on local rows (gathering from X_full), two b x b
+// ncclAllReduce (alpha and Gram partial sums), sqrtm redundantly on every
+// rank, and an in-place ncclAllGather of X_full.  The rank's W_j lives in its
+// own slot of X_full, W_{j-1} in the local buffer W: pass 1 writes W' over
+// W_{j-1} in W, pass 2 (SWAP form) writes W_{j+1} into the X_full slot and
+// W_j into W, so the all-gather moves only the peers' slabs (an out-of-place
+// all-gather also copies the rank's own 1.28 GB slab every step).
 static int block_lanczos_dist16(lz_handle *h, int64_t n_local, int64_t n_pad, int64_t nnz, const int64_t *rp,
                                 const int32_t *col, const double *val, int m, int64_t lc_local,
-                                const double *B, double *q, double *alpha, double *beta, double *Q0,
-                                double *W, double *X)
+                                const double *B, double *q, double *alpha, double *beta, double *W, double *X)
 {
     constexpr int64_t bb = 256;
     ncclComm_t comm = comm_of(h);
     QfreeBufs qb(h);
     double *slab = h->scratch;  // one reduced b x b slab, all-reduced in place
-    const double *own = X + (int64_t)h->rank * n_pad * 16;
+    double *own = X + (int64_t)h->rank * n_pad * 16;
     int P = 0;
     Pass1Plan pl;
     LZ_TRY(pass1_plan(h, n_local, rp, col, n_pad * h->nranks, (int64_t)h->rank * n_pad, &pl));
@@ -420,26 +422,23 @@ static int block_lanczos_dist16(lz_handle *h, int64_t n_local, int64_t n_pad, in
     LZ_NCCL_TRY(ncclAllReduce(slab, slab, bb, ncclDouble, ncclSum, comm, h->stream));
     LZ_TRY(sqrtm_pair<double>(h, 16, nullptr, 1, beta, qb.binv[0], nullptr, slab));
     LZ_NCCL_TRY(ncclAllGather(B, X, n_pad * 16, ncclDouble, comm, h->stream));
-    const double *cur = B, *prev = nullptr;  // this rank's W_j, W_{j-1}
     for (int j = 0; j < m; ++j) {
-        double *out = j == 0 ? W : j == 1 ? Q0 : const_cast<double *>(prev);
         const double *bi = qb.binv[j & 1];
-        LZ_TRY(fused_spmm16(h, n_local, rp, col, val, X, n_pad * h->nranks, own, prev, out, bi,
+        // W' over W_{j-1} (row r read, then written, by the same wave)
+        LZ_TRY(fused_spmm16(h, n_local, rp, col, val, X, n_pad * h->nranks, own, j ? W : nullptr, W, bi,
                             j ? qb.P : nullptr, lc_local, q + j * 16, &P, pl.pairs, nnz, (int64_t)h->rank * n_pad,
                             pl.win));
         LZ_TRY(gram_finish<double>(h, 16, P, 0, slab, h->partials2));
         LZ_NCCL_TRY(ncclAllReduce(slab, slab, bb, ncclDouble, ncclSum, comm, h->stream));
         LZ_TRY(gram_finish<double>(h, 16, 1, 1, alpha + j * bb, slab, bi, qb.P));
-        LZ_TRY(fused_update16(h, n_local, out, cur, qb.P, &P));
+        LZ_TRY(fused_update16_swap(h, n_local, W, own, qb.P, &P));
         if (j + 1 < m) {
             LZ_TRY(gram_finish<double>(h, 16, P, 0, slab));
             LZ_NCCL_TRY(ncclAllReduce(slab, slab, bb, ncclDouble, ncclSum, comm, h->stream));
             LZ_TRY(sqrtm_pair<double>(h, 16, nullptr, 1, beta + (j + 1) * bb, qb.binv[(j + 1) & 1], nullptr, slab,
                                       bi, qb.P));
-            LZ_NCCL_TRY(ncclAllGather(out, X, n_pad * 16, ncclDouble, comm, h->stream));
+            LZ_NCCL_TRY(ncclAllGather(own, X, n_pad * 16, ncclDouble, comm, h->stream));  // in place
         }
-        prev = cur;
-        cur = out;
     }
     LZ_HIP_TRY(hipMemcpyAsync(beta + m * bb, qb.binv[(m - 1) & 1], sizeof(double) * bb, hipMemcpyDeviceToDevice,
                               h->stream));
@@ -962,12 +961,13 @@ int lz_block_lanczos_dist(lz_handle *h, int64_t n_local, int64_t n_pad, int64_t 
     LZ_ARG_CHECK(dtype == LZ_F64 && b == 16, "distributed path: b = 16 fp64");
     LZ_ARG_CHECK(n_pad >= n_local && n_pad * h->nranks == n_global && m >= 1,
                  "dist sizes: n_pad >= n_local and n_global == n_pad * nranks (padded numbering)");
-    LZ_ARG_CHECK(B_local && q && alpha && beta && Q0 && W && X_full, "NULL buffer");
+    LZ_ARG_CHECK(B_local && q && alpha && beta && W && X_full, "NULL buffer");
+    (void)Q0;
     (void)Q1;
     const int64_t lc = (lc_rank == h->rank) ? lc_local : -1;
     return block_lanczos_dist16(h, n_local, n_pad, nnz_local, rp, col, (const double *)val, m, lc,
                                 (const double *)B_local, (double *)q, (double *)alpha,
-                                (double *)beta, (double *)Q0, (double *)W, (double *)X_full);
+                                (double *)beta, (double *)W, (double *)X_full);
 }
 
 static int halo_init_impl(lz_handle *h, int64_t row0, int64_t n_local, const int64_t *recv_counts,

@@ -344,9 +344,14 @@ static int fold_slabs(lz_handle *h, const double *part, int64_t P, int bb, int *
     return LZ_OK;
 }
 
-template <bool REV, int NW = 8>
+// SWAP (the all-gather form, lz_api.hip block_lanczos_dist16): Q is this
+// rank's slot of the all-gathered block.  W'' goes there (the next all-gather
+// is in place) and W_j, the next step's W_{j-1}, goes to Wn over W' -- one
+// 1.28 GB write more than the in-place pass, one slab copy (read + write) less
+// inside the all-gather.  Each row is read, then written, by the same wave.
+template <bool REV, int NW = 8, bool SWAP = false>
 __global__ __launch_bounds__(64 * NW) void k_fused_update16(int64_t n, double *__restrict__ Wn,
-                                                        const double *__restrict__ Q,
+                                                        std::conditional_t<SWAP, double, const double> *__restrict__ Q,
                                                         const double *__restrict__ alpha,
                                                         double *__restrict__ part)
 {
@@ -396,10 +401,20 @@ __global__ __launch_bounds__(64 * NW) void k_fused_update16(int64_t n, double *_
         if (r0 >= n) continue;
 #pragma unroll
         for (int kc = 0; kc < 4; ++kc) acc = mfma16(qv[kc], na_op[kc], acc);
+        double *dst = Wn;
+        if constexpr (SWAP) {
+            dst = Q;
+            const int64_t row = r0 + (lane & 15);
+            if (row < n) {
+                double2 *p2 = reinterpret_cast<double2 *>(Wn + row * 16 + 4 * (lane >> 4));
+                p2[0] = make_double2(qv[0], qv[1]);
+                p2[1] = make_double2(qv[2], qv[3]);
+            }
+        }
 #pragma unroll
         for (int r = 0; r < 4; ++r) {
             const int64_t row = r0 + (lane >> 4) + 4 * r;
-            if (row < n) Wn[r0 * 16 + 64 * r + lane] = acc[r];
+            if (row < n) dst[r0 * 16 + 64 * r + lane] = acc[r];
         }
 #pragma unroll
         for (int r = 0; r < 4; ++r) gacc = mfma16(acc[r], acc[r], gacc);
@@ -967,6 +982,21 @@ int fused_update16(lz_handle *h, int64_t n, double *Wn, const double *Q, const d
     LZ_TRY(ensure_partials(h, (size_t)grid * 256));
     const int ev = prof_begin(h, PROF_UPDATE_PASS);
     hipLaunchKernelGGL((k_fused_update16<true, 8>), dim3(grid), dim3(512), 0, h->stream, n, Wn, Q, alpha,
+                       h->partials);
+    prof_end(h, ev);
+    LZ_LAUNCH_CHECK();
+    *nparts = grid;
+    return LZ_OK;
+}
+
+// the SWAP form (k_fused_update16 above): Xown = W'' (was W_j), Wn = W_j (was W')
+int fused_update16_swap(lz_handle *h, int64_t n, double *Wn, double *Xown, const double *alpha, int *nparts)
+{
+    const int64_t units = ceil_div(ceil_div(n, 16), 8);
+    const int grid = (int)std::max<int64_t>(1, std::min<int64_t>(units, (int64_t)h->n_cu));
+    LZ_TRY(ensure_partials(h, (size_t)grid * 256));
+    const int ev = prof_begin(h, PROF_UPDATE_PASS);
+    hipLaunchKernelGGL((k_fused_update16<true, 8, true>), dim3(grid), dim3(512), 0, h->stream, n, Wn, Xown, alpha,
                        h->partials);
     prof_end(h, ev);
     LZ_LAUNCH_CHECK();

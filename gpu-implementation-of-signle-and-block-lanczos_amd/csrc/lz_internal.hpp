@@ -59,6 +59,7 @@ int strip_pairs(lz_handle *h, int64_t n, const int64_t *rp, const uint64_t **out
 // slabs of Wn^T Wn.
 int fused_update16(lz_handle *h, int64_t n, double *Wn, const double *Wcur, const double *P2,
                    int *nparts);
+int fused_update16_swap(lz_handle *h, int64_t n, double *Wn, double *Xown, const double *alpha, int *nparts);
 // C = A*B, 16 x 16 row-major fp64, on the stream
 int mm16(lz_handle *h, const double *A, const double *B, double *C);
 

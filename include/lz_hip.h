@@ -188,10 +188,10 @@ int lz_comm_destroy(lz_handle *h);
  *     numbering (global row r of rank g -> g*n_pad + (r - row0_g); host helper
  *     lzh_remap_cols_padded of include/lz_host.h);
  *   - X_full: n_global x b row-major workspace with n_global == n_pad * nranks
- *     (checked), receiving the all-gathered residual every iteration;
- *   - B_local, Q0, W: n_pad x b (rows past n_local are zero padding; the
- *     residual slab alternates between W and Q0 and is all-gathered whole);
- *     Q1 unused.
+ *     (checked), holding the all-gathered residual every iteration; the rank's
+ *     own slot is where its residual is updated, so the all-gather is in place;
+ *   - B_local, W: n_pad x b (rows past n_local are zero padding); W holds the
+ *     previous residual W_{j-1}; Q0 and Q1 unused (may be NULL).
  * lc_rank: the rank owning row lc (q written there only; other ranks' q
  * untouched).  Outputs alpha/beta identical on every rank.  Gather sources of
  * 2^24+ rows take the windowed fused pass (each strip's columns within 2^23
