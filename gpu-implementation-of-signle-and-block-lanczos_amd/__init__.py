@@ -86,6 +86,12 @@ HIP_SYMBOLS = [
     ("lz_block_lanczos_halo", _c_int, [_c_vp, _c_i64, _c_i64, _c_vp, _c_vp, _c_vp, _c_int, _c_int, _c_int,
                                        _c_i64, _c_int, _c_vp, _c_vp, _c_vp, _c_vp, _c_vp, _c_vp]),
     ("lz_comm_destroy", _c_int, [_c_vp]),
+    ("lz_local_group_create", _c_int, [_c_int, _c_int, ctypes.POINTER(_c_vp)]),
+    ("lz_local_group_destroy", _c_int, [_c_vp]),
+    ("lz_local_group_abort", _c_int, [_c_vp]),
+    ("lz_comm_init_local", _c_int, [_c_vp, _c_vp, _c_int]),
+    ("lz_comm_abort", _c_int, [_c_vp]),
+    ("lz_debug_last_split", _c_int, [_c_vp, _c_vp]),
     ("lz_block_lanczos_dist", _c_int, [_c_vp, _c_i64, _c_i64, _c_i64, _c_i64, _c_vp, _c_vp, _c_vp,
                                        _c_int, _c_int, _c_int, _c_i64, _c_int, _c_vp, _c_vp, _c_vp,
                                        _c_vp, _c_vp, _c_vp, _c_vp, _c_vp]),
@@ -570,6 +576,24 @@ class Handle:
         buf = ctypes.create_string_buffer(uid, 128)
         _check(self.L.lz_comm_init(self._h, nranks, rank, buf), "lz_comm_init")
 
+    def comm_init_local(self, group: "LocalGroup", rank: int):
+        """Attach this handle as virtual rank `rank` of an in-process group (one device)."""
+        _check(self.L.lz_comm_init_local(self.ptr, group.ptr, rank), "lz_comm_init_local")
+        group._keep.append(self)
+
+    def last_split(self):
+        """(i0, i1) of the last distributed solve's interior rows (pass 1 beside the
+        exchange), or None when it ran unsplit."""
+        v = (_c_i64 * 2)()
+        _check(self.L.lz_debug_last_split(self._h, v), "lz_debug_last_split")
+        return None if v[0] < 0 else (int(v[0]), int(v[1]))
+
+    def comm_abort(self):
+        _check(self.L.lz_comm_abort(self._h), "lz_comm_abort")
+
+    def comm_destroy(self):
+        _check(self.L.lz_comm_destroy(self._h), "lz_comm_destroy")
+
     def block_lanczos_dist(self, A_local: CsrDevice, n_pad: int, n_global: int, B_local, m: int,
                            lc_local: int, lc_rank: int, q, alpha, beta, Q0, W, X_full):
         n_local, b = A_local.n, B_local.shape[1]
@@ -603,6 +627,80 @@ class Handle:
                                             lc_local, lc_rank, _ptr(B_local), _ptr(q), _ptr(alpha),
                                             _ptr(beta), _ptr(X0), _ptr(X1)),
                "lz_block_lanczos_halo")
+
+
+class LocalGroup:
+    """N virtual ranks on one device in this process (lz_local_group_create):
+    every rank's Handle attaches with comm_init_local and then runs the same
+    distributed entry points an RCCL rank runs, from its own thread."""
+
+    def __init__(self, nranks: int, device: int = 0):
+        L = hip_lib()
+        g = _c_vp()
+        _check(L.lz_local_group_create(device, nranks, ctypes.byref(g)), "lz_local_group_create")
+        self.ptr, self.nranks, self.device, self.L = g, nranks, device, L
+        self._keep = []
+
+    def abort(self):
+        if self.ptr:
+            self.L.lz_local_group_abort(self.ptr)
+
+    def close(self):
+        if self.ptr:
+            self.L.lz_local_group_destroy(self.ptr)
+            self.ptr = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+
+def run_virtual_ranks(nranks: int, fn, device: int = 0, timeout: float = 600.0):
+    """Run fn(rank, handle) for ranks 0..nranks-1, each in its own thread with its
+    own torch stream and its own lz Handle attached to one LocalGroup.  Inputs
+    made before the call are synchronised first; returns the list of results.
+    A rank that raises aborts the group, so no other rank waits for it."""
+    import threading
+    torch = _torch()
+    torch.cuda.synchronize(device)
+    group = LocalGroup(nranks, device)
+    handles = [Handle(device) for _ in range(nranks)]
+    out, errs = [None] * nranks, [None] * nranks
+
+    def body(r):
+        try:
+            with torch.cuda.device(device), torch.cuda.stream(torch.cuda.Stream(device)):
+                handles[r].comm_init_local(group, r)
+                out[r] = fn(r, handles[r])
+                torch.cuda.current_stream(device).synchronize()
+        except BaseException as e:  # noqa: BLE001 -- reported below
+            errs[r] = e
+            group.abort()
+
+    threads = [threading.Thread(target=body, args=(r,), daemon=True) for r in range(nranks)]
+    try:
+        for t in threads:
+            t.start()
+        for t in threads:
+            t.join(timeout)
+        if any(t.is_alive() for t in threads):
+            group.abort()
+            for t in threads:
+                t.join(30)
+        if any(t.is_alive() for t in threads):  # never free what a live thread may still use
+            raise LanczosError("virtual ranks did not finish")
+    finally:
+        if not any(t.is_alive() for t in threads):
+            torch.cuda.synchronize(device)
+            for h in handles:
+                h.close()
+            group.close()
+    for r, e in enumerate(errs):
+        if e is not None:
+            raise LanczosError(f"virtual rank {r}: {e}") from e
+    return out
 
 
 def comm_unique_id() -> bytes:

@@ -1,7 +1,5 @@
 // lz_api.hip -- the extern "C" boundary of liblz_hip.so (include/lz_hip.h)
 // plus the device-resident Lanczos methods behind it.
-#include <rccl/rccl.h>
-
 #include <cstdarg>
 #include <cstring>
 #include <algorithm>
@@ -9,6 +7,7 @@
 #include <vector>
 
 #include <type_traits>
+#include "lz_comm.hpp"
 #include "lz_common.hpp"
 #include "lz_internal.hpp"
 #include "lz_kernels.hpp"
@@ -385,82 +384,32 @@ static int fdtd_block(lz_handle *h, int64_t n, int64_t nnz, const int64_t *rp, c
 }
 
 // ------------------------------------------------------------ multi-GPU
-static ncclComm_t comm_of(lz_handle *h) { return reinterpret_cast<ncclComm_t>(h->comm); }
+// Row-partitioned iteration: rank g owns a contiguous row range
+// of A and of every Krylov block.  Each step needs the rows of W_j its CSR
+// references on other ranks (the exchange) and two b x b sums (all-reduces);
+// the sqrtm is then computed redundantly on every rank.  Every collective goes
+// through lz::Comm (lz_comm.hpp): RCCL between processes, or device copies
+// between the virtual ranks of one process (the N-rank tests on one GPU).
 
-#define LZ_NCCL_TRY(expr)                                                            \
-    do {                                                                             \
-        ncclResult_t r_ = (expr);                                                    \
-        if (r_ != ncclSuccess) {                                                     \
-            ::lz::set_error("%s -> %s", #expr, ncclGetErrorString(r_));             \
-            return LZ_E_COMM;                                                        \
-        }                                                                            \
-    } while (0)
-
-// b = 16 fp64 row-partitioned iteration (Q-free, as block_lanczos_fused16).
-// Per step: the fused pass on local rows (gathering from X_full), two b x b
-// ncclAllReduce (alpha and Gram partial sums), sqrtm redundantly on every
-// rank, and an in-place ncclAllGather of X_full.  The rank's W_j lives in its
-// own slot of X_full, W_{j-1} in the local buffer W: pass 1 writes W' over
-// W_{j-1} in W, pass 2 (SWAP form) writes W_{j+1} into the X_full slot and
-// W_j into W, so the all-gather moves only the peers' slabs (an out-of-place
-// all-gather also copies the rank's own 1.28 GB slab every step).
-static int block_lanczos_dist16(lz_handle *h, int64_t n_local, int64_t n_pad, int64_t nnz, const int64_t *rp,
-                                const int32_t *col, const double *val, int m, int64_t lc_local,
-                                const double *B, double *q, double *alpha, double *beta, double *W, double *X)
+int attach_comm(lz_handle *h, Comm *c)
 {
-    constexpr int64_t bb = 256;
-    ncclComm_t comm = comm_of(h);
-    QfreeBufs qb(h);
-    double *slab = h->scratch;  // one reduced b x b slab, all-reduced in place
-    double *own = X + (int64_t)h->rank * n_pad * 16;
-    int P = 0;
-    Pass1Plan pl;
-    LZ_TRY(pass1_plan(h, n_local, rp, col, n_pad * h->nranks, (int64_t)h->rank * n_pad, &pl));
-    // beta_0 from the global Gram of B
-    LZ_TRY(gram_partials<double>(h, n_local, 16, B, B, 16, &P));
-    LZ_TRY(gram_finish<double>(h, 16, P, 0, slab));
-    LZ_NCCL_TRY(ncclAllReduce(slab, slab, bb, ncclDouble, ncclSum, comm, h->stream));
-    LZ_TRY(sqrtm_pair<double>(h, 16, nullptr, 1, beta, qb.binv[0], nullptr, slab));
-    LZ_NCCL_TRY(ncclAllGather(B, X, n_pad * 16, ncclDouble, comm, h->stream));
-    for (int j = 0; j < m; ++j) {
-        const double *bi = qb.binv[j & 1];
-        // W' over W_{j-1} (row r read, then written, by the same wave)
-        LZ_TRY(fused_spmm16(h, n_local, rp, col, val, X, n_pad * h->nranks, own, j ? W : nullptr, W, bi,
-                            j ? qb.P : nullptr, lc_local, q + j * 16, &P, pl.pairs, nnz, (int64_t)h->rank * n_pad,
-                            pl.win));
-        LZ_TRY(gram_finish<double>(h, 16, P, 0, slab, h->partials2));
-        LZ_NCCL_TRY(ncclAllReduce(slab, slab, bb, ncclDouble, ncclSum, comm, h->stream));
-        LZ_TRY(gram_finish<double>(h, 16, 1, 1, alpha + j * bb, slab, bi, qb.P));
-        LZ_TRY(fused_update16_swap(h, n_local, W, own, qb.P, &P));
-        if (j + 1 < m) {
-            LZ_TRY(gram_finish<double>(h, 16, P, 0, slab));
-            LZ_NCCL_TRY(ncclAllReduce(slab, slab, bb, ncclDouble, ncclSum, comm, h->stream));
-            LZ_TRY(sqrtm_pair<double>(h, 16, nullptr, 1, beta + (j + 1) * bb, qb.binv[(j + 1) & 1], nullptr, slab,
-                                      bi, qb.P));
-            LZ_NCCL_TRY(ncclAllGather(own, X, n_pad * 16, ncclDouble, comm, h->stream));  // in place
-        }
-    }
-    LZ_HIP_TRY(hipMemcpyAsync(beta + m * bb, qb.binv[(m - 1) & 1], sizeof(double) * bb, hipMemcpyDeviceToDevice,
-                              h->stream));
+    h->comm = c;
+    h->nranks = c->nranks;
+    h->rank = c->rank;
+    LZ_HIP_TRY(hipStreamCreateWithFlags(&h->xstream, hipStreamNonBlocking));
+    LZ_HIP_TRY(hipEventCreateWithFlags(&h->ev_cx, hipEventDisableTiming));
+    LZ_HIP_TRY(hipEventCreateWithFlags(&h->ev_xd, hipEventDisableTiming));
     return LZ_OK;
 }
 
-// ---------------------------------------------------- halo exchange (8e)
-// Row-partitioned iteration that moves only the rows other ranks reference
-// ("halo exchange of only the referenced columns"): each rank's
-// Krylov blocks live in X buffers of n_local + n_halo rows -- its own rows,
-// then the halo rows in the order lzh_halo_plan numbered them (ascending
-// global row, so each peer's rows are one contiguous run).  Per step the owner
-// packs the requested rows (k_halo_pack16) and one grouped ncclSend/ncclRecv
-// round moves them straight into the receivers' halo runs.  For a banded
-// operator that is 2 * halfwidth rows per rank instead of the all-gather's
-// (nranks - 1) * n_local, and the gather source stays < 2 GiB / 2^24 rows, so
-// the buffer-addressed fused pass applies at every rank count.
+// Halo plan (lz_halo_init): each peer's requested rows are one contiguous run
+// of the receiver's halo (ascending global row, so grouped by owner).
 struct HaloPlan {
     int64_t n_local = 0, n_halo = 0, n_send = 0;
     std::vector<int64_t> soff, roff;  // nranks + 1 row offsets per peer
     int32_t *send_idx = nullptr;      // device: local rows to pack, grouped by peer
-    double *sendbuf = nullptr;        // device: n_send x 16
+    void *sendbuf = nullptr;          // device: n_send packed rows
+    size_t send_cap = 0;              // bytes
 };
 
 static void halo_free(lz_handle *h)
@@ -473,93 +422,289 @@ static void halo_free(lz_handle *h)
     h->halo = nullptr;
 }
 
-__global__ void k_halo_pack16(int64_t ns, const int32_t *__restrict__ idx, const double *__restrict__ X,
-                              double *__restrict__ out)
+static void detach_comm(lz_handle *h)
 {
-    // one 16-B piece per thread, 8 pieces per 128-B row
-    for (int64_t t = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; t < ns * 8;
+    halo_free(h);
+    if (h->xstream) (void)hipStreamSynchronize(h->xstream);
+    delete h->comm;
+    h->comm = nullptr;
+    if (h->ev_cx) (void)hipEventDestroy(h->ev_cx);
+    if (h->ev_xd) (void)hipEventDestroy(h->ev_xd);
+    if (h->xstream) (void)hipStreamDestroy(h->xstream);
+    h->ev_cx = h->ev_xd = nullptr;
+    h->xstream = nullptr;
+    h->nranks = 1;
+    h->rank = 0;
+}
+
+// grow a device workspace; never inside the steps (it synchronises)
+static int grow_ws(lz_handle *h, void **buf, size_t *cap, size_t bytes)
+{
+    if (bytes <= *cap) return LZ_OK;
+    LZ_HIP_TRY(hipStreamSynchronize(h->stream));
+    if (h->xstream) LZ_HIP_TRY(hipStreamSynchronize(h->xstream));
+    (void)hipFree(*buf);
+    *buf = nullptr;
+    *cap = 0;
+    LZ_HIP_TRY(hipMalloc(buf, bytes));
+    *cap = bytes;
+    return LZ_OK;
+}
+
+// rows idx[i] of X (rowb bytes each) packed one after another, V-sized pieces
+template <typename V>
+__global__ void k_halo_pack(int64_t ns, const int32_t *__restrict__ idx, const char *__restrict__ X, int64_t rowb,
+                            V *__restrict__ out)
+{
+    const int64_t per = rowb / (int64_t)sizeof(V);
+    for (int64_t t = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; t < ns * per;
          t += (int64_t)gridDim.x * blockDim.x) {
-        const int64_t r = t >> 3;
-        const int p = (int)(t & 7);
-        reinterpret_cast<double2 *>(out)[t] =
-            reinterpret_cast<const double2 *>(X + (int64_t)idx[r] * 16)[p];
+        const int64_t r = t / per;
+        out[t] = reinterpret_cast<const V *>(X + (int64_t)idx[r] * rowb)[t - r * per];
     }
 }
 
-// fill rows [n_local, n_local + n_halo) of X from their owners
-static int halo_exchange16(lz_handle *h, const HaloPlan &hp, double *X)
+// fill rows [n_local, n_local + n_halo) of X (rowb bytes per row) from their
+// owners: pack the requested own rows, then one grouped point-to-point round
+static int halo_exchange(lz_handle *h, HaloPlan &hp, void *X, size_t rowb, hipStream_t s)
 {
-    if (h->nranks == 1 || !h->comm) return LZ_OK;
+    if (!h->comm || h->nranks == 1) return LZ_OK;
+    LZ_ARG_CHECK(hp.send_cap >= (size_t)hp.n_send * rowb, "halo send buffer smaller than the plan (internal)");
     if (hp.n_send > 0) {
-        const int grid = (int)std::min<int64_t>(ceil_div(hp.n_send * 8, 256), (int64_t)h->n_cu * 4);
-        hipLaunchKernelGGL(k_halo_pack16, dim3(grid), dim3(256), 0, h->stream, hp.n_send, hp.send_idx, X,
-                           hp.sendbuf);
+        const bool v16 = rowb % 16 == 0;
+        const int64_t pieces = hp.n_send * (int64_t)(rowb / (v16 ? 16 : 4));
+        const int grid = (int)std::max<int64_t>(1, std::min<int64_t>(ceil_div(pieces, 256), (int64_t)h->n_cu * 4));
+        if (v16)
+            hipLaunchKernelGGL(k_halo_pack<uint4>, dim3(grid), dim3(256), 0, s, hp.n_send, hp.send_idx,
+                               (const char *)X, (int64_t)rowb, (uint4 *)hp.sendbuf);
+        else
+            hipLaunchKernelGGL(k_halo_pack<uint32_t>, dim3(grid), dim3(256), 0, s, hp.n_send, hp.send_idx,
+                               (const char *)X, (int64_t)rowb, (uint32_t *)hp.sendbuf);
         LZ_LAUNCH_CHECK();
     }
-    ncclComm_t comm = comm_of(h);
-    LZ_NCCL_TRY(ncclGroupStart());
-    ncclResult_t r = ncclSuccess;
-    for (int p = 0; p < h->nranks && r == ncclSuccess; ++p) {
+    std::vector<P2POp> ops;
+    ops.reserve(h->nranks);
+    char *sb = static_cast<char *>(hp.sendbuf), *xb = static_cast<char *>(X);
+    for (int p = 0; p < h->nranks; ++p) {
         if (p == h->rank) continue;
-        const int64_t sc = hp.soff[p + 1] - hp.soff[p], rc = hp.roff[p + 1] - hp.roff[p];
-        if (sc) r = ncclSend(hp.sendbuf + hp.soff[p] * 16, (size_t)sc * 16, ncclDouble, p, comm, h->stream);
-        if (rc && r == ncclSuccess)
-            r = ncclRecv(X + (hp.n_local + hp.roff[p]) * 16, (size_t)rc * 16, ncclDouble, p, comm, h->stream);
+        const size_t sc = (size_t)(hp.soff[p + 1] - hp.soff[p]) * rowb, rc = (size_t)(hp.roff[p + 1] - hp.roff[p]) * rowb;
+        if (sc || rc)
+            ops.push_back(P2POp{p, sb + hp.soff[p] * rowb, sc, xb + (hp.n_local + hp.roff[p]) * rowb, rc});
     }
-    const ncclResult_t e = ncclGroupEnd();
-    LZ_NCCL_TRY(r);
-    LZ_NCCL_TRY(e);
-    return LZ_OK;
+    return h->comm->exchange(ops.data(), (int)ops.size(), s);
 }
 
-static int allreduce_bb(lz_handle *h, double *slab)
+// Interior / boundary split of the local rows (once per solve): rows
+// [i0, i1) reference only columns in [lo, hi) -- the rank's own rows of the
+// gather source -- so their pass 1 (or SpMM) needs no exchanged row and runs
+// while the exchange is in flight; rows [0, i0) and [i1, n) follow it.  i0 is
+// the end of the last row in the first half that reaches outside, i1 the first
+// such row in the second half (a banded partition's halo rows sit at both
+// ends), both rounded outward to 16-row strips.
+struct SplitPlan {
+    bool on = false;
+    int64_t i0 = 0, i1 = 0;
+};
+
+__global__ void k_span_init(int64_t n, unsigned long long *out)
 {
-    if (h->nranks == 1 || !h->comm) return LZ_OK;
-    LZ_NCCL_TRY(ncclAllReduce(slab, slab, 256, ncclDouble, ncclSum, comm_of(h), h->stream));
-    return LZ_OK;
+    out[0] = 0;
+    out[1] = (unsigned long long)n;
 }
 
-// b = 16 fp64.  Same step as block_lanczos_dist16 with the all-gather replaced
-// by the halo exchange; the residual alternates between X0 and X1: the fused
-// pass gathers from one and writes the other, whose own rows hold W_{j-1}
-// (read, then overwritten, row by row) -- Q-free as block_lanczos_fused16.
-static int block_lanczos_halo16(lz_handle *h, const HaloPlan &hp, int64_t nnz, const int64_t *rp, const int32_t *col,
-                                const double *val, int m, int64_t lc_local, const double *B, double *q,
-                                double *alpha, double *beta, double *X0, double *X1)
+__global__ __launch_bounds__(256) void k_local_span(int64_t n, const int64_t *__restrict__ rp,
+                                                    const int32_t *__restrict__ col, int64_t lo, int64_t hi,
+                                                    unsigned long long *__restrict__ out)
 {
-    constexpr int64_t bb = 256;
-    const int64_t n = hp.n_local, nx = hp.n_local + hp.n_halo;
-    QfreeBufs qb(h);
-    double *slab = h->scratch;
-    int P = 0;
-    Pass1Plan pl;
-    LZ_TRY(pass1_plan(h, n, rp, col, nx, 0, &pl));
-    LZ_TRY(gram_partials<double>(h, n, 16, B, B, 16, &P));
-    LZ_TRY(gram_finish<double>(h, 16, P, 0, slab));
-    LZ_TRY(allreduce_bb(h, slab));
-    LZ_TRY(sqrtm_pair<double>(h, 16, nullptr, 1, beta, qb.binv[0], nullptr, slab));
-    LZ_HIP_TRY(hipMemcpyAsync(X0, B, sizeof(double) * n * 16, hipMemcpyDeviceToDevice, h->stream));
-    LZ_TRY(halo_exchange16(h, hp, X0));
-    double *xs[2] = {X0, X1};
-    for (int j = 0; j < m; ++j) {
-        double *in = xs[j & 1], *out = xs[(j + 1) & 1];
-        const double *bi = qb.binv[j & 1];
-        LZ_TRY(fused_spmm16(h, n, rp, col, val, in, nx, in, j ? out : nullptr, out, bi, j ? qb.P : nullptr,
-                            lc_local, q + j * 16, &P, pl.pairs, nnz, 0, pl.win));
-        LZ_TRY(gram_finish<double>(h, 16, P, 0, slab, h->partials2));
-        LZ_TRY(allreduce_bb(h, slab));
-        LZ_TRY(gram_finish<double>(h, 16, 1, 1, alpha + j * bb, slab, bi, qb.P));
-        LZ_TRY(fused_update16(h, n, out, in, qb.P, &P));
-        if (j + 1 < m) {
-            LZ_TRY(gram_finish<double>(h, 16, P, 0, slab));
-            LZ_TRY(allreduce_bb(h, slab));
-            LZ_TRY(sqrtm_pair<double>(h, 16, nullptr, 1, beta + (j + 1) * bb, qb.binv[(j + 1) & 1], nullptr, slab,
-                                      bi, qb.P));
-            LZ_TRY(halo_exchange16(h, hp, out));
+    unsigned long long head = 0, tail = (unsigned long long)n;
+    for (int64_t r = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; r < n; r += (int64_t)gridDim.x * blockDim.x) {
+        bool ext = false;
+        for (int64_t k = rp[r], e = rp[r + 1]; k < e; ++k) {
+            const int64_t c = col[k];
+            ext |= (c < lo) | (c >= hi);
+        }
+        if (ext) {
+            if (2 * r < n) head = head > (unsigned long long)(r + 1) ? head : (unsigned long long)(r + 1);
+            else tail = tail < (unsigned long long)r ? tail : (unsigned long long)r;
         }
     }
-    LZ_HIP_TRY(hipMemcpyAsync(beta + m * bb, qb.binv[(m - 1) & 1], sizeof(double) * bb, hipMemcpyDeviceToDevice,
-                              h->stream));
+    for (int o = 32; o > 0; o >>= 1) {
+        const unsigned long long a = __shfl_xor(head, o, 64), t = __shfl_xor(tail, o, 64);
+        head = a > head ? a : head;
+        tail = t < tail ? t : tail;
+    }
+    if ((threadIdx.x & 63) == 0) {
+        atomicMax(&out[0], head);
+        atomicMin(&out[1], tail);
+    }
+}
+
+static int split_plan(lz_handle *h, int64_t n, const int64_t *rp, const int32_t *col, int64_t lo, int64_t hi,
+                      SplitPlan *sp)
+{
+    sp->on = false;
+    const char *e = getenv("LZ_DIST_OVERLAP");  // "0": exchange, then the whole pass (A/B)
+    if ((e && e[0] == '0') || !h->comm || h->nranks < 2 || n < 64) return LZ_OK;
+    unsigned long long *d = reinterpret_cast<unsigned long long *>(h->scratch + 7 * kMaxB * kMaxB);
+    hipLaunchKernelGGL(k_span_init, dim3(1), dim3(1), 0, h->stream, n, d);
+    const int grid = (int)std::max<int64_t>(1, std::min<int64_t>(ceil_div(n, (int64_t)256), (int64_t)h->n_cu * 8));
+    hipLaunchKernelGGL(k_local_span, dim3(grid), dim3(256), 0, h->stream, n, rp, col, lo, hi, d);
+    LZ_LAUNCH_CHECK();
+    unsigned long long hs[2] = {0, 0};
+    LZ_HIP_TRY(hipMemcpyAsync(hs, d, sizeof(hs), hipMemcpyDeviceToHost, h->stream));
+    LZ_HIP_TRY(hipStreamSynchronize(h->stream));
+    const int64_t i0 = ceil_div((int64_t)hs[0], 16) * 16, i1 = ((int64_t)hs[1] / 16) * 16;
+    // worth a second launch only when most rows are interior and some are not
+    if (i1 - i0 >= n / 4 && (i0 > 0 || i1 < n)) {
+        sp->on = true;
+        sp->i0 = i0;
+        sp->i1 = i1;
+    }
+    return LZ_OK;
+}
+
+enum { kFormHalo = 0, kFormAllgather = 1 };
+
+// The distributed iteration, both exchange forms, any b <= 32, fp64 / fp32.
+//   b = 16 fp64: the fused Q-free passes of block_lanczos_fused16 (pass 1 =
+//     SpMM + epilogue, pass 2 update + Gram);
+//   other b: the SpMM, then the VALU / MFMA passes E and U of block_lanczos_sep.
+// Buffers (rows of b elements, row-major):
+//   halo      X0, X1: n + n_halo rows; the residual alternates between them,
+//             own rows first, then the halo; pass 1 gathers from one and writes
+//             the other's own rows (W_{j-1} there, read then overwritten).
+//   allgather X0 = X_full (n_pad * nranks rows; the rank's W_j lives in its own
+//             slot), X1 = W (n_pad rows, W_{j-1}); pass 2 in its SWAP form
+//             writes W_{j+1} into the slot and W_j into W, so the all-gather is
+//             in place and moves only the peers' slabs.
+// With a split plan the exchange of step j's result runs on the handle's
+// exchange stream while pass 1 (or the SpMM) of step j+1 runs over the
+// interior rows; the boundary rows follow once it has landed.  Issue order:
+// pass 2 -> all-reduce -> sqrtm -> exchange (xstream) -> interior pass 1, so on
+// one communicator the step's small all-reduces never queue behind the
+// exchange.
+template <typename T>
+static int dist_solve(lz_handle *h, int form, HaloPlan *hp, int64_t n, int64_t n_pad, int64_t nnz, const int64_t *rp,
+                      const int32_t *col, const T *val, int b, int m, int64_t lc, const T *B, T *q, T *alpha, T *beta,
+                      T *X0, T *X1)
+{
+    Comm *cm = h->comm;
+    const bool ag = form == kFormAllgather;
+    const bool f16 = std::is_same<T, double>::value && b == 16;
+    const int64_t bb = (int64_t)b * b;
+    const size_t rowb = sizeof(T) * (size_t)b;
+    const int64_t nx = ag ? n_pad * h->nranks : n + (hp ? hp->n_halo : 0);
+    const int64_t own_off = ag ? (int64_t)h->rank * n_pad : 0;
+    double *slab = h->scratch;  // the reduced b x b slab (fp64), all-reduced in place
+    T *sc = reinterpret_cast<T *>(h->scratch + 4 * kMaxB * kMaxB);
+    T *binv[2] = {sc, sc + bb}, *P = sc + 2 * bb;
+    T *own = X0 + own_off * b;  // allgather: this rank's slot of X_full
+    // ---- once per solve (before any step: these may synchronise)
+    T *Y = nullptr;
+    if (!f16) {
+        LZ_TRY(grow_ws(h, &h->ybuf, &h->ybuf_cap, (size_t)std::max<int64_t>(n, 1) * rowb));
+        Y = static_cast<T *>(h->ybuf);
+    }
+    if (!ag && hp && cm && h->nranks > 1)
+        LZ_TRY(grow_ws(h, &hp->sendbuf, &hp->send_cap, (size_t)std::max<int64_t>(hp->n_send, 1) * rowb));
+    Pass1Plan pl;
+    if (f16) LZ_TRY(pass1_plan(h, n, rp, col, nx, own_off, &pl));
+    SplitPlan sp;
+    if (!f16 || fused16_direct(nx, pl.win)) LZ_TRY(split_plan(h, n, rp, col, own_off, own_off + n, &sp));
+    h->last_split[0] = sp.on ? sp.i0 : -1;
+    h->last_split[1] = sp.on ? sp.i1 : -1;
+    const bool reduce = cm && (ag || h->nranks > 1);
+    auto allreduce = [&]() -> int { return reduce ? cm->allreduce_sum(slab, (size_t)bb, h->stream) : LZ_OK; };
+    // step jj's buffers
+    auto gsrc = [&](int jj) -> T * { return ag ? X0 : (jj & 1 ? X1 : X0); };       // gather source, W_jj in own rows
+    auto wj = [&](int jj) -> T * { return ag ? own : gsrc(jj); };                   // W_jj's own rows
+    auto wn = [&](int jj) -> T * { return ag ? X1 : (jj & 1 ? X0 : X1); };          // W' / W'' (own rows)
+    // pass 1 (b = 16: fused) or the SpMM (other b) of step jj over rows [r0, r1)
+    int nslab = 0;  // b = 16: folded slabs written so far this step (at h->partials2)
+    auto pass1 = [&](int jj, int64_t r0, int64_t r1) -> int {
+        if (r1 <= r0) return LZ_OK;
+        const int64_t nnz_r = (int64_t)((double)nnz * (double)(r1 - r0) / (double)n);  // same kernel shape as the whole
+        if (!f16)
+            return spmm_rm<T>(h, r1 - r0, nnz_r, rp + r0, col, val, b, gsrc(jj), b, nx, Y + r0 * b, b);
+        if constexpr (std::is_same<T, double>::value) {
+            const int64_t lcr = (lc >= r0 && lc < r1) ? lc - r0 : -1;
+            int np = 0;
+            LZ_TRY(fused_spmm16(h, r1 - r0, rp + r0, col, val, gsrc(jj), nx, wj(jj) + r0 * 16,
+                                jj ? wn(jj) + r0 * 16 : nullptr, wn(jj) + r0 * 16, binv[jj & 1], jj ? P : nullptr, lcr,
+                                q + (int64_t)jj * 16, &np, pl.pairs + r0 / 16, nnz_r, own_off + r0, pl.win, nslab));
+            nslab += np;
+        }
+        return LZ_OK;
+    };
+    // the exchange that completes step jj's gather source (W_jj in own rows)
+    auto exchange = [&](int jj, hipStream_t s) -> int {
+        if (ag) return cm->allgather(own, X0, (size_t)n_pad * rowb, s);
+        return hp ? halo_exchange(h, *hp, gsrc(jj), rowb, s) : LZ_OK;
+    };
+    // ---- beta_0 from the global Gram of B, W_0 = B into the gather source
+    int np = 0;
+    LZ_TRY(gram_partials<T>(h, n, b, B, B, b, &np));
+    LZ_TRY(gram_finish<double>(h, b, np, 0, slab));
+    LZ_TRY(allreduce());
+    LZ_TRY(sqrtm_pair<T>(h, b, nullptr, 1, beta, binv[0], nullptr, slab));
+    if (ag) {
+        LZ_TRY(cm->allgather(B, X0, (size_t)n_pad * rowb, h->stream));
+    } else {
+        LZ_HIP_TRY(hipMemcpyAsync(X0, B, (size_t)n * rowb, hipMemcpyDeviceToDevice, h->stream));
+        LZ_TRY(exchange(0, h->stream));
+    }
+    bool interior_done = false;  // step j's interior rows already ran beside the exchange
+    for (int j = 0; j < m; ++j) {
+        const T *bi = binv[j & 1];
+        if (interior_done) {
+            LZ_HIP_TRY(hipStreamWaitEvent(h->stream, h->ev_xd, 0));
+            LZ_TRY(pass1(j, 0, sp.i0));
+            LZ_TRY(pass1(j, sp.i1, n));
+        } else {
+            nslab = 0;
+            LZ_TRY(pass1(j, 0, n));
+        }
+        if (f16) {
+            LZ_TRY(gram_finish<double>(h, 16, nslab, 0, slab, h->partials2));
+        } else {
+            LZ_TRY(fused_e_sep<T>(h, n, b, Y, wj(j), j ? wn(j) : nullptr, wn(j), bi, j ? P : nullptr, lc,
+                                  q + (int64_t)j * b, &np));
+            LZ_TRY(gram_finish<double>(h, b, np, 0, slab));
+        }
+        LZ_TRY(allreduce());
+        // alpha_j and P2 = beta_j^-1 alpha_j (this step's P1 is consumed)
+        LZ_TRY(gram_finish<T>(h, b, 1, 1, alpha + j * bb, slab, bi, P));
+        if constexpr (std::is_same<T, double>::value) {
+            if (f16) {
+                if (ag) LZ_TRY(fused_update16_swap(h, n, X1, own, P, &np));
+                else LZ_TRY(fused_update16(h, n, wn(j), wj(j), P, &np));
+            }
+        }
+        if (!f16) {
+            if (ag) LZ_TRY(fused_u_swap_sep<T>(h, n, b, X1, own, P, &np));
+            else LZ_TRY(fused_u_sep<T>(h, n, b, wn(j), wj(j), P, &np));
+        }
+        interior_done = false;
+        if (j + 1 < m) {
+            LZ_TRY(gram_finish<double>(h, b, np, 0, slab));
+            LZ_TRY(allreduce());
+            // beta_{j+1}, its inverse and P1 = beta_j^-1 beta_{j+1}
+            LZ_TRY(sqrtm_pair<T>(h, b, nullptr, 1, beta + (j + 1) * bb, binv[(j + 1) & 1], nullptr, slab, bi, P));
+            if (sp.on) {
+                LZ_HIP_TRY(hipEventRecord(h->ev_cx, h->stream));
+                LZ_HIP_TRY(hipStreamWaitEvent(h->xstream, h->ev_cx, 0));
+                LZ_TRY(exchange(j + 1, h->xstream));
+                LZ_HIP_TRY(hipEventRecord(h->ev_xd, h->xstream));
+                nslab = 0;
+                LZ_TRY(pass1(j + 1, sp.i0, sp.i1));
+                interior_done = true;
+            } else {
+                LZ_TRY(exchange(j + 1, h->stream));
+            }
+        }
+    }
+    LZ_HIP_TRY(hipMemcpyAsync(beta + m * bb, binv[(m - 1) & 1], sizeof(T) * bb, hipMemcpyDeviceToDevice, h->stream));
+    if (cm) LZ_TRY(cm->fence(h->stream));  // no peer reads this rank's buffers after the call
     return LZ_OK;
 }
 
@@ -641,11 +786,11 @@ int lz_finalize(lz_handle *h)
 {
     if (!h) return LZ_OK;
     (void)hipSetDevice(h->device);
-    halo_free(h);
+    detach_comm(h);
     (void)hipFree(h->pairs);
     (void)hipFree(h->longq);
     (void)hipFree(h->cm_buf);
-    if (h->comm) ncclCommDestroy(comm_of(h));
+    (void)hipFree(h->ybuf);
     if (h->ev_pool) {
         for (int i = 0; i < h->ev_cap; ++i) (void)hipEventDestroy(h->ev_pool[i]);
         delete[] h->ev_pool;
@@ -915,37 +1060,37 @@ int lz_fdtd_block(lz_handle *h, int64_t n, int64_t nnz, const int64_t *rp, const
                              T_end, lc, (float *)U, (float *)D, (float *)out);
 }
 
-int lz_comm_unique_id(unsigned char out[128])
-{
-    static_assert(sizeof(ncclUniqueId) == 128, "ncclUniqueId size");
-    ncclUniqueId id;
-    LZ_NCCL_TRY(ncclGetUniqueId(&id));
-    std::memcpy(out, &id, 128);
-    return LZ_OK;
-}
-
 int lz_comm_init(lz_handle *h, int nranks, int rank, const unsigned char id[128])
 {
     LZ_HANDLE_CHECK(h);
     LZ_ARG_CHECK(nranks >= 1 && rank >= 0 && rank < nranks && id, "comm args");
-    ncclUniqueId uid;
-    std::memcpy(&uid, id, 128);
-    ncclComm_t c;
-    LZ_NCCL_TRY(ncclCommInitRank(&c, nranks, uid, rank));
-    h->comm = c;
-    h->nranks = nranks;
-    h->rank = rank;
+    LZ_ARG_CHECK(h->comm == nullptr, "handle already has a communicator (lz_comm_destroy first)");
+    Comm *c = nullptr;
+    LZ_TRY(make_rccl_comm(nranks, rank, id, &c));
+    return attach_comm(h, c);
+}
+
+int lz_debug_last_split(lz_handle *h, int64_t out[2])
+{
+    LZ_ARG_CHECK(h && out, "NULL argument");
+    out[0] = h->last_split[0];
+    out[1] = h->last_split[1];
     return LZ_OK;
 }
 
 int lz_comm_destroy(lz_handle *h)
 {
     LZ_HANDLE_CHECK(h);
-    halo_free(h);
-    if (h->comm) ncclCommDestroy(comm_of(h));
-    h->comm = nullptr;
-    h->nranks = 1;
-    h->rank = 0;
+    detach_comm(h);
+    return LZ_OK;
+}
+
+static int dist_args(lz_handle *h, lz_dtype dtype, int b, int m)
+{
+    LZ_ARG_CHECK(dtype == LZ_F64 || dtype == LZ_F32, "dtype");
+    LZ_ARG_CHECK(b >= 1 && b <= 32, "distributed block Lanczos: 1 <= b <= 32");
+    LZ_ARG_CHECK(m >= 1, "m >= 1");
+    (void)h;
     return LZ_OK;
 }
 
@@ -958,16 +1103,21 @@ int lz_block_lanczos_dist(lz_handle *h, int64_t n_local, int64_t n_pad, int64_t 
     LZ_HANDLE_CHECK(h);
     LZ_ARG_CHECK(h->comm != nullptr, "lz_comm_init first");
     LZ_TRY(check_csr(n_local, nnz_local, rp, col, val));
-    LZ_ARG_CHECK(dtype == LZ_F64 && b == 16, "distributed path: b = 16 fp64");
-    LZ_ARG_CHECK(n_pad >= n_local && n_pad * h->nranks == n_global && m >= 1,
-                 "dist sizes: n_pad >= n_local and n_global == n_pad * nranks (padded numbering)");
+    LZ_TRY(dist_args(h, dtype, b, m));
+    LZ_ARG_CHECK(n_local >= 1 && n_pad >= n_local && n_pad * h->nranks == n_global,
+                 "dist sizes: n_pad >= n_local >= 1 and n_global == n_pad * nranks (padded numbering)");
     LZ_ARG_CHECK(B_local && q && alpha && beta && W && X_full, "NULL buffer");
+    LZ_ARG_CHECK(W != X_full && B_local != X_full && B_local != W, "B_local, W, X_full must be distinct");
     (void)Q0;
     (void)Q1;
     const int64_t lc = (lc_rank == h->rank) ? lc_local : -1;
-    return block_lanczos_dist16(h, n_local, n_pad, nnz_local, rp, col, (const double *)val, m, lc,
-                                (const double *)B_local, (double *)q, (double *)alpha,
-                                (double *)beta, (double *)W, (double *)X_full);
+    if (dtype == LZ_F64)
+        return dist_solve<double>(h, kFormAllgather, nullptr, n_local, n_pad, nnz_local, rp, col, (const double *)val, b,
+                                  m, lc, (const double *)B_local, (double *)q, (double *)alpha, (double *)beta,
+                                  (double *)X_full, (double *)W);
+    return dist_solve<float>(h, kFormAllgather, nullptr, n_local, n_pad, nnz_local, rp, col, (const float *)val, b, m,
+                             lc, (const float *)B_local, (float *)q, (float *)alpha, (float *)beta, (float *)X_full,
+                             (float *)W);
 }
 
 static int halo_init_impl(lz_handle *h, int64_t row0, int64_t n_local, const int64_t *recv_counts,
@@ -991,7 +1141,7 @@ static int halo_init_impl(lz_handle *h, int64_t row0, int64_t n_local, const int
     LZ_ARG_CHECK(hp->n_halo == 0 || halo_rows, "halo_rows is NULL");
     LZ_ARG_CHECK(n_local + hp->n_halo < (1LL << 31), "n_local + n_halo must fit int32 columns");
     if (nr == 1) return LZ_OK;
-    ncclComm_t comm = comm_of(h);
+    Comm *cm = h->comm;
     // 1. counts: rank p tells rank q how many of q's rows it needs
     int64_t *dcnt = nullptr;
     LZ_HIP_TRY(hipMalloc(&dcnt, sizeof(int64_t) * 2 * nr));
@@ -1004,24 +1154,19 @@ static int halo_init_impl(lz_handle *h, int64_t row0, int64_t n_local, const int
             rc = LZ_E_HIP;
             break;
         }
-        ncclResult_t r = ncclGroupStart();
-        for (int p = 0; p < nr && r == ncclSuccess; ++p) {
-            if (p == h->rank) continue;
-            r = ncclSend(dcnt + p, 1, ncclInt64, p, comm, h->stream);
-            if (r == ncclSuccess) r = ncclRecv(dcnt + nr + p, 1, ncclInt64, p, comm, h->stream);
-        }
-        const ncclResult_t e = ncclGroupEnd();
-        if (r != ncclSuccess || e != ncclSuccess) {
-            set_error("lz_halo_init: count exchange: %s", ncclGetErrorString(r != ncclSuccess ? r : e));
-            rc = LZ_E_COMM;
-            break;
-        }
+        std::vector<P2POp> ops;
+        for (int p = 0; p < nr; ++p)
+            if (p != h->rank) ops.push_back(P2POp{p, dcnt + p, sizeof(int64_t), dcnt + nr + p, sizeof(int64_t)});
+        rc = cm->exchange(ops.data(), (int)ops.size(), h->stream);
+        if (rc != LZ_OK) break;
         if (hipStreamSynchronize(h->stream) != hipSuccess ||
             hipMemcpy(scnt.data(), dcnt + nr, sizeof(int64_t) * nr, hipMemcpyDeviceToHost) != hipSuccess) {
             set_error("lz_halo_init: reading counts failed");
             rc = LZ_E_HIP;
         }
     } while (0);
+    if (rc == LZ_OK) rc = cm->fence(h->stream);  // peers are done reading dcnt
+    (void)hipStreamSynchronize(h->stream);
     (void)hipFree(dcnt);
     if (rc != LZ_OK) return rc;
     for (int p = 0; p < nr; ++p) {
@@ -1033,7 +1178,6 @@ static int halo_init_impl(lz_handle *h, int64_t row0, int64_t n_local, const int
     int32_t *dreq = nullptr;
     LZ_HIP_TRY(hipMalloc(&dreq, sizeof(int32_t) * std::max<int64_t>(1, hp->n_halo)));
     LZ_HIP_TRY(hipMalloc(&hp->send_idx, sizeof(int32_t) * std::max<int64_t>(1, hp->n_send)));
-    LZ_HIP_TRY(hipMalloc(&hp->sendbuf, sizeof(double) * 16 * std::max<int64_t>(1, hp->n_send)));
     std::vector<int32_t> sidx(hp->n_send);
     do {
         if (hp->n_halo &&
@@ -1042,20 +1186,16 @@ static int halo_init_impl(lz_handle *h, int64_t row0, int64_t n_local, const int
             rc = LZ_E_HIP;
             break;
         }
-        ncclResult_t r = ncclGroupStart();
-        for (int p = 0; p < nr && r == ncclSuccess; ++p) {
+        std::vector<P2POp> ops;
+        for (int p = 0; p < nr; ++p) {
             if (p == h->rank) continue;
             const int64_t sc = hp->soff[p + 1] - hp->soff[p], rcv = hp->roff[p + 1] - hp->roff[p];
-            if (rcv) r = ncclSend(dreq + hp->roff[p], (size_t)rcv, ncclInt32, p, comm, h->stream);
-            if (sc && r == ncclSuccess)
-                r = ncclRecv(hp->send_idx + hp->soff[p], (size_t)sc, ncclInt32, p, comm, h->stream);
+            if (sc || rcv)
+                ops.push_back(P2POp{p, dreq + hp->roff[p], sizeof(int32_t) * (size_t)rcv, hp->send_idx + hp->soff[p],
+                                    sizeof(int32_t) * (size_t)sc});
         }
-        const ncclResult_t e = ncclGroupEnd();
-        if (r != ncclSuccess || e != ncclSuccess) {
-            set_error("lz_halo_init: request exchange: %s", ncclGetErrorString(r != ncclSuccess ? r : e));
-            rc = LZ_E_COMM;
-            break;
-        }
+        rc = cm->exchange(ops.data(), (int)ops.size(), h->stream);
+        if (rc != LZ_OK) break;
         if (hipStreamSynchronize(h->stream) != hipSuccess ||
             (hp->n_send && hipMemcpy(sidx.data(), hp->send_idx, sizeof(int32_t) * hp->n_send,
                                      hipMemcpyDeviceToHost) != hipSuccess)) {
@@ -1063,6 +1203,8 @@ static int halo_init_impl(lz_handle *h, int64_t row0, int64_t n_local, const int
             rc = LZ_E_HIP;
         }
     } while (0);
+    if (rc == LZ_OK) rc = cm->fence(h->stream);  // peers are done reading dreq
+    (void)hipStreamSynchronize(h->stream);
     (void)hipFree(dreq);
     if (rc != LZ_OK) return rc;
     // 3. global -> local row; every requested row must be ours
@@ -1081,7 +1223,10 @@ int lz_halo_init(lz_handle *h, int64_t row0, int64_t n_local, const int64_t *rec
 {
     LZ_HANDLE_CHECK(h);
     const int rc = halo_init_impl(h, row0, n_local, recv_counts, halo_rows);
-    if (rc != LZ_OK) halo_free(h);  // never leave a half-built plan behind
+    if (rc != LZ_OK) {
+        if (h->comm) h->comm->abort();  // a peer blocked in the same set-up must not wait for this rank
+        halo_free(h);                   // never leave a half-built plan behind
+    }
     return rc;
 }
 
@@ -1098,8 +1243,11 @@ int lz_halo_exchange(lz_handle *h, lz_dtype dtype, int b, void *X)
 {
     LZ_HANDLE_CHECK(h);
     LZ_ARG_CHECK(h->halo, "lz_halo_init first");
-    LZ_ARG_CHECK(dtype == LZ_F64 && b == 16 && X, "halo exchange: b = 16 fp64");
-    return halo_exchange16(h, *static_cast<const HaloPlan *>(h->halo), (double *)X);
+    LZ_ARG_CHECK((dtype == LZ_F64 || dtype == LZ_F32) && b >= 1 && b <= kMaxB && X, "halo exchange args");
+    HaloPlan &hp = *static_cast<HaloPlan *>(h->halo);
+    const size_t rowb = (size_t)b * (dtype == LZ_F64 ? 8 : 4);
+    if (h->comm && h->nranks > 1) LZ_TRY(grow_ws(h, &hp.sendbuf, &hp.send_cap, (size_t)std::max<int64_t>(hp.n_send, 1) * rowb));
+    return halo_exchange(h, hp, X, rowb, h->stream);
 }
 
 int lz_block_lanczos_halo(lz_handle *h, int64_t n_local, int64_t nnz_local, const int64_t *rp,
@@ -1109,15 +1257,20 @@ int lz_block_lanczos_halo(lz_handle *h, int64_t n_local, int64_t nnz_local, cons
 {
     LZ_HANDLE_CHECK(h);
     LZ_ARG_CHECK(h->halo, "lz_halo_init first");
-    const HaloPlan &hp = *static_cast<const HaloPlan *>(h->halo);
+    HaloPlan &hp = *static_cast<HaloPlan *>(h->halo);
     LZ_TRY(check_csr(n_local, nnz_local, rp, col, val));
     LZ_ARG_CHECK(n_local == hp.n_local, "n_local differs from lz_halo_init");
-    LZ_ARG_CHECK(dtype == LZ_F64 && b == 16, "halo path: b = 16 fp64");
-    LZ_ARG_CHECK(m >= 1 && n_local >= 1, "sizes");
+    LZ_TRY(dist_args(h, dtype, b, m));
+    LZ_ARG_CHECK(n_local >= 1, "sizes");
     LZ_ARG_CHECK(B_local && q && alpha && beta && X0 && X1 && X0 != X1, "NULL / aliased buffer");
     const int64_t lc = (lc_rank == h->rank) ? lc_local : -1;
-    return block_lanczos_halo16(h, hp, nnz_local, rp, col, (const double *)val, m, lc, (const double *)B_local,
-                                (double *)q, (double *)alpha, (double *)beta, (double *)X0, (double *)X1);
+    if (dtype == LZ_F64)
+        return dist_solve<double>(h, kFormHalo, &hp, n_local, n_local, nnz_local, rp, col, (const double *)val, b, m,
+                                  lc, (const double *)B_local, (double *)q, (double *)alpha, (double *)beta,
+                                  (double *)X0, (double *)X1);
+    return dist_solve<float>(h, kFormHalo, &hp, n_local, n_local, nnz_local, rp, col, (const float *)val, b, m, lc,
+                             (const float *)B_local, (float *)q, (float *)alpha, (float *)beta, (float *)X0,
+                             (float *)X1);
 }
 
 }  // extern "C"

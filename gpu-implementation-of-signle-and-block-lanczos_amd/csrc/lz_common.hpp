@@ -10,6 +10,8 @@
 
 namespace lz {
 
+class Comm;  // lz_comm.hpp
+
 // thread-local last error (lz_last_error)
 void set_error(const char *fmt, ...);
 
@@ -71,8 +73,16 @@ struct lz_handle {
     double *partials2 = nullptr;  // first-level folded slabs: 256 * kMaxB * kMaxB doubles
     double *scratch = nullptr;    // 8 * kMaxB * kMaxB doubles
     int *err_flag = nullptr;      // device: nonzero if a persistent kernel gave up a bounded spin
-    void *comm = nullptr;         // ncclComm_t when lz_comm_init was called
+    lz::Comm *comm = nullptr;     // lz_comm_init (RCCL) or lz_comm_init_local (virtual ranks)
     int nranks = 1, rank = 0;
+    // the Krylov-block exchange of the distributed iteration runs on its own
+    // stream, beside the interior rows' pass 1 (ev_cx: main -> exchange stream,
+    // ev_xd: exchange done -> main)
+    hipStream_t xstream = nullptr;
+    hipEvent_t ev_cx = nullptr, ev_xd = nullptr;
+    int64_t last_split[2] = {-1, -1};  // lz_debug_last_split
+    void *ybuf = nullptr;         // distributed generic-b iteration: the local SpMM result
+    size_t ybuf_cap = 0;          // bytes
     void *halo = nullptr;         // lz::HaloPlan when lz_halo_init was called
     uint64_t *pairs = nullptr;    // per-16-row-strip row order by length (k_strip_pairs)
     int *longq = nullptr;         // k_spmm_seg long-tile queue: [0], [1] counts (alternate calls), [2..] tile ids

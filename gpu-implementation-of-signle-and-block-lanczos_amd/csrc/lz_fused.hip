@@ -932,10 +932,12 @@ int gather_window_ok(lz_handle *h, int64_t n, const int64_t *rp, const int32_t *
 // one 1024 / 768-thread block per CU.  Gather sources past 2^24 rows use the
 // windowed instantiation when every strip's columns fit its window
 // (gather_window_ok), else the 64-bit tile kernel.
+bool fused16_direct(int64_t nx, int win) { return nx < (1 << 24) || win; }
+
 int fused_spmm16(lz_handle *h, int64_t n, const int64_t *rp, const int32_t *col, const double *val,
                  const double *Wg, int64_t nx, const double *Wown, const double *Qbuf, double *Wn,
                  const double *binv, const double *beta, int64_t lc, double *qrow, int *nparts,
-                 const uint64_t *pairs, int64_t nnz, int64_t row_off, int win)
+                 const uint64_t *pairs, int64_t nnz, int64_t row_off, int win, int slab_off)
 {
     const int64_t tiles = ceil_div(n, kFusedRows);
     LZ_ARG_CHECK(tiles >= 1 && tiles < (1LL << 31), "tile count");
@@ -950,7 +952,8 @@ int fused_spmm16(lz_handle *h, int64_t n, const int64_t *rp, const int32_t *col,
         const int ev = prof_begin(h, PROF_SPMM_PASS);
         auto go = [&](auto kern) {  // one folded slab per block, at h->partials2
             hipLaunchKernelGGL(kern, dim3(grid), dim3(64 * (nc + 2)), 0, h->stream, n, rp, col, val, Wg, nx, Wown,
-                               Qbuf, Wn, binv, beta, lc, qrow, h->partials2, h->err_flag, pairs, row_off);
+                               Qbuf, Wn, binv, beta, lc, qrow, h->partials2 + (int64_t)slab_off * 256, h->err_flag,
+                               pairs, row_off);
         };
         if (!wide && buf) go(k_fused_pp16<14, 2376, 3, 2, false>);
         else if (!wide) go(k_fused_pp16<14, 2376, 3, 2, true>);
@@ -961,6 +964,7 @@ int fused_spmm16(lz_handle *h, int64_t n, const int64_t *rp, const int32_t *col,
         *nparts = grid;
         return LZ_OK;
     }
+    LZ_ARG_CHECK(slab_off == 0, "the 64-bit fused pass covers the whole row range (slab_off 0)");
     LZ_TRY(ensure_partials(h, tiles * 256));
     const int ev = prof_begin(h, PROF_SPMM_PASS);
     hipLaunchKernelGGL(k_fused_spmm16<false>, dim3((unsigned)tiles), dim3(512), 0, h->stream, n, rp, col, val, Wg, nx,

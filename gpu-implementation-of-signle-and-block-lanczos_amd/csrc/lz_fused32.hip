@@ -356,9 +356,12 @@ __global__ __launch_bounds__(256) void k_fused_e_gen(int64_t n, int b, const T *
         if (t + 256 * kk < bb) part[(int64_t)blockIdx.x * bb + t + 256 * kk] = acc[kk];
 }
 
-template <typename T>
-__global__ __launch_bounds__(256) void k_fused_u_gen(int64_t n, int b, T *__restrict__ Wn, const T *__restrict__ Wj,
-                                                     const T *__restrict__ P2, double *__restrict__ part)
+// SWAP (the distributed all-gather form): W'' goes to Wj's rows (the rank's
+// slot of the gathered block) and W_j to Wn's (the next step's W_{j-1}); the
+// tile's rows of both are staged in LDS before any store.
+template <typename T, bool SWAP = false>
+__global__ __launch_bounds__(256) void k_fused_u_gen(int64_t n, int b, T *Wn, T *Wj, const T *__restrict__ P2,
+                                                     double *__restrict__ part)
 {
     constexpr int TR = kGenRows, MB = 32;
     __shared__ double sp[MB * MB], tj[TR * MB], tw[TR * MB];
@@ -384,7 +387,12 @@ __global__ __launch_bounds__(256) void k_fused_u_gen(int64_t n, int b, T *__rest
                 double x = tw[e];
                 for (int k = 0; k < b; ++k) x = fma(-tj[r * b + k], sp[k * b + c], x);
                 const T xT = (T)x;
-                Wn[r0 * b + e] = xT;
+                if constexpr (SWAP) {
+                    Wj[r0 * b + e] = xT;
+                    Wn[r0 * b + e] = (T)tj[e];
+                } else {
+                    Wn[r0 * b + e] = xT;
+                }
                 v[kk] = (double)xT;
             }
         }
@@ -434,13 +442,30 @@ int fused_u_sep(lz_handle *h, int64_t n, int b, T *Wn, const T *Wj, const T *P2,
     const int grid = (int)std::max<int64_t>(1, std::min<int64_t>(ceil_div(n, (int64_t)kGenRows), (int64_t)h->n_cu * 2));
     LZ_TRY(ensure_partials(h, (size_t)grid * b * b));
     const int ev = prof_begin(h, PROF_UPDATE_PASS);
-    hipLaunchKernelGGL((k_fused_u_gen<T>), dim3(grid), dim3(256), 0, h->stream, n, b, Wn, Wj, P2, h->partials);
+    hipLaunchKernelGGL((k_fused_u_gen<T>), dim3(grid), dim3(256), 0, h->stream, n, b, Wn, const_cast<T *>(Wj), P2,
+                       h->partials);
     prof_end(h, ev);
     LZ_LAUNCH_CHECK();
     *nparts = grid;
     return LZ_OK;
 }
 
+template <typename T>
+int fused_u_swap_sep(lz_handle *h, int64_t n, int b, T *Wn, T *Xown, const T *P2, int *nparts)
+{
+    LZ_ARG_CHECK(b >= 1 && b <= 32, "fused pass U (swap): 1 <= b <= 32");
+    const int grid = (int)std::max<int64_t>(1, std::min<int64_t>(ceil_div(n, (int64_t)kGenRows), (int64_t)h->n_cu * 2));
+    LZ_TRY(ensure_partials(h, (size_t)grid * b * b));
+    const int ev = prof_begin(h, PROF_UPDATE_PASS);
+    hipLaunchKernelGGL((k_fused_u_gen<T, true>), dim3(grid), dim3(256), 0, h->stream, n, b, Wn, Xown, P2, h->partials);
+    prof_end(h, ev);
+    LZ_LAUNCH_CHECK();
+    *nparts = grid;
+    return LZ_OK;
+}
+
+template int fused_u_swap_sep<double>(lz_handle *, int64_t, int, double *, double *, const double *, int *);
+template int fused_u_swap_sep<float>(lz_handle *, int64_t, int, float *, float *, const float *, int *);
 template int fused_e_sep<double>(lz_handle *, int64_t, int, const double *, const double *, const double *, double *,
                                  const double *, const double *, int64_t, double *, int *);
 template int fused_e_sep<float>(lz_handle *, int64_t, int, const float *, const float *, const float *, float *,

@@ -48,7 +48,12 @@ int copy_row(lz_handle *h, int b, const T *Q, int64_t ld, int col_major, int64_t
 int fused_spmm16(lz_handle *h, int64_t n, const int64_t *rp, const int32_t *col,
                  const double *val, const double *Wg, int64_t nx, const double *Wown, const double *Wprev,
                  double *Wn, const double *binv, const double *P1, int64_t lc, double *qrow, int *nparts,
-                 const uint64_t *pairs, int64_t nnz, int64_t row_off, int win);
+                 const uint64_t *pairs, int64_t nnz, int64_t row_off, int win, int slab_off = 0);
+// slab_off: this launch's folded slabs go to h->partials2 + slab_off * 256 (a
+// pass split over row ranges writes its launches' slabs side by side); the
+// 64-bit fallback (gather source past 2^24 rows, no window) needs slab_off 0.
+// Whether the buffer-addressed kernels (slab per block, at most n_cu) apply:
+bool fused16_direct(int64_t nx, int win);
 // gather source of 2^24+ rows: does every strip's column set fit its window?
 // (row_off: X row of local row 0; synchronises the stream once)
 int gather_window_ok(lz_handle *h, int64_t n, const int64_t *rp, const int32_t *col, int64_t nx, int64_t row_off,
@@ -89,6 +94,9 @@ int fused_e_sep(lz_handle *h, int64_t n, int b, const T *Y, const T *Wj, const T
                 const T *P1, int64_t lc, T *qrow, int *nparts);
 template <typename T>
 int fused_u_sep(lz_handle *h, int64_t n, int b, T *Wn, const T *Wj, const T *P2, int *nparts);
+// the same pass in SWAP form (VALU, any b <= 32): Xown <- W' - Xown P2, Wn <- Xown (old)
+template <typename T>
+int fused_u_swap_sep(lz_handle *h, int64_t n, int b, T *Wn, T *Xown, const T *P2, int *nparts);
 
 // fp64 scalar helpers for the vector Lanczos (lz_fused.hip)
 template <typename T>

@@ -180,6 +180,29 @@ int lz_comm_unique_id(unsigned char out[128]);
 int lz_comm_init(lz_handle *h, int nranks, int rank, const unsigned char id[128]);
 int lz_comm_destroy(lz_handle *h);
 
+/* Virtual ranks: an N-rank decomposition driven from ONE process on one
+ * device, one host thread and one stream per rank (test and rehearsal
+ * support; the reference has no multi-GPU code to mirror).  Every rank's
+ * handle attaches to the group with lz_comm_init_local and then calls the
+ * same entry points an RCCL rank calls (lz_halo_init, lz_block_lanczos_halo,
+ * lz_block_lanczos_dist); the collectives meet at a host barrier and move
+ * data with device copies on the calling rank's stream, ordered by events.
+ * A rank that fails calls lz_comm_abort (or lz_local_group_abort) so that the
+ * others return LZ_E_COMM instead of waiting; a barrier also gives up after
+ * LZ_LOCAL_TIMEOUT_S seconds (default 300).  The group's state lives until
+ * the last attached handle is finalized. */
+typedef struct lz_local_group lz_local_group;  /* opaque */
+int lz_local_group_create(int device, int nranks, lz_local_group **g);
+int lz_local_group_destroy(lz_local_group *g);
+int lz_local_group_abort(lz_local_group *g);
+int lz_comm_init_local(lz_handle *h, lz_local_group *g, int rank);
+/* wake every rank of h's group blocked in a collective (local groups; a no-op for RCCL) */
+int lz_comm_abort(lz_handle *h);
+/* Test support: the interior row range [out[0], out[1]) whose pass 1 ran
+ * beside the exchange in the handle's last distributed solve ({-1, -1}: the
+ * solve ran unsplit). */
+int lz_debug_last_split(lz_handle *h, int64_t out[2]);
+
 /* Distributed block Lanczos, all-gather form (the north star's exchange).
  * Every rank's slab is padded to n_pad rows (n_pad >= max rows per rank) and
  * ncclAllGather places rank g's slab at rows [g*n_pad, (g+1)*n_pad) of X_full,
@@ -192,6 +215,12 @@ int lz_comm_destroy(lz_handle *h);
  *     own slot is where its residual is updated, so the all-gather is in place;
  *   - B_local, W: n_pad x b (rows past n_local are zero padding); W holds the
  *     previous residual W_{j-1}; Q0 and Q1 unused (may be NULL).
+ * Any 1 <= b <= 32 (b = 1 is the single-vector recurrence,
+ * methods/vector_lanczos.hpp:8-67, with alpha[m] / beta[m+1] scalars), fp64 or
+ * fp32: b = 16 fp64 runs the fused passes, other shapes the SpMM plus the
+ * fused dense passes.  Rows that reference only the rank's own rows run
+ * their pass 1 (SpMM) while the all-gather is in flight on the handle's
+ * exchange stream; the rest follow it (LZ_DIST_OVERLAP=0: exchange first).
  * lc_rank: the rank owning row lc (q written there only; other ranks' q
  * untouched).  Outputs alpha/beta identical on every rank.  Gather sources of
  * 2^24+ rows take the windowed fused pass (each strip's columns within 2^23
@@ -215,14 +244,15 @@ int lz_block_lanczos_dist(lz_handle *h, int64_t n_local, int64_t n_pad, int64_t 
 int lz_halo_init(lz_handle *h, int64_t row0, int64_t n_local, const int64_t *recv_counts,
                  const int32_t *halo_rows);
 int lz_halo_sizes(lz_handle *h, int64_t *n_halo, int64_t *n_send);
-/* fill rows [n_local, n_local + n_halo) of X (b = 16 fp64, row-major) from
- * their owners; rows [0, n_local) must hold this rank's block */
+/* fill rows [n_local, n_local + n_halo) of X (b columns, row-major, ld = b)
+ * from their owners; rows [0, n_local) must hold this rank's block */
 int lz_halo_exchange(lz_handle *h, lz_dtype dtype, int b, void *X);
 /* Distributed block Lanczos over the halo plan; replaces the single-GPU
  * block_lanczos_blas (methods/block_lanczos.hpp:88-167) on a row partition.
- * col: compact numbering from lzh_halo_plan.  B_local: n_local x 16; X0, X1:
- * (n_local + n_halo) x 16 workspaces (the residual alternates between them).
- * alpha/beta identical on every rank; q written on lc_rank only. */
+ * col: compact numbering from lzh_halo_plan.  B_local: n_local x b; X0, X1:
+ * (n_local + n_halo) x b workspaces (the residual alternates between them).
+ * alpha/beta identical on every rank; q written on lc_rank only.  Shapes and
+ * the interior / boundary overlap as lz_block_lanczos_dist. */
 int lz_block_lanczos_halo(lz_handle *h, int64_t n_local, int64_t nnz_local, const int64_t *row_ptr,
                           const int32_t *col, const void *val, lz_dtype dtype, int b, int m,
                           int64_t lc_local, int lc_rank, const void *B_local, void *q, void *alpha,

@@ -1,0 +1,226 @@
+"""N-rank decompositions driven natively from ONE GPU (virtual ranks).
+
+Each virtual rank is a host thread with its own stream and its own lz handle,
+attached to an in-process group (lz_local_group_create / lz_comm_init_local):
+the ranks run exactly the entry points an RCCL rank runs -- lz_halo_init's
+count and request exchanges, lz_block_lanczos_halo (owner-side packing, the
+point-to-point round into the halo runs, the compact-column fused pass) and
+lz_block_lanczos_dist (the in-place all-gather, pass 2's SWAP form, the padded
+numbering, the windowed pass 1 past 2^24 gathered rows) -- with the
+collectives moved by device copies instead of RCCL.  Every run is compared
+with the single-process CPU oracle on the global operator
+(methods/block_lanczos.hpp:104-166 op order), and every rank's alpha/beta must
+be bit-identical.
+
+Covered: nnz-balanced uneven slabs (lzh_partition_rows), lc owned by a rank
+other than 0, halos reaching past the neighbours, a power-law operator, the
+interior/boundary split (pass 1 of the interior rows beside the exchange) on
+and off, b in {1, 4, 16} fp64 and b = 32 fp32, and a gathered block of
+2^24+ rows.
+"""
+import os
+
+import numpy as np
+import pytest
+
+from test_gpu_lanczos import assert_close_run
+
+pytestmark = pytest.mark.gpu
+
+
+def _slab(A, r0, r1):
+    rp = A.row_ptr[r0:r1 + 1] - A.row_ptr[r0]
+    k0, k1 = int(A.row_ptr[r0]), int(A.row_ptr[r1])
+    return rp.astype(np.int64), A.col[k0:k1].copy(), A.val[k0:k1].copy()
+
+
+def _owner(bounds, row):
+    return int(np.searchsorted(bounds, row, side="right") - 1)
+
+
+def run_dist(lz, torch, A, B, m, lc, nranks, form, overlap=True, bounds=None):
+    """Run the distributed block Lanczos over `nranks` virtual ranks; returns
+    (q, alpha, beta) of lc's owner, the list of every rank's (alpha, beta), and
+    every rank's split (interior rows) or None."""
+    n, b = B.shape
+    if bounds is None:
+        bounds = lz.partition_rows(A, nranks)
+    bounds = np.asarray(bounds, np.int64)
+    lc_rank = _owner(bounds, lc)
+    n_pad = int(np.max(np.diff(bounds)))
+    dt = torch.float64 if B.dtype == np.float64 else torch.float32
+    val_dt = B.dtype
+    old = os.environ.get("LZ_DIST_OVERLAP")
+    os.environ["LZ_DIST_OVERLAP"] = "1" if overlap else "0"
+
+    def rank_fn(r, h):
+        kw = dict(dtype=dt, device="cuda")
+        r0, r1 = int(bounds[r]), int(bounds[r + 1])
+        nl = r1 - r0
+        rp, col, val = _slab(A, r0, r1)
+        val = val.astype(val_dt)
+        q = torch.zeros(m * b, **kw)
+        al = torch.zeros(m, b, b, **kw)
+        be = torch.zeros(m + 1, b, b, **kw)
+        Bl = torch.from_numpy(np.ascontiguousarray(B[r0:r1])).cuda()
+        if form == "halo":
+            ccol, cnt, rows = lz.halo_plan(col, bounds, r)
+            h.halo_init(r0, nl, cnt, rows)
+            nh = int(rows.size)
+            assert h.halo_sizes()[0] == nh
+            Ad = lz.CsrDevice.from_host(lz.CsrHost(nl, rp, ccol, val), n_cols=nl + nh)
+            X0 = torch.zeros(nl + nh, b, **kw)
+            X1 = torch.zeros(nl + nh, b, **kw)
+            h.block_lanczos_halo(Ad, Bl, m, lc - bounds[lc_rank], lc_rank, q, al, be, X0, X1)
+        else:
+            pcol = lz.remap_cols_padded(col, bounds, n_pad)
+            Ad = lz.CsrDevice.from_host(lz.CsrHost(nl, rp, pcol, val), n_cols=n_pad * nranks)
+            Bp = torch.zeros(n_pad, b, **kw)
+            Bp[:nl] = Bl
+            W = torch.zeros(n_pad, b, **kw)
+            X = torch.zeros(n_pad * nranks, b, **kw)
+            h.block_lanczos_dist(Ad, n_pad, n_pad * nranks, Bp, m, lc - bounds[lc_rank], lc_rank, q, al, be,
+                                 None, W, X)
+        assert h.device_error() == 0
+        return q.cpu().numpy(), al.cpu().numpy(), be.cpu().numpy(), h.last_split()
+
+    try:
+        res = lz.run_virtual_ranks(nranks, rank_fn)
+    finally:
+        if old is None:
+            os.environ.pop("LZ_DIST_OVERLAP", None)
+        else:
+            os.environ["LZ_DIST_OVERLAP"] = old
+    for r in range(1, nranks):  # every rank holds the same alpha / beta bits
+        assert np.array_equal(res[r][1], res[0][1]) and np.array_equal(res[r][2][:m], res[0][2][:m]), r
+    q, al, be, _ = res[lc_rank]
+    return (q, al, be), [x[3] for x in res]
+
+
+@pytest.mark.parametrize("form", ["halo", "allgather"])
+@pytest.mark.parametrize("nranks", [2, 4, 8])
+def test_vranks_b16_banded(lz, orc, torch_cuda, form, nranks):
+    """Banded operator, nnz-balanced slabs, lc on a rank other than 0; the
+    interior rows' pass 1 runs beside the exchange (split must be on)."""
+    A = lz.gen_banded(120_011, 10.0, 1500, seed=100 + nranks)
+    B = lz.uniform_B(A.n, 16, seed=7)
+    m, lc = 7, 120_011 * 5 // 8 + 3
+    got, splits = run_dist(lz, torch_cuda, A, B, m, lc, nranks, form)
+    assert all(s is not None for s in splits), splits  # every rank split its rows
+    assert_close_run(lz, m, 16, got, orc.block_lanczos(A, B, m, lc))
+
+
+@pytest.mark.parametrize("form", ["halo", "allgather"])
+def test_vranks_b16_overlap_off_equals_on(lz, orc, torch_cuda, form):
+    """LZ_DIST_OVERLAP=0 (exchange, then the whole pass) against the split run:
+    both match the oracle; the halos reach past the neighbouring ranks."""
+    A = lz.gen_banded(48_007, 10.0, 9000, seed=11)  # half width > rows per rank at 8 ranks
+    B = lz.uniform_B(A.n, 16, seed=12)
+    m, lc = 6, 47_000
+    ref = orc.block_lanczos(A, B, m, lc)
+    for ov in (False, True):
+        got, splits = run_dist(lz, torch_cuda, A, B, m, lc, 8, form, overlap=ov)
+        if not ov:
+            assert all(s is None for s in splits)
+        assert_close_run(lz, m, 16, got, ref)
+
+
+@pytest.mark.parametrize("form", ["halo", "allgather"])
+def test_vranks_b16_powerlaw(lz, orc, torch_cuda, form):
+    """Power-law rows (config C5's generator, fp64): rows everywhere reach other
+    ranks, so the split is off on most ranks and the halo is most of the block."""
+    A = lz.gen_powerlaw(40_009, 10.0, 2.1, 5000, seed=13, dtype=np.float64)
+    B = lz.uniform_B(A.n, 16, seed=14)
+    m, lc = 5, 123
+    got, _ = run_dist(lz, torch_cuda, A, B, m, lc, 4, form)
+    assert_close_run(lz, m, 16, got, orc.block_lanczos(A, B, m, lc))
+
+
+@pytest.mark.parametrize("form", ["halo", "allgather"])
+@pytest.mark.parametrize("b", [1, 4])
+@pytest.mark.parametrize("nranks", [2, 4])
+def test_vranks_generic_b(lz, orc, torch_cuda, form, b, nranks):
+    """b = 1 (the single-vector recurrence, methods/vector_lanczos.hpp:8-67) and
+    the reference driver's N_COL = 4 (test_lanczos.cu:5), fp64."""
+    A = lz.gen_banded(30_011, 10.0, 800, seed=20 + b)
+    B = lz.uniform_B(A.n, b, seed=21)
+    m, lc = 8, 30_011 - 5
+    got, splits = run_dist(lz, torch_cuda, A, B, m, lc, nranks, form)
+    assert all(s is not None for s in splits)
+    assert_close_run(lz, m, b, got, orc.block_lanczos(A, B, m, lc))
+    if b == 1:  # the same numbers as the single-vector oracle
+        qv, av, bv = orc.vector_lanczos(A, B[:, 0], m, lc)
+        assert np.allclose(got[1].ravel(), av, rtol=1e-9, atol=1e-12)
+        assert np.allclose(got[2].ravel()[:m], bv, rtol=1e-9, atol=1e-12)
+        assert np.allclose(got[0], qv, rtol=1e-9, atol=1e-12)
+
+
+@pytest.mark.parametrize("form", ["halo", "allgather"])
+def test_vranks_b32_f32(lz, orc, torch_cuda, form):
+    """b = 32 fp32 (config C5's shape) at 2 ranks: MFMA pass E, VALU pass U / SWAP."""
+    A = lz.gen_banded(20_011, 10.0, 600, seed=30, dtype=np.float32)
+    B = lz.uniform_B(A.n, 32, seed=31, dtype=np.float32)
+    m, lc = 5, 15_000
+    got, _ = run_dist(lz, torch_cuda, A, B, m, lc, 2, form)
+    qo, ao, bo = orc.block_lanczos(A, B, m, lc)
+    q, al, be = got
+    scale = max(1.0, float(np.abs(ao).max()), float(np.abs(bo[:m]).max()))
+    assert np.max(np.abs(al - ao)) <= 1e-4 * scale
+    assert np.max(np.abs(be[:m] - bo[:m])) <= 1e-4 * scale
+    assert np.allclose(q, qo, rtol=1e-4, atol=1e-4 * np.abs(qo).max())
+
+
+def test_vranks_allgather_wide_window(lz, orc, torch_cuda):
+    """8 ranks whose gathered block has 8 * n_pad >= 2^24 rows (2.2 GB at b = 16
+    fp64): pass 1 gathers through its 2^24-row window, interior split on."""
+    n = 8 * ((1 << 21) + 1000)
+    A = lz.gen_banded(n, 3.0, 200, seed=41)
+    B = lz.uniform_B(A.n, 16, seed=42)
+    m, lc = 3, n - 77
+    got, splits = run_dist(lz, torch_cuda, A, B, m, lc, 8, "allgather")
+    assert all(s is not None for s in splits)
+    assert_close_run(lz, m, 16, got, orc.block_lanczos(A, B, m, lc))
+
+
+@pytest.mark.parametrize("b,dtype", [(4, np.float32), (16, np.float64), (3, np.float64)])
+def test_vranks_halo_exchange_rows(lz, torch_cuda, b, dtype):
+    """lz_halo_exchange alone at 3 ranks: every halo row equals its owner's row."""
+    torch = torch_cuda
+    A = lz.gen_banded(9_001, 6.0, 2000, seed=50)
+    bounds = np.array([0, 2000, 6500, 9001], np.int64)
+    G = np.arange(A.n * b, dtype=dtype).reshape(A.n, b) / 7.0
+    tdt = torch.float32 if dtype == np.float32 else torch.float64
+
+    def rank_fn(r, h):
+        r0, r1 = int(bounds[r]), int(bounds[r + 1])
+        _, col, _ = _slab(A, r0, r1)
+        _, cnt, rows = lz.halo_plan(col, bounds, r)
+        h.halo_init(r0, r1 - r0, cnt, rows)
+        X = torch.zeros(r1 - r0 + rows.size, b, dtype=tdt, device="cuda")
+        X[: r1 - r0] = torch.from_numpy(G[r0:r1]).cuda()
+        h.halo_exchange(X)
+        return X.cpu().numpy(), rows
+
+    for r, (X, rows) in enumerate(lz.run_virtual_ranks(3, rank_fn)):
+        nl = int(bounds[r + 1] - bounds[r])
+        assert np.array_equal(X[nl:], G[rows.astype(np.int64)]), r
+
+
+def test_vranks_failing_rank_aborts_group(lz, torch_cuda):
+    """A rank that fails before a collective aborts the group: the others
+    return an error (LZ_E_COMM) instead of waiting at the barrier."""
+    import time
+    A = lz.gen_banded(4_000, 5.0, 100, seed=60)
+    bounds = np.array([0, 2000, 4000], np.int64)
+
+    def rank_fn(r, h):
+        if r == 1:
+            raise RuntimeError("rank 1 fails on purpose")
+        _, col, _ = _slab(A, 0, 2000)
+        _, cnt, rows = lz.halo_plan(col, bounds, 0)
+        h.halo_init(0, 2000, cnt, rows)  # collective: rank 1 never arrives
+
+    t0 = time.time()
+    with pytest.raises(lz.LanczosError):
+        lz.run_virtual_ranks(2, rank_fn)
+    assert time.time() - t0 < 60
