@@ -78,34 +78,105 @@ def fused_kernel(nnz, n):
     return f"k_fused_pp16<{shape},{'true' if win else 'false'}>", "k_fused_pp16"
 
 
+PASS2_KERNEL = "k_fused_update16<true,8,false>"  # the single-GPU pass 2 (lz_fused.hip fused_update16)
+
+
 def spmm_kernel(nnz, n):
     """The plain SpMM kernel lz_csr_spmm launches for b = 16 fp64 (lz_spmm.hip launch_spmm_rm)."""
     cap = 1536 if nnz > 13.0 * n else 768
     win = n >= (1 << 24)
-    return f"k_spmm_seg<double,16,48,{cap},{'true' if win else 'false'},0>"
+    return f"k_spmm_seg<double,16,48,{cap},{'true' if win else 'false'},0,false,false>"
 
 
-def pmc_record(kind, kernel, n, nnz, hw):
+# the source file of each profiled kernel: a committed counter file is used only
+# while that file is byte-identical to the one profiled (profiles record its sha256)
+KERNEL_SRC = {"k_fused_pp16": "lz_fused.hip", "k_fused_update16": "lz_fused.hip", "k_spmm_seg": "lz_spmm.hip",
+              "k_fused_el32": "lz_fused32.hip", "k_fused_ub32": "lz_fused32.hip", "k_gram16_f64": "lz_dense.hip",
+              "k_gram32_f32": "lz_dense.hip"}
+CSRC = os.path.join(ROOT, "gpu-implementation-of-signle-and-block-lanczos_amd", "csrc")
+
+
+def source_sha(kernel):
+    import hashlib
+    f = next((v for k, v in KERNEL_SRC.items() if kernel.startswith(k)), None)
+    if not f:
+        return None
+    return hashlib.sha256(open(os.path.join(CSRC, f), "rb").read()).hexdigest()[:16]
+
+
+def _norm(name):
+    return name.replace(" ", "").replace("lz::", "").replace("void", "").split("(")[0]
+
+
+def pmc_record(kind, kernel, n, nnz, hw, kernel_full=None):
     """A committed rocprofv3 PMC summary (profiles/*_pmc_<kind>_<kernel>.json or,
-    kind "", profiles/*_pmc_<kernel>.json) of this bench's workload, newest first."""
+    kind "", profiles/*_pmc_<kernel>.json) of this bench's workload, newest first.
+    Refused (None, reason) unless it names the kernel instantiation this run
+    launches (kernel_full) and was taken on the current source of that kernel."""
     pat = f"*_pmc_{kind + '_' if kind else ''}{kernel}.json"
+    reason = "no committed counter file for this workload"
     for f in sorted(glob.glob(os.path.join(ROOT, "profiles", pat)), reverse=True):
         try:
             d = json.load(open(f))
         except (OSError, ValueError):
             continue
         w = d.get("workload", {})
-        if w.get("n") == n and w.get("nnz") == nnz and w.get("halfwidth") == hw:
-            return d, os.path.relpath(f, ROOT)
-    return None, None
+        if not (w.get("n") == n and w.get("nnz") == nnz and w.get("halfwidth") == hw):
+            continue
+        rel = os.path.relpath(f, ROOT)
+        if _norm(d.get("kernel_full", "")) != _norm(kernel_full or kernel):
+            reason = f"{rel}: kernel {d.get('kernel_full')!r} is not the launched {kernel_full!r}"
+            continue
+        if d.get("source_sha") is None or d.get("source_sha") != source_sha(kernel):
+            reason = f"{rel}: taken on another source of {KERNEL_SRC.get(kernel, '?')} (stale)"
+            continue
+        return d, rel
+    return None, reason
 
 
-def pmc_traffic(kernel, n, nnz, hw):
+def pmc_traffic(kernel, n, nnz, hw, kernel_full=None):
     """HBM bytes per launch of `kernel` from the committed PMC summary (separate
     FETCH_SIZE / WRITE_SIZE passes, FETCH_SIZE doubled per MI355X_MICROARCH.md's
-    gfx950 note; scripts/pmc_traffic.py).  None unless taken on this workload."""
-    d, src = pmc_record("", kernel, n, nnz, hw)
-    return (d.get("hbm_bytes_per_launch"), src) if d else (None, None)
+    gfx950 note; scripts/pmc_traffic.py).  (None, reason) unless taken on this
+    workload, this kernel instantiation and this source."""
+    d, src = pmc_record("", kernel, n, nnz, hw, kernel_full)
+    return (d.get("hbm_bytes_per_launch"), src) if d else (None, src)
+
+
+def host_cpu():
+    try:
+        for line in open("/proc/cpuinfo"):
+            if line.startswith("model name"):
+                return line.split(":", 1)[1].strip()
+    except OSError:
+        pass
+    return "unknown"
+
+
+def cpu_stats(t_each, unit_per_s=1.0):
+    """best / mean / worst rate of per-iteration wall times (the first one warms up)."""
+    s = np.asarray(t_each[1:] if len(t_each) > 1 else t_each, dtype=float)
+    return {"value": round(unit_per_s / float(s.min()), 4), "mean": round(unit_per_s / float(s.mean()), 4),
+            "worst": round(unit_per_s / float(s.max()), 4), "samples": int(s.size)}
+
+
+def compare_run(lz, m, b, got, ref, tol_rel, ritz_tol):
+    """alpha / beta / q / Ritz of the first m steps against the oracle's."""
+    al, be, q = got
+    ao, bo, qo = ref
+    al, be = np.asarray(al[:m], np.float64), np.asarray(be[:m + 1], np.float64)
+    ao, bo = np.asarray(ao, np.float64), np.asarray(bo, np.float64)
+    scale = max(1.0, float(np.abs(ao).max()), float(np.abs(bo[:m]).max()))
+    r_gpu = lz.ritz_values(m, b, al, be)
+    r_cpu = lz.ritz_values(m, b, ao, bo)
+    res = {"steps_checked": m, "max_dalpha_rel": float(np.max(np.abs(al - ao)) / scale),
+           "max_dbeta_rel": float(np.max(np.abs(be[:m] - bo[:m])) / scale),
+           "max_dritz": float(np.max(np.abs(r_gpu - r_cpu))), "tol_rel": tol_rel, "ritz_tol": ritz_tol}
+    if q is not None:
+        res["max_dq"] = float(np.max(np.abs(np.asarray(q[: qo.size], np.float64) - qo)))
+    res["ok"] = bool(res["max_dalpha_rel"] <= tol_rel and res["max_dbeta_rel"] <= tol_rel
+                     and res["max_dritz"] <= ritz_tol)
+    return res
 
 
 def parse_args():
@@ -123,7 +194,9 @@ def parse_args():
                     help="oracle iterations after the start-up step; the first is a warm-up, the "
                          "CPU baseline is the best of the rest (BASELINE.md 3: best of 5; c3 default 6, "
                          "c4 default 2: BASELINE.md reports the C4 CPU baseline at C3 scale only)")
-    ap.add_argument("--no-cpu-baseline", action="store_true", help="skip the oracle leg (CPU baseline + parity)")
+    ap.add_argument("--no-cpu-baseline", action="store_true",
+                    help="N = 1: skip the oracle legs (CPU baselines + parity); N > 1 always checks parity")
+    ap.add_argument("--parity-steps", type=int, default=3, help="N > 1: steps checked against the oracle")
     ap.add_argument("--spmm-reps", type=int, default=20)
     ap.add_argument("--c2-steps", type=int, default=None, help="single-vector Lanczos steps at BASELINE config 1 (0: skip)")
     ap.add_argument("--c5-steps", type=int, default=None, help="block-32 fp32 power-law steps at BASELINE config 4 (0: skip)")
@@ -285,6 +358,32 @@ def main():
     if h.device_error() != 0:
         raise RuntimeError("device error word set in the breakdown run")
 
+    # ---- N > 1: the first steps against the CPU oracle on the GLOBAL operator (rank 0
+    # builds it; every rank learns the verdict).  A multi-GPU line is never printed
+    # unchecked.
+    ref_g = None
+    parity = None
+    if world > 1:
+        m_chk = min(K, args.parity_steps)
+        verdict = [None]
+        if rank == 0:
+            t_o = time.time()
+            A_g = lz.gen_banded(n_total, args.nnz_per_row, args.halfwidth, seed)
+            B_g = lz.uniform_B(n_total, b, seed)
+            orc = ge.load_oracle()
+            qo, ao, bo = orc.block_lanczos(A_g, B_g, m_chk, lc)
+            ref_g = (ao, bo, qo)
+            del A_g, B_g
+            parity = compare_run(lz, m_chk, b, (al_gpu, be_gpu, q_gpu), ref_g, 1e-9, RITZ_TOL)
+            parity.update({"device_error": err, "against": f"oracle/lz_oracle.c on the global n={n_total} operator "
+                                                           f"and start block (rank 0), {world} ranks' result",
+                           "oracle_s": round(time.time() - t_o, 1)})
+            log(f"N>1 parity: {parity}")
+            verdict = [parity["ok"]]
+        dist.broadcast_object_list(verdict, src=0)
+        if not verdict[0]:
+            raise RuntimeError(f"multi-GPU parity check against the oracle failed: {parity}")
+
     # ---- N > 1: the other exchange form (halo <-> the north star's all-gather) on the same partition
     other = None
     if world > 1 and not args.no_second_exchange:
@@ -296,9 +395,18 @@ def main():
         if h.device_error() != 0:
             raise RuntimeError(f"device error word set in the {ex2} run")
         a2 = alpha[:K].cpu().numpy()
+        b2_ = beta[: K + 1].cpu().numpy()
+        q2_ = q[: K * b].cpu().numpy()
         other = {"exchange": ex2, "parallelism": par2, "iters_per_s": round(K / el2, 3),
                  "ms_per_step": round(el2 / K * 1e3, 4),
                  "max_dalpha_vs_headline": float(np.max(np.abs(a2 - al_gpu)))}
+        verdict = [None]
+        if rank == 0:
+            other["parity"] = compare_run(lz, min(K, args.parity_steps), b, (a2, b2_, q2_), ref_g, 1e-9, RITZ_TOL)
+            verdict = [other["parity"]["ok"]]
+        dist.broadcast_object_list(verdict, src=0)
+        if not verdict[0]:
+            raise RuntimeError(f"{ex2} exchange: parity check against the oracle failed: {other}")
         del run2
 
     # ---- plain SpMM kernel (the BASELINE headline kernel) on the same operator
@@ -318,23 +426,35 @@ def main():
         plain = {"kernel": spmm_kernel(A.nnz, n), "avg_ms": round(ms / cnt, 4),
                  "bytes_per_launch": spmm_bytes(n, A.nnz, b), "achieved_GBs": round(gbs, 1),
                  "frac_of_hbm_peak": round(gbs / HBM_PEAK_GBS, 4)}
+        if not args.no_cpu_baseline:  # the CPU SpMM on the same operator and block
+            orc = ge.load_oracle()
+            Yc, tc = orc.csr_spmm_timed(A, B, reps=3)
+            Yg = Y.cpu().numpy()
+            plain["parity_max_rel"] = float(np.max(np.abs(Yg - Yc)) / max(1e-300, float(np.abs(Yc).max())))
+            if not plain["parity_max_rel"] <= 1e-12:
+                raise RuntimeError(f"plain SpMM differs from the oracle: {plain['parity_max_rel']}")
+            plain["cpu_baseline"] = {"value": round(spmm_bytes(n, A.nnz, b) / tc / 1e9, 2), "unit": "GB/s",
+                                     "ms": round(tc * 1e3, 2), "cores": orc.num_threads(), "kind": "port",
+                                     "sample": "best of 3 oracle CSR SpMMs (OpenMP over rows), same A and block"}
+            del Yc, Yg
         del Y
 
     # ---- CPU oracle on the same operator and start block, rank 0, N = 1: the CPU
     # baseline (best of the timed iterations) and the bench's own parity check
-    cpu = parity = None
+    cpu = None
     if world == 1 and not args.no_cpu_baseline:
         orc = ge.load_oracle()
         m_o = min(K, 1 + max(1, args.cpu_iters))
         t_o = time.time()
         qo, ao, bo, t_each = orc.block_lanczos_timed(A, B, m_o, lc)
         log(f"oracle: {m_o} steps in {time.time() - t_o:.1f}s")
-        samples = t_each[1:] if t_each.size > 1 else t_each  # the first iteration warms the caches
-        cpu = {"value": round(1.0 / float(samples.min()), 4), "unit": "iters/s", "cores": orc.num_threads(),
-               "kind": "port", "mean_iters_per_s": round(1.0 / float(samples.mean()), 4),
-               "sample": f"best of {samples.size} block-Lanczos iterations (after the start-up step and one "
+        st_ = cpu_stats(t_each)  # the first iteration warms the caches
+        cpu = {"value": st_["value"], "unit": "iters/s", "cores": orc.num_threads(), "kind": "port",
+               "mean_iters_per_s": st_["mean"], "worst_iters_per_s": st_["worst"], "host_cpu": host_cpu(),
+               "sample": f"best of {st_['samples']} block-Lanczos iterations (after the start-up step and one "
                          f"warm-up iteration) of the same n={n} nnz={A.nnz} b={b} fp64 operator and start "
-                         f"block, oracle/lz_oracle.c OpenMP"}
+                         f"block, oracle/lz_oracle.c OpenMP; host cores are shared on this pool, so the rate "
+                         f"varies between boxes (r02: 1.85-5.31 it/s)"}
         scale = max(1.0, np.abs(ao).max(), np.abs(bo[:m_o]).max())
         r_gpu = lz.ritz_values(m_o, b, al_gpu[:m_o], be_gpu[: m_o + 1])
         r_cpu = lz.ritz_values(m_o, b, ao, bo)
@@ -368,6 +488,26 @@ def main():
               "iters_per_s": round(k2 / dt2, 1), "us_per_iter": round(dt2 / k2 * 1e6, 2),
               "iteration_GBs": round((A2.nnz * 12 + (n2 + 1) * 8 + 5 * n2 * 8) / (dt2 / k2) / 1e9, 1),
               "note": "A + 5 n s bytes per step (A, w read, q_{j-1} read, q_j written, w' written)"}
+        if not args.no_cpu_baseline:
+            orc = ge.load_oracle()
+            m2 = min(k2, 12)
+            bvh = b2.cpu().numpy()
+            qo2, ao2, bo2, t2 = orc.vector_lanczos_timed(A2, bvh, m2, 84)
+            c2["parity"] = compare_run(lz, m2, 1, (al2.cpu().numpy()[:m2].reshape(m2, 1, 1),
+                                                   np.r_[be2.cpu().numpy()[:m2], 0.0].reshape(m2 + 1, 1, 1),
+                                                   q2.cpu().numpy()[:m2]),
+                                       (ao2.reshape(m2, 1, 1), np.r_[bo2, 0.0].reshape(m2 + 1, 1, 1), qo2),
+                                       1e-9, RITZ_TOL)
+            if not c2["parity"]["ok"]:
+                raise RuntimeError(f"C2 parity check failed: {c2['parity']}")
+            st2 = cpu_stats(t2)
+            _, ts2 = orc.csr_spmm_timed(A2, bvh[:, None], reps=5)
+            c2["cpu_baseline"] = {"value": st2["value"], "unit": "iters/s", "mean": st2["mean"], "worst": st2["worst"],
+                                  "cores": orc.num_threads(), "kind": "port", "host_cpu": host_cpu(),
+                                  "spmv_GBs": round(spmm_bytes(n2, A2.nnz, 1) / ts2 / 1e9, 2),
+                                  "sample": f"best of {st2['samples']} single-vector iterations (after one warm-up) of "
+                                            f"the same operator and start vector, oracle/lz_oracle.c OpenMP "
+                                            f"(deterministic chunked dots); spmv_GBs: best of 5 oracle SpMVs"}
         del A2d, v0, v1, v2
 
     # ---- BASELINE config 4 (block Lanczos b=32 fp32, power-law rows): an extra line
@@ -390,9 +530,27 @@ def main():
                           f"nnz={A5.nnz}, max row {int(np.diff(A5.row_ptr).max())}",
               "iters_per_s": round(k5 / dt5, 2), "ms_per_iter": round(dt5 / k5 * 1e3, 3),
               "finite": bool(torch.isfinite(al5).all())}
+        if not args.no_cpu_baseline:  # fp32: 1e-4 relative
+            orc = ge.load_oracle()
+            m5 = min(k5, 4)
+            B5h = B5.cpu().numpy()
+            qo5, ao5, bo5, t5 = orc.block_lanczos_timed(A5, B5h, m5, 84)
+            scale5 = max(1.0, float(np.abs(ao5).max()), float(np.abs(bo5[:m5]).max()))
+            c5["parity"] = compare_run(lz, m5, 32, (al5.cpu().numpy(), be5.cpu().numpy(), q5.cpu().numpy()),
+                                       (ao5, bo5, qo5), 1e-4, 1e-4 * scale5)
+            if not c5["parity"]["ok"]:
+                raise RuntimeError(f"C5 parity check failed: {c5['parity']}")
+            st5 = cpu_stats(t5)
+            _, ts5 = orc.csr_spmm_timed(A5, B5h, reps=2)
+            c5["cpu_baseline"] = {"value": st5["value"], "unit": "iters/s", "mean": st5["mean"], "worst": st5["worst"],
+                                  "cores": orc.num_threads(), "kind": "port", "host_cpu": host_cpu(),
+                                  "spmm_GBs": round(spmm_bytes(n5, A5.nnz, 32, 4) / ts5 / 1e9, 2),
+                                  "sample": f"best of {st5['samples']} fp32 block iterations (after the start-up "
+                                            f"step and one warm-up) of the same operator and start block, "
+                                            f"oracle/lz_oracle.c OpenMP; spmm_GBs: best of 2 oracle SpMMs"}
         # MFMA utilisation of the C5 dense step (v_mfma_f32_32x32x2_f32), committed PMC passes
         for kern in ("k_fused_el32", "k_fused_ub32"):  # the beta^2 form's passes (the default at b = 32)
-            d, src = pmc_record("mfma", kern, n5, A5.nnz, 0)
+            d, src = pmc_record("mfma", kern, n5, A5.nnz, 0, kern)
             if d:
                 c5.setdefault("mfma", {})[kern] = {"pmc_MfmaUtil_pct": d.get("MfmaUtil_pct"),
                                                    "mfma_flop_per_launch": d.get("mfma_flop_per_launch"),
@@ -429,13 +587,28 @@ def main():
                "spmm_GBs": round(spmm_bytes(n, Ar.nnz, b) / t_sp / 1e9, 1),
                "spmm_frac_of_hbm_peak": round(spmm_bytes(n, Ar.nnz, b) / t_sp / 1e9 / HBM_PEAK_GBS, 4),
                "finite": bool(torch.isfinite(alr).all())}
+        if not args.no_cpu_baseline:
+            orc = ge.load_oracle()
+            mr = min(kr, 3)
+            qor, aor, bor, tr = orc.block_lanczos_timed(Ar, B, mr, 84)
+            c3r["parity"] = compare_run(lz, mr, b, (alr.cpu().numpy(), ber.cpu().numpy(), qr.cpu().numpy()),
+                                        (aor, bor, qor), 1e-9, RITZ_TOL)
+            if not c3r["parity"]["ok"]:
+                raise RuntimeError(f"C3 random-column parity check failed: {c3r['parity']}")
+            str_ = cpu_stats(tr)
+            c3r["cpu_baseline"] = {"value": str_["value"], "unit": "iters/s", "mean": str_["mean"],
+                                   "cores": orc.num_threads(), "kind": "port", "host_cpu": host_cpu(),
+                                   "sample": f"best of {str_['samples']} block iterations of the same operator, "
+                                             f"oracle/lz_oracle.c OpenMP"}
         # measured HBM traffic of this SpMM (committed PMC passes of the same operator): re-fetched
         # bytes, NOT algorithmic throughput
-        tr_r, src_r = pmc_traffic("k_spmm_seg_random_columns", n, Ar.nnz, n)
+        tr_r, src_r = pmc_traffic("k_spmm_seg_random_columns", n, Ar.nnz, n, spmm_kernel(Ar.nnz, n))
         if tr_r:
             c3r.update({"spmm_pmc_hbm_bytes": tr_r, "spmm_pmc_refetch_ratio": round(tr_r / spmm_bytes(n, Ar.nnz, b), 2),
                         "spmm_pmc_hbm_GBs_incl_refetch": round(tr_r / t_sp / 1e9, 1),
                         "pmc_source": src_r})
+        else:
+            c3r["spmm_pmc_note"] = src_r
         del Ard, Yr, Pr
 
     if rank == 0:
@@ -448,7 +621,7 @@ def main():
         if fused and t_pass:
             ach = fused_pass_bytes(n, A.nnz, b) / t_pass / 1e9
             kname, kshort = fused_kernel(A.nnz, n)
-            traffic, tsrc = pmc_traffic(kshort, n, A.nnz, hw)
+            traffic, tsrc = pmc_traffic(kshort, n, A.nnz, hw, kname)
             roof = {"bound": "hbm", "kernel": kname, "achieved": round(ach, 1),
                     "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": round(ach / HBM_PEAK_GBS, 4),
                     "traffic": traffic, "traffic_unit": "bytes/launch", "traffic_source": tsrc,
@@ -458,14 +631,17 @@ def main():
             # against the fp64 MFMA peak, plus the rocprofv3 MfmaUtil counter of the same kernels
             mfma = {"unit": "TFLOP/s", "peak": FP64_MFMA_PEAK_TFS, "dtype": "f64 (v_mfma_f64_16x16x4f64)",
                     "pass2_update_gram": None, "pass1_epilogue": None}
-            for key, kern, fl, t in (("pass2_update_gram", "k_fused_update16", PASS2_MFMA_FLOP_PER_ROW, t_upd),
-                                     ("pass1_epilogue", kshort, PASS1_MFMA_FLOP_PER_ROW, t_pass)):
+            for key, kern, kfull, fl, t in (("pass2_update_gram", "k_fused_update16", PASS2_KERNEL,
+                                             PASS2_MFMA_FLOP_PER_ROW, t_upd),
+                                            ("pass1_epilogue", kshort, kname, PASS1_MFMA_FLOP_PER_ROW, t_pass)):
                 if not t:
                     continue
                 tf = fl * n / t / 1e12
                 ent = {"kernel": kern, "mfma_flop_per_launch": fl * n, "avg_ms": round(t * 1e3, 4),
                        "achieved": round(tf, 3), "frac": round(tf / FP64_MFMA_PEAK_TFS, 4)}
-                d, src = pmc_record("mfma", kern, n, A.nnz, hw)
+                d, src = pmc_record("mfma", kern, n, A.nnz, hw, kfull)
+                if not d:
+                    ent["pmc_note"] = src
                 if d:
                     ent.update({"pmc_MfmaUtil_pct": d.get("MfmaUtil_pct"),
                                 "pmc_mfma_flop_per_launch": d.get("mfma_flop_per_launch"), "pmc_source": src})

@@ -50,6 +50,10 @@ def lib():
             "lzo_fdtd_block": (_c_int, [_c_i64, _c_vp, _c_vp, _c_vp, _c_int, _c_vp, _c_i64, _c_dbl, _c_i64, _c_vp]),
             "lzo_block_lanczos_timed": (_c_int, [_c_i64, _c_vp, _c_vp, _c_vp, _c_int, _c_int, _c_i64, _c_vp, _c_vp,
                                                  _c_vp, _c_vp, _c_vp]),
+            "lzo_block_lanczos_f32_timed": (_c_int, [_c_i64, _c_vp, _c_vp, _c_vp, _c_int, _c_int, _c_i64, _c_vp,
+                                                     _c_vp, _c_vp, _c_vp, _c_vp]),
+            "lzo_vector_lanczos_timed": (_c_int, [_c_i64, _c_vp, _c_vp, _c_vp, _c_int, _c_i64, _c_vp, _c_vp, _c_vp,
+                                                  _c_vp, _c_vp]),
         }
         for k, (r, a) in sig.items():
             f = getattr(L, k)
@@ -163,19 +167,55 @@ def fdtd_block(A, B, steps, T_end, lc):
 
 def block_lanczos_timed(A, B: np.ndarray, m: int, lc: int):
     """block_lanczos restated, with the wall seconds of each iteration j = 1..m-1
-    (the start-up step untimed): (q, alpha, beta, t_each[m-1])."""
+    (the start-up step untimed): (q, alpha, beta, t_each[m-1]).  fp32 when B is
+    float32."""
     rp, col, val = _csr(A)
-    B = np.ascontiguousarray(B, np.float64)
+    f32 = np.asarray(B).dtype == np.float32
+    dt = np.float32 if f32 else np.float64
+    B = np.ascontiguousarray(B, dt)
     n, b = B.shape
-    q = np.zeros(m * b)
-    alpha = np.zeros((m, b, b))
-    beta = np.zeros((m + 1, b, b))
+    q = np.zeros(m * b, dt)
+    alpha = np.zeros((m, b, b), dt)
+    beta = np.zeros((m + 1, b, b), dt)
     t = np.zeros(max(m - 1, 1))
-    rc = lib().lzo_block_lanczos_timed(n, _p(rp), _p(col), _p(val.astype(np.float64)), b, m, lc, _p(B), _p(q),
-                                       _p(alpha), _p(beta), _p(t))
+    fn = lib().lzo_block_lanczos_f32_timed if f32 else lib().lzo_block_lanczos_timed
+    rc = fn(n, _p(rp), _p(col), _p(val.astype(dt, copy=False)), b, m, lc, _p(B), _p(q), _p(alpha), _p(beta), _p(t))
     if rc:
         raise RuntimeError(f"lzo_block_lanczos_timed rc={rc}")
     return q, alpha, beta, t[: m - 1]
+
+
+def vector_lanczos_timed(A, bvec: np.ndarray, m: int, lc: int):
+    """vector_lanczos restated (fp64) with the wall seconds of each iteration j = 1..m-1."""
+    rp, col, val = _csr(A)
+    bvec = np.ascontiguousarray(bvec, np.float64).ravel()
+    q, alpha, beta = np.zeros(m), np.zeros(m), np.zeros(m)
+    t = np.zeros(max(m - 1, 1))
+    rc = lib().lzo_vector_lanczos_timed(A.n, _p(rp), _p(col), _p(val.astype(np.float64, copy=False)), m, lc,
+                                        _p(bvec), _p(q), _p(alpha), _p(beta), _p(t))
+    if rc:
+        raise RuntimeError(f"lzo_vector_lanczos_timed rc={rc}")
+    return q, alpha, beta, t[: m - 1]
+
+
+def csr_spmm_timed(A, X: np.ndarray, reps: int = 3):
+    """(Y, best seconds) of `reps` oracle SpMMs Y = A X (OpenMP over rows; X row-major)."""
+    import time
+    rp, col, val = _csr(A)
+    X = np.ascontiguousarray(X)
+    b = X.shape[1]
+    f32 = X.dtype == np.float32
+    v = val.astype(np.float32 if f32 else np.float64, copy=False)
+    Y = np.empty((A.n, b), X.dtype)
+    best = float("inf")
+    for _ in range(reps):
+        t0 = time.perf_counter()
+        if f32:
+            lib().lzo_csr_spmm_f32(A.n, _p(rp), _p(col), _p(v), b, _p(X), b, _p(Y), b)
+        else:
+            lib().lzo_csr_spmm(A.n, _p(rp), _p(col), _p(v), b, _p(X), b, _p(Y), b, 0)
+        best = min(best, time.perf_counter() - t0)
+    return Y, best
 
 
 # ------------------------------------------------- reference host code (_ref)

@@ -203,39 +203,82 @@ int lzo_block_lanczos_timed(int64_t n, const int64_t *rp, const int32_t *col, co
 /* ------------------------------------------------- single-vector Lanczos
  * vector_lanczos, methods/vector_lanczos.hpp:8-67 (the correct variant; the
  * BLAS variant's axpy at :116 updates q0 instead of w and is not restated). */
-int lzo_vector_lanczos(int64_t n, const int64_t *rp, const int32_t *col, const double *val, int m,
-                       int64_t lc, const double *bvec, double *q, double *alpha, double *beta)
+/* Deterministic parallel dot product: a fixed number of contiguous chunks, each
+ * summed in order, the chunk sums added in chunk order -- the same bits for any
+ * thread count (the single-vector oracle's reductions at n = 1e6, config C2). */
+#define LZO_NCHUNK 256
+static double dot_chunked(int64_t n, const double *x, const double *y)
+{
+    double part[LZO_NCHUNK];
+#pragma omp parallel for schedule(static)
+    for (int c = 0; c < LZO_NCHUNK; ++c) {
+        const int64_t lo = n * c / LZO_NCHUNK, hi = n * (c + 1) / LZO_NCHUNK;
+        double s = 0.0;
+        for (int64_t i = lo; i < hi; ++i) s += x[i] * y[i];
+        part[c] = s;
+    }
+    double s = 0.0;
+    for (int c = 0; c < LZO_NCHUNK; ++c) s += part[c];
+    return s;
+}
+
+/* y = a*y + b*x elementwise (order-free: parallel) */
+static void axpby(int64_t n, double a, double *y, double b, const double *x)
+{
+#pragma omp parallel for schedule(static)
+    for (int64_t i = 0; i < n; ++i) y[i] = a * y[i] + b * x[i];
+}
+
+static int vector_lanczos_impl(int64_t n, const int64_t *rp, const int32_t *col, const double *val, int m,
+                               int64_t lc, const double *bvec, double *q, double *alpha, double *beta,
+                               double *t_each)
 {
     double *q0 = (double *)malloc(n * sizeof(double));
     double *q1 = (double *)malloc(n * sizeof(double));
     double *w = (double *)malloc(n * sizeof(double));
     if (!q0 || !q1 || !w) return -2;
-    double s = 0.0;
-    for (int64_t i = 0; i < n; ++i) s += bvec[i] * bvec[i];
-    beta[0] = sqrt(s);                                    /* :20 */
-    for (int64_t i = 0; i < n; ++i) q0[i] = bvec[i] * (1.0 / beta[0]);   /* :23 */
+    beta[0] = sqrt(dot_chunked(n, bvec, bvec));           /* :20 */
+    const double s0 = 1.0 / beta[0];
+#pragma omp parallel for schedule(static)
+    for (int64_t i = 0; i < n; ++i) q0[i] = bvec[i] * s0; /* :23 */
     q[0] = q0[lc];                                        /* :26 */
     lzo_csr_spmm(n, rp, col, val, 1, q0, 1, w, 1, 0);     /* :29 */
-    s = 0.0;
-    for (int64_t i = 0; i < n; ++i) s += w[i] * q0[i];
-    alpha[0] = s;                                         /* :32 */
-    for (int64_t i = 0; i < n; ++i) w[i] -= alpha[0] * q0[i];           /* :35 */
+    alpha[0] = dot_chunked(n, w, q0);                     /* :32 */
+    axpby(n, 1.0, w, -alpha[0], q0);                      /* :35 */
     for (int j = 1; j < m; ++j) {
-        s = 0.0;
-        for (int64_t i = 0; i < n; ++i) s += w[i] * w[i];
-        beta[j] = sqrt(s);                                /* :43 */
-        for (int64_t i = 0; i < n; ++i) q1[i] = w[i] * (1.0 / beta[j]);  /* :46-47 */
+        const double t0 = lzo_wtime();
+        beta[j] = sqrt(dot_chunked(n, w, w));             /* :43 */
+        const double sj = 1.0 / beta[j];
+#pragma omp parallel for schedule(static)
+        for (int64_t i = 0; i < n; ++i) q1[i] = w[i] * sj;  /* :46-47 */
         lzo_csr_spmm(n, rp, col, val, 1, q1, 1, w, 1, 0); /* :50 */
-        for (int64_t i = 0; i < n; ++i) w[i] -= beta[j] * q0[i];        /* :53 */
-        s = 0.0;
-        for (int64_t i = 0; i < n; ++i) s += w[i] * q1[i];
-        alpha[j] = s;                                     /* :56 */
-        for (int64_t i = 0; i < n; ++i) w[i] -= alpha[j] * q1[i];       /* :59 */
+        axpby(n, 1.0, w, -beta[j], q0);                   /* :53 */
+        alpha[j] = dot_chunked(n, w, q1);                 /* :56 */
+        axpby(n, 1.0, w, -alpha[j], q1);                  /* :59 */
         double *t = q0; q0 = q1; q1 = t;                  /* :61 */
         q[j] = q0[lc];                                    /* :64 */
+        if (t_each) t_each[j - 1] = lzo_wtime() - t0;
     }
     free(q0); free(q1); free(w);
     return 0;
+}
+
+int lzo_vector_lanczos(int64_t n, const int64_t *rp, const int32_t *col, const double *val, int m,
+                       int64_t lc, const double *bvec, double *q, double *alpha, double *beta)
+{
+    return vector_lanczos_impl(n, rp, col, val, m, lc, bvec, q, alpha, beta, NULL);
+}
+
+int lzo_vector_lanczos_timed(int64_t n, const int64_t *rp, const int32_t *col, const double *val, int m,
+                             int64_t lc, const double *bvec, double *q, double *alpha, double *beta, double *t_each)
+{
+    return vector_lanczos_impl(n, rp, col, val, m, lc, bvec, q, alpha, beta, t_each);
+}
+
+int lzo_block_lanczos_f32_timed(int64_t n, const int64_t *rp, const int32_t *col, const float *val, int b, int m,
+                                int64_t lc, const float *B, float *q, float *alpha, float *beta, double *t_each)
+{
+    return block_lanczos_impl_f32(n, rp, col, val, b, m, lc, B, q, alpha, beta, t_each);
 }
 
 /* vector_lanczos<float> (methods/vector_lanczos.hpp:8-67 at T = float, as

@@ -91,7 +91,16 @@ int lzo_block_lanczos_timed(int64_t n, const int64_t *row_ptr, const int32_t *co
                             int b, int m, int64_t lc, const double *B, double *q, double *alpha,
                             double *beta, double *t_each);
 
+/* The single-vector and the fp32 block iterations with the wall seconds of
+ * each iteration j = 1..m-1 (bench.py's CPU baselines at configs C2 and C5). */
+int lzo_vector_lanczos_timed(int64_t n, const int64_t *row_ptr, const int32_t *col, const double *val, int m,
+                             int64_t lc, const double *bvec, double *q, double *alpha, double *beta, double *t_each);
+int lzo_block_lanczos_f32_timed(int64_t n, const int64_t *row_ptr, const int32_t *col, const float *val, int b,
+                                int m, int64_t lc, const float *B, float *q, float *alpha, float *beta,
+                                double *t_each);
+
 #ifdef __cplusplus
 }
 #endif
+
 #endif

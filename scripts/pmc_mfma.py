@@ -1,9 +1,12 @@
 """MFMA utilisation of the dense-step kernels from one rocprofv3 --pmc pass
 (SQ_VALU_MFMA_BUSY_CYCLES, SQ_INSTS_VALU_MFMA_{F64,F32}, ..._MOPS_*, GRBM_GUI_ACTIVE).
 
-    python scripts/pmc_mfma.py <pmc_dir> <tag> <n> <nnz> <hw> [kernel ...]
+    python scripts/pmc_mfma.py <pmc_dir> <tag> <n> <nnz> <hw> [kernel_full ...]
 
-Writes profiles/<tag>_pmc_mfma_<kernel>.json for every kernel substring given.
+Writes profiles/<tag>_pmc_mfma_<short>.json for every kernel instantiation given
+(as bench.py names it, e.g. "k_fused_update16<true,8,false>"; matched exactly
+against the demangled name), stamped with the sha256 of the kernel's source file
+and the commit (env LZ_COMMIT): bench.py refuses a summary of another source.
   MfmaUtil_pct = 100 * MFMA_BUSY_CYCLES / (GRBM_GUI_ACTIVE / 8 XCDs * 1024 SIMDs)
   (GRBM_GUI_ACTIVE is summed over the 8 XCDs; MFMA_BUSY_CYCLES over all SIMDs)
   mfma_flop_per_launch = 512 * MOPS (a MOP is 512 FLOP: v_mfma_f64_16x16x4f64 = 4
@@ -16,8 +19,11 @@ import os
 import sys
 from collections import defaultdict
 
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+from bench import _norm, source_sha  # noqa: E402
+
 d, tag, n, nnz, hw = sys.argv[1:6]
-kernels = sys.argv[6:] or ["k_fused_pp16", "k_fused_update16", "k_gram16_f64"]
+kernels = sys.argv[6:] or ["k_fused_pp16<14,2376,3,2,false>", "k_fused_update16<true,8,false>"]
 rows = defaultdict(lambda: defaultdict(list))
 for f in glob.glob(f"{d}/**/*counter_collection.csv", recursive=True):
     for r in csv.DictReader(open(f)):
@@ -26,8 +32,9 @@ for f in glob.glob(f"{d}/**/*counter_collection.csv", recursive=True):
         rows[key]["_ns"] = float(r["End_Timestamp"]) - float(r["Start_Timestamp"])
 root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 for k in kernels:
-    disp = [v for (name, _), v in rows.items() if k in name]
-    full = sorted({name for (name, _) in rows if k in name})
+    disp = [v for (name, _), v in rows.items() if _norm(name) == _norm(k)]
+    full = sorted({name.split("(")[0] for (name, _) in rows if _norm(name) == _norm(k)})
+    short = k.split("<")[0]
     if not disp:
         print(f"{k}: no dispatches")
         continue
@@ -35,7 +42,8 @@ for k in kernels:
     busy, grbm = avg.get("SQ_VALU_MFMA_BUSY_CYCLES", 0.0), avg.get("GRBM_GUI_ACTIVE", 0.0)
     mops = avg.get("SQ_INSTS_VALU_MFMA_MOPS_F64", 0.0) + avg.get("SQ_INSTS_VALU_MFMA_MOPS_F32", 0.0)
     cyc = grbm / 8.0
-    res = {"kernel": k, "kernel_names": full, "dispatches": len(disp),
+    res = {"kernel": short, "kernel_full": k, "kernel_names": full, "dispatches": len(disp),
+           "source_sha": source_sha(k), "commit": os.environ.get("LZ_COMMIT", "unknown"),
            "workload": {"n": int(n), "nnz": int(nnz), "halfwidth": int(hw)},
            "counters_avg_per_launch": avg,
            "MfmaUtil_pct": round(100.0 * busy / (cyc * 1024), 3) if cyc else None,
@@ -44,6 +52,6 @@ for k in kernels:
            "achieved_TFLOPs_profiled": round(512 * mops / avg["_ns"] / 1e3, 3) if avg.get("_ns") else None,
            "note": "one --pmc pass (no tracing); MfmaUtil = MFMA busy cycles / (GRBM_GUI_ACTIVE/8 x 1024 SIMDs); "
                    "profiled clocks run below unprofiled ones"}
-    out = os.path.join(root, "profiles", f"{tag}_pmc_mfma_{k}.json")
+    out = os.path.join(root, "profiles", f"{tag}_pmc_mfma_{short}.json")
     json.dump(res, open(out, "w"), indent=1)
     print(out, res["MfmaUtil_pct"], res["mfma_flop_per_launch"], res["effective_clock_GHz"])
