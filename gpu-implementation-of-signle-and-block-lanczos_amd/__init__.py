@@ -64,6 +64,7 @@ HIP_SYMBOLS = [
     ("lz_prof_read", _c_int, [_c_vp, _c_int, ctypes.POINTER(_c_dbl), ctypes.POINTER(_c_int)]),
     ("lz_csr_spmm", _c_int, [_c_vp, _c_i64, _c_i64, _c_i64, _c_vp, _c_vp, _c_vp, _c_int, _c_int,
                              _c_vp, _c_i64, _c_int, _c_vp, _c_i64]),
+    ("lz_to_row_major", _c_int, [_c_vp, _c_i64, _c_int, _c_int, _c_vp, _c_i64, _c_vp]),
     ("lz_csr_spmv", _c_int, [_c_vp, _c_i64, _c_i64, _c_i64, _c_vp, _c_vp, _c_vp, _c_int, _c_vp, _c_vp]),
     ("lz_gram", _c_int, [_c_vp, _c_i64, _c_int, _c_int, _c_vp, _c_i64, _c_vp]),
     ("lz_sym_cross_gram", _c_int, [_c_vp, _c_i64, _c_int, _c_int, _c_vp, _c_vp, _c_i64, _c_vp]),
@@ -477,6 +478,13 @@ class Handle:
         ldx, ldy = _ld(X), _ld(Y)
         _check(self.L.lz_csr_spmm(self.ptr, A.n, A.n_cols, A.nnz, _ptr(A.row_ptr), _ptr(A.col),
                                   _ptr(A.val), A.dtype, b, _ptr(X), ldx, layout, _ptr(Y), ldy), "lz_csr_spmm")
+        return Y
+
+    def to_row_major(self, Xcm, Y):
+        """Y (rows, b) row-major <- the column-major block viewed as Xcm (b, ld) (ld >= rows)."""
+        b, ld = Xcm.shape
+        rows = Y.shape[0]
+        _check(self.L.lz_to_row_major(self.ptr, rows, b, _dt(Xcm), _ptr(Xcm), ld, _ptr(Y)), "lz_to_row_major")
         return Y
 
     def spmv(self, A: CsrDevice, x, y):

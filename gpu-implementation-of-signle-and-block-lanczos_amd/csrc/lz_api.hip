@@ -901,6 +901,14 @@ int lz_csr_spmm(lz_handle *h, int64_t n_rows, int64_t n_cols, int64_t nnz, const
                           (float *)Y, ldy);
 }
 
+int lz_to_row_major(lz_handle *h, int64_t rows, int b, lz_dtype dtype, const void *X, int64_t ldx, void *Y)
+{
+    LZ_HANDLE_CHECK(h);
+    LZ_ARG_CHECK(X && Y && X != Y, "to_row_major: X, Y distinct, not NULL");
+    if (dtype == LZ_F64) return to_row_major<double>(h, rows, b, (const double *)X, ldx, (double *)Y);
+    return to_row_major<float>(h, rows, b, (const float *)X, ldx, (float *)Y);
+}
+
 int lz_csr_spmv(lz_handle *h, int64_t n_rows, int64_t n_cols, int64_t nnz, const int64_t *rp,
                 const int32_t *col, const void *val, lz_dtype dtype, const void *x, void *y)
 {

@@ -206,6 +206,12 @@ double powerlaw_xmin(double npr, double a) { return std::max(0.5, ((npr - 1.0) /
 // ------------------------------------------------------ eigen (tred2/tql2)
 // Householder tridiagonalisation followed by the implicit QL method (the
 // EISPACK tred2/tql2 algorithms).  V row-major k x k.
+// Attribution: a close restatement of the public-domain JAMA library's
+// EigenvalueDecomposition (tred2 / tql2, MathWorks and NIST, 1998-2012), which
+// follows the EISPACK routines of Smith et al. (1976) and Bowdler, Martin,
+// Reinsch and Wilkinson (Handbook for Auto. Comp., Vol. II -- Linear Algebra);
+// its local names (c2, c3, s2, el1, dl1, tst1) are kept.  Not from the
+// reference repository, which calls cuSOLVER syevd here (lib_utils.hpp:542-590).
 void tred2(int n, std::vector<double> &V, std::vector<double> &d, std::vector<double> &e)
 {
     auto Vr = [&](int i, int j) -> double & { return V[(size_t)i * n + j]; };

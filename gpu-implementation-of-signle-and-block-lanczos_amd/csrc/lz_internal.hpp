@@ -12,6 +12,9 @@ int spmm_rm(lz_handle *h, int64_t n, int64_t nnz, const int64_t *rp, const int32
 template <typename T>
 int spmm_cm(lz_handle *h, int64_t n, int64_t nnz, const int64_t *rp, const int32_t *col, const T *val, int b,
             const T *X, int64_t ldx, int64_t nx, T *Y, int64_t ldy);  // nx: rows of X
+// column-major rows x b (ld >= rows) -> row-major rows x b (ld = b)
+template <typename T>
+int to_row_major(lz_handle *h, int64_t rows, int b, const T *src, int64_t ld, T *dst);
 template <typename T>
 int spmv(lz_handle *h, int64_t n, const int64_t *rp, const int32_t *col, const T *val, const T *x,
          T *y, int64_t nnz_hint);

@@ -969,6 +969,21 @@ __global__ __launch_bounds__(256) void k_cm_transpose(int64_t rows, int b, const
     }
 }
 
+// column-major rows x b block (leading dimension ld >= rows) -> row-major (ld = b)
+template <typename T>
+int to_row_major(lz_handle *h, int64_t rows, int b, const T *src, int64_t ld, T *dst)
+{
+    LZ_ARG_CHECK(b >= 1 && b <= kMaxB && ld >= rows && rows >= 0, "to_row_major: 1 <= b <= 64, ld >= rows");
+    if (rows == 0) return LZ_OK;
+    const size_t lds = sizeof(T) * (size_t)b * (kCmRows + 1);
+    hipLaunchKernelGGL((k_cm_transpose<T>), dim3((unsigned)ceil_div(rows, (int64_t)kCmRows)), dim3(256), lds,
+                       h->stream, rows, b, src, ld, dst);
+    LZ_LAUNCH_CHECK();
+    return LZ_OK;
+}
+template int to_row_major<double>(lz_handle *, int64_t, int, const double *, int64_t, double *);
+template int to_row_major<float>(lz_handle *, int64_t, int, const float *, int64_t, float *);
+
 template <typename T>
 int spmm_cm(lz_handle *h, int64_t n, int64_t nnz, const int64_t *rp, const int32_t *col, const T *val, int b,
             const T *X, int64_t ldx, int64_t nx, T *Y, int64_t ldy)

@@ -6,11 +6,16 @@
 //   test_lanczos [-N 10] [-m 5] [--block 4] [--vector [--fp32]] [--unfused]
 //                [--matrix matrix_a|banded|powerlaw|file:PATH] [--n ROWS]
 //                [--nnz-per-row 10] [--halfwidth 4096] [--bug-compat-change-order]
-//                [--fdtd-steps 1000000] [--T-end 1] [--lc ROW] [--device 0]
+//                [--fdtd-steps STEPS] [--T-end 1] [--lc ROW] [--device 0] [--row-major-B]
 //
 // Defaults reproduce the reference run: block Lanczos, b = 4 (N_COL), fp64, on
 // the Yee operator of grid N with B from the glibc rand() stream and
-// lc = 1 + rand() % 100 drawn first.
+// lc = 1 + rand() % 100 drawn first; B is stored as the reference stores it,
+// column-major with its rows padded to a multiple of 768 (or 768 x #CU,
+// test_lanczos.cu:174-187), and handed to block_lanczos_blas that way; the
+// validation run is the reference's: 10^6 forward-Euler steps for the block
+// path (:325,336), 10^5 for the single-vector one (:118).  --fdtd-steps 0
+// skips it.
 #include <hip/hip_runtime.h>
 
 #include <chrono>
@@ -61,7 +66,8 @@ int main(int argc, char **argv)
     int N = 10, m = 5, b = 4, device = 0;
     bool vector = false, unfused = false, bug = false, fp32 = false;
     std::string matrix = "matrix_a";
-    int64_t nrows = 1000000, halfwidth = 4096, fdtd_steps = 0, lc = -1;
+    int64_t nrows = 1000000, halfwidth = 4096, fdtd_steps = -1, lc = -1;
+    bool row_major_B = false;
     double npr = 10.0, T_end = 1.0;
     for (int i = 1; i < argc; ++i) {
         std::string o = argv[i];
@@ -84,9 +90,11 @@ int main(int argc, char **argv)
         else if (o == "--T-end") T_end = std::stod(nxt());
         else if (o == "--lc") lc = (int64_t)std::stod(nxt());
         else if (o == "--device") device = std::atoi(nxt());
+        else if (o == "--row-major-B") row_major_B = true;  // B as an n x b row-major block instead
         else { std::fprintf(stderr, "unknown option %s\n", o.c_str()); return 2; }
     }
     if (vector) b = 1;
+    if (fdtd_steps < 0) fdtd_steps = vector ? 100000 : 1000000;  // test_lanczos.cu:118 / :325,336
     if (fp32 && !vector) { std::fprintf(stderr, "--fp32 applies to --vector\n"); return 2; }
     if (lc < 0) lc = lzh_rand_lc(1);  // 1 + rand() % 100, test_lanczos.cu:326
 
@@ -169,7 +177,18 @@ int main(int argc, char **argv)
         beta = be;
         beta.push_back(0.0);
     } else {
-        lz::Dense_matrix<double> Bm(n, b, B), Q0(n, b), Q1(n, b), W(n, b);
+        // the reference's padding of B (test_lanczos.cu:174-187): rows up to a
+        // multiple of 768 (6 warps x 4 x 32), or of 768 x #CU for large n
+        int ncu = 0;
+        lz::hip_check(hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, device), "CU count");
+        const int64_t pads = n < 768LL * ncu ? 768 : 768LL * ncu;
+        const int64_t ld = (n + pads - 1) / pads * pads;
+        std::vector<double> Bcm((size_t)ld * b, 0.0);
+        for (int64_t r = 0; r < n; ++r)
+            for (int c = 0; c < b; ++c) Bcm[(size_t)c * ld + r] = B[(size_t)r * b + c];
+        lz::Dense_matrix<double> Bm = row_major_B ? lz::Dense_matrix<double>(n, b, B)
+                                                  : lz::Dense_matrix<double>(ld, b, Bcm, LZ_COL_MAJOR, ld);
+        lz::Dense_matrix<double> Q0(ld, b, LZ_COL_MAJOR, ld), Q1(ld, b, LZ_COL_MAJOR, ld), W(ld, b, LZ_COL_MAJOR, ld);
         std::vector<lz::Dense_matrix<double>> al, be;
         for (int j = 0; j < m; ++j) al.emplace_back(b, b);
         for (int j = 0; j <= m; ++j) be.emplace_back(b, b);
@@ -200,12 +219,22 @@ int main(int argc, char **argv)
     sol = lz::block_solution(m, b, T_end, alpha, beta, qh);
     std::printf("Ritz values (%d):", m * b);
     for (double r : ritz) std::printf(" %.15e", r);
-    std::printf("\nSolution for block lanczos\n");
-    for (double s : sol) std::printf("%.15e\n", s);
+    if (vector) {  // test_lanczos.cu:111-112
+        std::printf("\nThe solution for vector_lanczos \n%.15e\n", sol[0]);
+    } else {       // test_lanczos.cu:288-289
+        std::printf("\nSolution for block lanczos\n");
+        for (double s : sol) std::printf("%.15e\n", s);
+    }
 
     if (fdtd_steps > 0) {
-        std::printf(" start fdtd \n");
         lz::Dense_matrix<double> U0(n, b, B);
+        if (vector) {  // fdtd_vector(A, b, 1e5, 1, lc), test_lanczos.cu:118-123
+            const std::vector<double> fd = lz::ftdt_block(Ad, U0, (unsigned)fdtd_steps, T_end, lc, ctx);
+            std::printf("Solution from fdtd %.15e\n", fd[0]);
+            std::printf("Relative error for block lanczos is %.6e\n", std::fabs(sol[0] - fd[0]) / std::fabs(fd[0]));
+            return 0;
+        }
+        std::printf(" start fdtd \n");  // ftdt_block(A, B, fdtd_steps, T_end, lc), test_lanczos.cu:292-301
         const std::vector<double> fd = lz::ftdt_block(Ad, U0, (unsigned)fdtd_steps, T_end, lc, ctx);
         std::printf("Solution from fdtd\n");
         double num = 0, den = 0;

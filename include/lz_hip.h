@@ -88,6 +88,14 @@ int lz_csr_spmm(lz_handle *h, int64_t n_rows, int64_t n_cols, int64_t nnz,
                 const int64_t *row_ptr, const int32_t *col, const void *val, lz_dtype dtype,
                 int b, const void *X, int64_t ldx, lz_layout layout, void *Y, int64_t ldy);
 
+/* Y (rows x b, row-major, ld = b) = X (rows x b, COLUMN-major, leading
+ * dimension ldx >= rows: the reference's Dense_matrix storage,
+ * objects/dense_matrix.hpp:9, whose ld is the row count padded to a multiple of
+ * 768, test_lanczos.cu:174-187).  One pass through LDS (coalesced column reads
+ * and row writes); lz_methods.hpp uses it to take the reference's column-major
+ * start block into the row-major iteration once. */
+int lz_to_row_major(lz_handle *h, int64_t rows, int b, lz_dtype dtype, const void *X, int64_t ldx, void *Y);
+
 /* y = A*x  (spmv, kernels/spmv_spmm.hpp:209-260) */
 int lz_csr_spmv(lz_handle *h, int64_t n_rows, int64_t n_cols, int64_t nnz,
                 const int64_t *row_ptr, const int32_t *col, const void *val, lz_dtype dtype,

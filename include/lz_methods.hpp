@@ -266,12 +266,41 @@ void spmv(const Csr_matrix<T> &A, const Vector<T> &x, Vector<T> &y, Context &ctx
 }
 
 // ------------------------------------------------------------------ methods
+// The iteration's start block as n x b row-major (ld = b): B itself when it is
+// stored that way, else its first n rows transposed once on the device into
+// `tmp` -- the reference's B is column-major with its rows padded to a multiple
+// of 768 (objects/dense_matrix.hpp:9, test_lanczos.cu:174-187).
+template <typename T>
+const T *row_major_block(const Dense_matrix<T> &B, int64_t n, DeviceArray<T> &tmp, Context &ctx, const char *who)
+{
+    const int b = B.n_cols();
+    if (B.n_rows() < n) throw std::runtime_error(std::string(who) + ": B has fewer rows than A");
+    if (B.layout() == LZ_ROW_MAJOR) {
+        if (B.ld() != b) throw std::runtime_error(std::string(who) + ": a row-major B needs ld = b");
+        return B.data();
+    }
+    tmp = DeviceArray<T>((size_t)n * b);
+    check(lz_to_row_major(ctx.get(), n, b, dtype_of<T>(), B.data(), B.ld(), tmp.data()), who);
+    return tmp.data();
+}
+
+// workspace blocks may come in either layout (the reference allocates Q0, Q1, W
+// like B): only their capacity matters, their content is overwritten
+template <typename T>
+void check_workspace(const Dense_matrix<T> &X, int64_t n, int b, const char *who)
+{
+    const int64_t cap = X.layout() == LZ_ROW_MAJOR ? X.n_rows() * X.ld() : (int64_t)X.n_cols() * X.ld();
+    if (cap < n * b) throw std::runtime_error(std::string(who) + ": workspace block smaller than n x b");
+}
+
 // block_lanczos_blas (methods/block_lanczos.hpp:88-167).  alpha: array of m
 // b x b matrices, beta: array of m + 1 (beta[m] = the last inverse square root,
-// as the reference's); B, Q0, Q1, W: n x b row-major blocks (Q0/Q1/W are
-// workspace).  eigen_val, n_blocks, n_loads are accepted for call-site
-// compatibility: the eigenvalues of each Gram are not needed by the caller,
-// and launch shapes are chosen per operator.
+// as the reference's).  B: the start block, row-major (ld = b) or the
+// reference's column-major layout with a padded leading dimension (rows past
+// A.n_rows() are padding, as in the reference).  Q0, Q1, W: workspace, either
+// layout.  eigen_val, n_blocks, n_loads are accepted for call-site
+// compatibility: the eigenvalues of each Gram are not needed by the caller, and
+// launch shapes are chosen per operator.
 template <typename T>
 void block_lanczos_blas(const Csr_matrix<T> &A, const Dense_matrix<T> &B, unsigned m, unsigned lc, Vector<T> &q,
                         Dense_matrix<T> *alpha, Dense_matrix<T> *beta, Dense_matrix<T> &Q0, Dense_matrix<T> &Q1,
@@ -279,12 +308,14 @@ void block_lanczos_blas(const Csr_matrix<T> &A, const Dense_matrix<T> &B, unsign
                         unsigned /*n_blocks*/ = 0, unsigned /*n_loads*/ = 0)
 {
     const int b = B.n_cols();
-    const int64_t n = B.n_rows(), bb = (int64_t)b * b;
-    if (B.layout() != LZ_ROW_MAJOR || B.ld() != b || q.size() < (int64_t)m * b)
-        throw std::runtime_error("block_lanczos_blas: B must be n x b row-major (ld = b), q >= m*b");
+    const int64_t n = A.n_rows(), bb = (int64_t)b * b;
+    if (q.size() < (int64_t)m * b) throw std::runtime_error("block_lanczos_blas: q needs m*b entries");
+    DeviceArray<T> Bt;
+    const T *Bp = row_major_block(B, n, Bt, ctx, "block_lanczos_blas");
+    for (Dense_matrix<T> *X : {&Q0, &Q1, &W}) check_workspace(*X, n, b, "block_lanczos_blas");
     DeviceArray<T> al((size_t)m * bb), be((size_t)(m + 1) * bb);
     check(lz_block_lanczos(ctx.get(), n, A.nnz(), A.row_ptr(), A.col(), A.val(), dtype_of<T>(), b, (int)m, lc,
-                           B.data(), q.data(), al.data(), be.data(), Q0.data(), Q1.data(), W.data()),
+                           Bp, q.data(), al.data(), be.data(), Q0.data(), Q1.data(), W.data()),
           "block_lanczos_blas");
     // scatter into the caller's per-step matrices (device to device, on the stream)
     for (unsigned j = 0; j < m; ++j)
@@ -305,11 +336,13 @@ void block_lanczos_blas_reference_order(const Csr_matrix<T> &A, const Dense_matr
                                         Dense_matrix<T> &Q0, Dense_matrix<T> &Q1, Dense_matrix<T> &W, Context &ctx)
 {
     const int b = B.n_cols();
-    const int64_t bb = (int64_t)b * b;
+    const int64_t n = A.n_rows(), bb = (int64_t)b * b;
+    DeviceArray<T> Bt;
+    const T *Bp = row_major_block(B, n, Bt, ctx, "block_lanczos_blas_reference_order");
+    for (Dense_matrix<T> *X : {&Q0, &Q1, &W}) check_workspace(*X, n, b, "block_lanczos_blas_reference_order");
     DeviceArray<T> al((size_t)m * bb), be((size_t)(m + 1) * bb);
-    check(lz_block_lanczos_unfused(ctx.get(), B.n_rows(), A.nnz(), A.row_ptr(), A.col(), A.val(), dtype_of<T>(), b,
-                                   (int)m, lc, B.data(), q.data(), al.data(), be.data(), Q0.data(), Q1.data(),
-                                   W.data()),
+    check(lz_block_lanczos_unfused(ctx.get(), n, A.nnz(), A.row_ptr(), A.col(), A.val(), dtype_of<T>(), b, (int)m,
+                                   lc, Bp, q.data(), al.data(), be.data(), Q0.data(), Q1.data(), W.data()),
           "block_lanczos_blas_reference_order");
     for (unsigned j = 0; j < m; ++j)
         hip_check(hipMemcpyAsync(alpha[j].data(), al.data() + j * bb, sizeof(T) * bb, hipMemcpyDeviceToDevice,
@@ -339,16 +372,20 @@ void vector_lanczos(const Csr_matrix<T> &A, const Vector<T> &b, unsigned m, unsi
 }
 
 // ftdt_block (methods/fdtd.hpp:33-56): Nsteps forward-Euler steps of U' = A U
-// from U0 (n x b row-major), returns row lc of the final state.
+// from U0 (n x b, row-major or the reference's padded column-major layout),
+// returns row lc of the final state.
 template <typename T>
 std::vector<T> ftdt_block(const Csr_matrix<T> &A, const Dense_matrix<T> &U0, unsigned Nsteps, double T_end, unsigned lc,
                           Context &ctx = default_context())
 {
     const int b = U0.n_cols();
-    Dense_matrix<T> U(U0.n_rows(), b), D(U0.n_rows(), b);
+    const int64_t n = A.n_rows();
+    DeviceArray<T> Ut;
+    const T *U0p = row_major_block(U0, n, Ut, ctx, "ftdt_block");
+    Dense_matrix<T> U(n, b), D(n, b);
     DeviceArray<T> out(b);
-    check(lz_fdtd_block(ctx.get(), U0.n_rows(), A.nnz(), A.row_ptr(), A.col(), A.val(), dtype_of<T>(), b, U0.data(),
-                        Nsteps, T_end, lc, U.data(), D.data(), out.data()),
+    check(lz_fdtd_block(ctx.get(), n, A.nnz(), A.row_ptr(), A.col(), A.val(), dtype_of<T>(), b, U0p, Nsteps, T_end,
+                        lc, U.data(), D.data(), out.data()),
           "ftdt_block");
     ctx.synchronize();
     return out.copy_to_host();

@@ -272,3 +272,18 @@ def test_errors_are_loud(lz, handle, torch_cuda):
     with pytest.raises(lz.LanczosError):  # b = 65 > the 64-column limit
         handle.spmm(A, torch.zeros(100, 65, dtype=torch.float64, device="cuda"),
                     torch.zeros(100, 65, dtype=torch.float64, device="cuda"))
+
+
+@pytest.mark.parametrize("b,dtype,ld_pad", [(4, "float64", 768), (16, "float64", 5), (32, "float32", 0), (3, "float64", 17)])
+def test_to_row_major(lz, handle, torch_cuda, b, dtype, ld_pad):
+    """lz_to_row_major: the reference's column-major Dense_matrix (leading
+    dimension = rows padded, objects/dense_matrix.hpp:9) into a row-major block."""
+    torch = torch_cuda
+    rows = 7001
+    ld = rows + ld_pad
+    tdt = getattr(torch, dtype)
+    Xcm = torch.randn(b, ld, dtype=tdt, device="cuda")
+    Y = torch.empty(rows, b, dtype=tdt, device="cuda")
+    handle.to_row_major(Xcm, Y)
+    torch.cuda.synchronize()
+    assert torch.equal(Y, Xcm[:, :rows].t())
