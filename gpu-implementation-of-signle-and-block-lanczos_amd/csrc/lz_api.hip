@@ -791,6 +791,8 @@ int lz_finalize(lz_handle *h)
     (void)hipFree(h->longq);
     (void)hipFree(h->cm_buf);
     (void)hipFree(h->ybuf);
+    (void)hipFree(h->fnz_colf);
+    (void)hipFree(h->fnz_trow);
     if (h->ev_pool) {
         for (int i = 0; i < h->ev_cap; ++i) (void)hipEventDestroy(h->ev_pool[i]);
         delete[] h->ev_pool;

@@ -81,6 +81,11 @@ struct lz_handle {
     hipStream_t xstream = nullptr;
     hipEvent_t ev_cx = nullptr, ev_xd = nullptr;
     int64_t last_split[2] = {-1, -1};  // lz_debug_last_split
+    // fixed-nnz SpMM format (experiment, lz_spmm.hip fnz_prepare): the operator's
+    // columns with row-end flags and each tile's first row, keyed by the operator
+    int32_t *fnz_colf = nullptr, *fnz_trow = nullptr;
+    int64_t fnz_key[4] = {0, 0, 0, 0};
+    bool fnz_ok = false;
     void *ybuf = nullptr;         // distributed generic-b iteration: the local SpMM result
     size_t ybuf_cap = 0;          // bytes
     void *halo = nullptr;         // lz::HaloPlan when lz_halo_init was called

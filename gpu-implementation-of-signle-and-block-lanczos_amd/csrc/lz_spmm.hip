@@ -793,6 +793,330 @@ __global__ __launch_bounds__(256) void k_spmv(int64_t n, const int64_t *__restri
     }
 }
 
+// ---------------------------------------------------------------------------
+// Fixed-nnz tiles (experiment; LZ_SPMM_FNZ=1 selects it for 128-B rows).
+// Tile t owns the rows whose FIRST entry lies in [tK, (t+1)K): the CSR window
+// it stages, entries [tK - 1, tK + K + S), is known from t alone, so the run's
+// loads issue at once, beside the one load of its first row trow[t] -- no
+// row-pointer round trip ahead of them.  Row ends ride in bit 31 of a copy of
+// the column index (colf, built once per operator), so row starts, row ids and
+// row offsets come from one block scan over the staged flags.  Requires: no
+// empty rows, every row <= S + 1 entries, at most RMAX rows per tile, columns
+// < 2^31 (fnz_prepare checks, else the default kernel runs).
+constexpr int kFnzK = 448, kFnzS = 64, kFnzRmax = 80;
+
+__global__ __launch_bounds__(256) void k_fnz_flags(int64_t n, const int64_t *__restrict__ rp,
+                                                   const int32_t *__restrict__ col, int32_t *__restrict__ colf,
+                                                   int *__restrict__ stats)
+{
+    int maxlen = 0, bad = 0;
+    for (int64_t r = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; r < n; r += (int64_t)gridDim.x * blockDim.x) {
+        const int64_t a = rp[r], e = rp[r + 1];
+        const int64_t len = e - a;
+        maxlen = len > maxlen ? (int)(len < (1 << 30) ? len : (1 << 30)) : maxlen;
+        bad |= len == 0;
+        for (int64_t k = a; k < e; ++k) {
+            const int32_t c = col[k];
+            bad |= c < 0;
+            colf[k] = (int32_t)((uint32_t)c | (k == e - 1 ? 0x80000000u : 0u));
+        }
+    }
+    atomicMax(&stats[0], maxlen);
+    if (bad) atomicOr(&stats[1], 1);
+}
+
+// trow[t] = first row whose first entry is >= t*K (rows before it start earlier)
+__global__ __launch_bounds__(256) void k_fnz_trow(int64_t ntiles, int64_t n, const int64_t *__restrict__ rp, int K,
+                                                  int32_t *__restrict__ trow, int *__restrict__ stats)
+{
+    int maxrows = 0;
+    for (int64_t t = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; t <= ntiles;
+         t += (int64_t)gridDim.x * blockDim.x) {
+        const int64_t key = t * K;
+        int64_t lo = 0, hi = n;  // smallest r in [0, n] with rp[r] >= key
+        while (lo < hi) {
+            const int64_t mid = (lo + hi) >> 1;
+            if (rp[mid] >= key) hi = mid;
+            else lo = mid + 1;
+        }
+        trow[t] = (int32_t)lo;
+        if (t > 0) {  // rows of tile t - 1
+            int64_t lo2 = 0, hi2 = n;
+            const int64_t key2 = (t - 1) * (int64_t)K;
+            while (lo2 < hi2) {
+                const int64_t mid = (lo2 + hi2) >> 1;
+                if (rp[mid] >= key2) hi2 = mid;
+                else lo2 = mid + 1;
+            }
+            const int64_t nr = lo - lo2;
+            maxrows = nr > maxrows ? (int)(nr < (1 << 30) ? nr : (1 << 30)) : maxrows;
+        }
+    }
+    atomicMax(&stats[2], maxrows);
+}
+
+template <typename T, int B, int K, int S, int RMAX>
+__global__ __launch_bounds__(256) void k_spmm_fnz(int64_t nnz, const int32_t *__restrict__ colf,
+                                                  const T *__restrict__ val, const int32_t *__restrict__ trow,
+                                                  const T *__restrict__ X, int64_t ldx, int64_t nx,
+                                                  T *__restrict__ Y, int64_t ldy)
+{
+    using Sh = SpmmShape<T, B>;
+    constexpr int VEC = Sh::VEC, LPR = Sh::LPR, G = 256 / LPR, UNR = 8;
+    constexpr int WIN = K + S + 1;           // local i <-> entry tK - 1 + i
+    constexpr int EPT = (WIN + 255) / 256;   // scan: entries per thread
+    static_assert(RMAX <= 255 && K % 4 == 0, "row ids are bytes; 16-B column pieces");
+    __shared__ int32_t cs[WIN + UNR];
+    __shared__ T vs[WIN + UNR];
+    __shared__ uint8_t rid[WIN + UNR];
+    __shared__ int32_t rel[RMAX + 1];
+    __shared__ Vec<T, VEC> yt[RMAX][LPR];
+    __shared__ Vec<T, VEC> head[G][LPR];
+    __shared__ int32_t wsum[4], bnd[2];
+    const int tid = threadIdx.x;
+    const int64_t t = xcd_remap(blockIdx.x, gridDim.x);
+    const int64_t e0 = t * K - 1;  // entry of local index 0
+    const int32_t row0 = trow[t], row1 = trow[t + 1];
+    const int nrows = row1 - row0;  // rows owned (their first entry in [tK, tK + K))
+    {   // stage entries [e0, e0 + WIN) with 16-B loads; entries outside [0, nnz) read as row ends
+        constexpr int EPV = 16 / (int)sizeof(T);
+        const int64_t bc = e0 < 0 ? 0 : (e0 & ~(int64_t)3), bv = e0 < 0 ? 0 : (e0 & ~(int64_t)(EPV - 1));
+        const int64_t ce = e0 + WIN;  // one past the last staged entry
+        constexpr int SPTC = ((WIN + 4) / 4 + 255) / 256, SPTV = ((WIN + EPV) / EPV + 255) / 256;
+        const __amdgpu_buffer_rsrc_t cr = lz_rsrc(colf + bc, 0x7fffffffu);
+        const __amdgpu_buffer_rsrc_t vr = lz_rsrc(val + bv, 0x7fffffffu);
+        constexpr int AUX = 2;  // nt: streamed once
+        int4 ct[SPTC];
+        int4 vt[SPTV];
+#pragma unroll
+        for (int q = 0; q < SPTC; ++q) {
+            const int64_t k = bc + 4 * (int64_t)(tid + 256 * q);
+            ct[q] = int4{0, 0, 0, 0};
+            if (k + 4 <= nnz && k < ce)
+                ct[q] = __builtin_bit_cast(int4, __builtin_amdgcn_raw_buffer_load_b128(cr, (uint32_t)((k - bc) * 4), 0, AUX));
+            else if (k < ce && k < nnz) {
+                ct[q].x = colf[k];
+                if (k + 1 < nnz) ct[q].y = colf[k + 1];
+                if (k + 2 < nnz) ct[q].z = colf[k + 2];
+            }
+        }
+#pragma unroll
+        for (int q = 0; q < SPTV; ++q) {
+            const int64_t k = bv + EPV * (int64_t)(tid + 256 * q);
+            vt[q] = int4{0, 0, 0, 0};
+            if (k + EPV <= nnz && k < ce) {
+                vt[q] = __builtin_bit_cast(int4, __builtin_amdgcn_raw_buffer_load_b128(vr, (uint32_t)((k - bv) * sizeof(T)), 0, AUX));
+            } else if (k < ce && k < nnz) {
+                T tv[EPV] = {};
+                for (int e = 0; e < EPV && k + e < nnz; ++e) tv[e] = val[k + e];
+                __builtin_memcpy(&vt[q], tv, 16);
+            }
+        }
+        // entries before 0 or past nnz: a row end (flag) with a zero value
+        for (int i = tid; i < WIN + UNR; i += 256) {
+            const int64_t e = e0 + i;
+            if (e < 0 || e >= nnz || i >= WIN) {
+                cs[i] = (int32_t)0x80000000u;
+                vs[i] = T(0);
+            }
+        }
+#pragma unroll
+        for (int q = 0; q < SPTC; ++q) {
+            const int64_t k = bc + 4 * (int64_t)(tid + 256 * q);
+            const int32_t cv[4] = {ct[q].x, ct[q].y, ct[q].z, ct[q].w};
+#pragma unroll
+            for (int e = 0; e < 4; ++e)
+                if (k + e >= e0 && k + e < ce && k + e >= 0 && k + e < nnz) cs[k + e - e0] = cv[e];
+        }
+#pragma unroll
+        for (int q = 0; q < SPTV; ++q) {
+            const int64_t k = bv + EPV * (int64_t)(tid + 256 * q);
+            T tv[EPV];
+            __builtin_memcpy(tv, &vt[q], 16);
+#pragma unroll
+            for (int e = 0; e < EPV; ++e)
+                if (k + e >= e0 && k + e < ce && k + e >= 0 && k + e < nnz) vs[k + e - e0] = tv[e];
+        }
+        __syncthreads();
+    }
+    // Block scan of the row-end flags.  E(i) = ends in local [0, i).  A row
+    // starts at local i when local i - 1 ends one; the owned rows start in
+    // [1, K], so an entry at local i lies in owned row E(i) - 1 when
+    // 0 <= E(i) - 1 < nrows (entries of the row begun before tK count 0 ends,
+    // entries past the last owned row count nrows + 1).
+    int f[EPT], cnt = 0;
+#pragma unroll
+    for (int u = 0; u < EPT; ++u) {
+        const int i = tid * EPT + u;
+        f[u] = i < WIN ? (int)((uint32_t)cs[i] >> 31) : 0;
+        cnt += f[u];
+    }
+    int incl = cnt;
+#pragma unroll
+    for (int o = 1; o < 64; o <<= 1) {
+        const int y = __shfl_up(incl, o, 64);
+        if ((tid & 63) >= o) incl += y;
+    }
+    if ((tid & 63) == 63) wsum[tid >> 6] = incl;
+    if (tid == 0) {
+        bnd[0] = WIN;
+        bnd[1] = 0;
+    }
+    __syncthreads();
+    int Ei = incl - cnt;
+    for (int w = 0; w < (tid >> 6); ++w) Ei += wsum[w];
+    int lo = WIN, hi = 0;
+#pragma unroll
+    for (int u = 0; u < EPT; ++u) {
+        const int i = tid * EPT + u;
+        const int r = Ei - 1;
+        if (i < WIN && r >= 0 && r < nrows) {
+            rid[i] = (uint8_t)r;
+            if ((uint32_t)cs[i - 1] >> 31) rel[r] = i;  // i >= 1 here: local 0 is never owned
+            if (f[u] && r == nrows - 1) rel[nrows] = i + 1;
+            lo = i < lo ? i : lo;
+            hi = i + 1 > hi ? i + 1 : hi;
+        }
+        Ei += f[u];
+    }
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) {
+        const int a2 = __shfl_xor(lo, o, 64), b2 = __shfl_xor(hi, o, 64);
+        lo = a2 < lo ? a2 : lo;
+        hi = b2 > hi ? b2 : hi;
+    }
+    if ((tid & 63) == 0) {
+        atomicMin(&bnd[0], lo);
+        atomicMax(&bnd[1], hi);
+    }
+    __syncthreads();
+    if (nrows <= 0) return;  // block-uniform: a long row from an earlier tile covers this one
+    const int b0 = bnd[0], b1 = bnd[1], N = b1 - b0;
+    const __amdgpu_buffer_rsrc_t xr = lz_rsrc(X, (uint32_t)(nx * ldx * (int64_t)sizeof(T)));
+    const int gi = tid / LPR, p = tid % LPR;
+    const uint32_t rowb = (uint32_t)(ldx * sizeof(T)), lane_off = p * VEC * sizeof(T);
+    Vec<T, VEC> zero;
+#pragma unroll
+    for (int i = 0; i < VEC; ++i) zero.v[i] = T(0);
+    const int Es = ((N + G - 1) / G + UNR - 1) / UNR * UNR;  // slice length, UNR-aligned
+    const int start = b0 + gi * Es, end = (start + Es < b1) ? start + Es : b1;
+    if (start < end) {  // group-uniform
+        int cur = rid[start];
+        bool open = rel[cur] < start;  // cur began in an earlier group's slice
+        Vec<T, VEC> acc = zero;
+        for (int s0 = start; s0 < end; s0 += UNR) {
+            int32_t cc[UNR];
+            T vv[UNR];
+            int rr[UNR];
+#pragma unroll
+            for (int u = 0; u < UNR; ++u) {
+                cc[u] = cs[s0 + u] & 0x7fffffff;
+                vv[u] = vs[s0 + u];
+                rr[u] = rid[s0 + u];
+            }
+            Vec<T, VEC> xs[UNR];
+#pragma unroll
+            for (int u = 0; u < UNR; ++u) {
+                const uint32_t off = s0 + u < end ? __umul24((unsigned)cc[u], rowb) + lane_off : 0x80000000u;
+                xs[u] = ldbuf<T, VEC>(xr, off);
+            }
+#pragma unroll
+            for (int u = 0; u < UNR; ++u) {
+                const int r = s0 + u < end ? rr[u] : cur;
+                if (r != cur) {  // row cur ends inside the slice
+                    if (open) head[gi][p] = acc;
+                    else yt[cur][p] = acc;
+                    acc = zero;
+                    cur = r;
+                    open = false;
+                }
+#pragma unroll
+                for (int i = 0; i < VEC; ++i) acc.v[i] = fma(vv[u], xs[u].v[i], acc.v[i]);
+            }
+        }
+        if (open) head[gi][p] = acc;
+        else yt[cur][p] = acc;
+    }
+    __syncthreads();
+    // rows over several slices: first piece (in yt) + the later groups' heads, in group order
+    for (int r = gi; r < nrows; r += G) {
+        const int a = rel[r] - b0, e = rel[r + 1] - b0;
+        const int g1 = a / Es, g2 = (e - 1) / Es;
+        if (g1 == g2) continue;
+        Vec<T, VEC> sum = yt[r][p];
+        for (int g = g1 + 1; g <= g2; ++g) {
+#pragma unroll
+            for (int i = 0; i < VEC; ++i) sum.v[i] += head[g][p].v[i];
+        }
+        yt[r][p] = sum;
+    }
+    __syncthreads();
+    for (int idx = tid; idx < nrows * LPR; idx += 256) {
+        T *dst = Y + ((int64_t)row0 + idx / LPR) * ldy + (idx % LPR) * VEC;
+        Vec<T, VEC> y = yt[idx / LPR][idx % LPR];
+        if constexpr (sizeof(T) * VEC == 16) {
+            typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
+            u32x4 uu;
+            __builtin_memcpy(&uu, &y, 16);
+            __builtin_nontemporal_store(uu, reinterpret_cast<u32x4 *>(dst));
+        } else {
+            stv<T, VEC>(dst, y);
+        }
+    }
+}
+
+// Build (or reuse) the fixed-nnz format of an operator (cached on the handle
+// by its pointers and sizes; experiment: a caller changing the arrays in
+// place behind the same pointers would see stale flags).  false: the operator
+// has a shape the kernel does not cover (empty rows, rows past S + 1 entries,
+// more than RMAX rows in a tile).
+static int fnz_prepare(lz_handle *h, int64_t n, int64_t nnz, const int64_t *rp, const int32_t *col, bool *ok)
+{
+    *ok = false;
+    const int64_t ntiles = ceil_div(nnz, (int64_t)kFnzK);
+    if (nnz <= 0 || n >= (1LL << 31) || ntiles + 1 >= (1LL << 31)) return LZ_OK;
+    if (h->fnz_key[0] == (int64_t)(uintptr_t)rp && h->fnz_key[1] == (int64_t)(uintptr_t)col && h->fnz_key[2] == n &&
+        h->fnz_key[3] == nnz) {
+        *ok = h->fnz_ok;
+        return LZ_OK;
+    }
+    LZ_HIP_TRY(hipStreamSynchronize(h->stream));
+    (void)hipFree(h->fnz_colf);
+    (void)hipFree(h->fnz_trow);
+    h->fnz_colf = nullptr;
+    h->fnz_trow = nullptr;
+    h->fnz_key[0] = 0;
+    LZ_HIP_TRY(hipMalloc(&h->fnz_colf, sizeof(int32_t) * (size_t)nnz));
+    LZ_HIP_TRY(hipMalloc(&h->fnz_trow, sizeof(int32_t) * (size_t)(ntiles + 1)));
+    int *stats = h->err_flag + 12;  // [0] max row length, [1] empty / negative, [2] max rows per tile
+    LZ_HIP_TRY(hipMemsetAsync(stats, 0, 3 * sizeof(int), h->stream));
+    const int g1 = (int)std::max<int64_t>(1, std::min<int64_t>(ceil_div(n, (int64_t)256), (int64_t)h->n_cu * 8));
+    hipLaunchKernelGGL(k_fnz_flags, dim3(g1), dim3(256), 0, h->stream, n, rp, col, h->fnz_colf, stats);
+    const int g2 = (int)std::max<int64_t>(1, std::min<int64_t>(ceil_div(ntiles + 1, (int64_t)256), (int64_t)h->n_cu * 8));
+    hipLaunchKernelGGL(k_fnz_trow, dim3(g2), dim3(256), 0, h->stream, ntiles, n, rp, kFnzK, h->fnz_trow, stats);
+    LZ_LAUNCH_CHECK();
+    int st[3] = {0, 0, 0};
+    LZ_HIP_TRY(hipMemcpyAsync(st, stats, sizeof(st), hipMemcpyDeviceToHost, h->stream));
+    LZ_HIP_TRY(hipStreamSynchronize(h->stream));
+    h->fnz_ok = st[1] == 0 && st[0] <= kFnzS + 1 && st[2] <= kFnzRmax;
+    h->fnz_key[0] = (int64_t)(uintptr_t)rp;
+    h->fnz_key[1] = (int64_t)(uintptr_t)col;
+    h->fnz_key[2] = n;
+    h->fnz_key[3] = nnz;
+    *ok = h->fnz_ok;
+    return LZ_OK;
+}
+
+template <typename T, int B>
+static int launch_fnz(lz_handle *h, int64_t nnz, const T *val, const T *X, int64_t ldx, int64_t nx, T *Y,
+                      int64_t ldy)
+{
+    const int64_t ntiles = ceil_div(nnz, (int64_t)kFnzK);
+    hipLaunchKernelGGL((k_spmm_fnz<T, B, kFnzK, kFnzS, kFnzRmax>), dim3((unsigned)ntiles), dim3(256), 0, h->stream, nnz,
+                       h->fnz_colf, val, h->fnz_trow, X, ldx, nx, Y, ldy);
+    return LZ_OK;
+}
+
 // nnz-split SpMM with the long-tile queue: the main kernel, then a persistent
 // kernel over the queued tiles (an empty queue costs one short launch).
 template <typename T, int B, int TR, int CAP, bool WIN, bool YCM = false, bool EPI = false>
@@ -838,7 +1162,13 @@ static int launch_spmm_rm(lz_handle *h, int64_t n, int64_t nnz, const int64_t *r
     int rc = LZ_OK;
     if constexpr (S::LPR == 8) {
         const bool wide = (double)nnz > 13.0 * (double)n;
-        if (ycm) {
+        const char *fz = getenv("LZ_SPMM_FNZ");  // experiment: fixed-nnz tiles (read per call)
+        bool fnz = false;
+        if (fz && fz[0] == '1' && !ycm && buf_ok && ldx == B && ldy == B)
+            LZ_TRY(fnz_prepare(h, n, nnz, rp, col, &fnz));
+        if (fnz) {
+            rc = launch_fnz<T, B>(h, nnz, val, X, ldx, nx, Y, ldy);
+        } else if (ycm) {
             if (buf_ok && !wide) rc = launch_seg<T, B, 48, 768, false, true>(h, n, rp, col, val, X, ldx, nx, Y, ldy);
             else if (buf_ok) rc = launch_seg<T, B, 48, 1536, false, true>(h, n, rp, col, val, X, ldx, nx, Y, ldy);
             else if (!wide) rc = launch_seg<T, B, 48, 768, true, true>(h, n, rp, col, val, X, ldx, nx, Y, ldy);

@@ -287,3 +287,25 @@ def test_to_row_major(lz, handle, torch_cuda, b, dtype, ld_pad):
     handle.to_row_major(Xcm, Y)
     torch.cuda.synchronize()
     assert torch.equal(Y, Xcm[:, :rows].t())
+
+
+@pytest.mark.parametrize("n,npr,hw,dtype,b", [(50021, 10.0, 2048, "float64", 16), (3001, 30.0, 100, "float64", 16),
+                                              (100003, 3.0, 500, "float64", 16), (40009, 12.0, 900, "float32", 32),
+                                              (449, 10.0, 40, "float64", 16)])
+def test_spmm_fixed_nnz_tiles(lz, orc, handle, torch_cuda, monkeypatch, n, npr, hw, dtype, b):
+    """LZ_SPMM_FNZ=1: tiles of 448 entries owning the rows that start in them
+    (row ends in the column's bit 31) against the oracle; 3 nnz/row puts > 80
+    rows in a tile, so that operator takes the default kernel."""
+    torch = torch_cuda
+    monkeypatch.setenv("LZ_SPMM_FNZ", "1")
+    npdt = np.float64 if dtype == "float64" else np.float32
+    A = lz.gen_banded(n, npr, hw, seed=n % 997, dtype=npdt)
+    rng = np.random.default_rng(3)
+    X = rng.standard_normal((n, b)).astype(npdt)
+    Y = torch.empty(n, b, dtype=getattr(torch, dtype), device="cuda")
+    Ad = lz.CsrDevice.from_host(A)
+    handle.spmm(Ad, torch.from_numpy(X).cuda(), Y)
+    torch.cuda.synchronize()
+    ref = orc.csr_spmm(A, X)
+    tol = 1e-13 if dtype == "float64" else 1e-5
+    assert np.allclose(Y.cpu().numpy(), ref, rtol=tol, atol=tol * np.abs(ref).max())
