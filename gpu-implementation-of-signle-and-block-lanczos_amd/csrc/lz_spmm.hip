@@ -803,7 +803,7 @@ __global__ __launch_bounds__(256) void k_spmv(int64_t n, const int64_t *__restri
 // row offsets come from one block scan over the staged flags.  Requires: no
 // empty rows, every row <= S + 1 entries, at most RMAX rows per tile, columns
 // < 2^31 (fnz_prepare checks, else the default kernel runs).
-constexpr int kFnzK = 448, kFnzS = 64, kFnzRmax = 80;
+constexpr int kFnzK = 448, kFnzS = 64, kFnzRmax = 88;
 
 __global__ __launch_bounds__(256) void k_fnz_flags(int64_t n, const int64_t *__restrict__ rp,
                                                    const int32_t *__restrict__ col, int32_t *__restrict__ colf,

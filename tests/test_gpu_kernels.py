@@ -294,7 +294,7 @@ def test_to_row_major(lz, handle, torch_cuda, b, dtype, ld_pad):
                                               (449, 10.0, 40, "float64", 16)])
 def test_spmm_fixed_nnz_tiles(lz, orc, handle, torch_cuda, monkeypatch, n, npr, hw, dtype, b):
     """LZ_SPMM_FNZ=1: tiles of 448 entries owning the rows that start in them
-    (row ends in the column's bit 31) against the oracle; 3 nnz/row puts > 80
+    (row ends in the column's bit 31) against the oracle; 3 nnz/row puts > 88
     rows in a tile, so that operator takes the default kernel."""
     torch = torch_cuda
     monkeypatch.setenv("LZ_SPMM_FNZ", "1")
