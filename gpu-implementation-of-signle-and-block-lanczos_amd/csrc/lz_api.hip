@@ -584,9 +584,9 @@ enum { kFormHalo = 0, kFormAllgather = 1 };
 // one communicator the step's small all-reduces never queue behind the
 // exchange.
 template <typename T>
-static int dist_solve(lz_handle *h, int form, HaloPlan *hp, int64_t n, int64_t n_pad, int64_t nnz, const int64_t *rp,
-                      const int32_t *col, const T *val, int b, int m, int64_t lc, const T *B, T *q, T *alpha, T *beta,
-                      T *X0, T *X1)
+static int dist_solve_impl(lz_handle *h, int form, HaloPlan *hp, int64_t n, int64_t n_pad, int64_t nnz,
+                           const int64_t *rp, const int32_t *col, const T *val, int b, int m, int64_t lc, const T *B,
+                           T *q, T *alpha, T *beta, T *X0, T *X1)
 {
     Comm *cm = h->comm;
     const bool ag = form == kFormAllgather;
@@ -706,6 +706,19 @@ static int dist_solve(lz_handle *h, int form, HaloPlan *hp, int64_t n, int64_t n
     LZ_HIP_TRY(hipMemcpyAsync(beta + m * bb, binv[(m - 1) & 1], sizeof(T) * bb, hipMemcpyDeviceToDevice, h->stream));
     if (cm) LZ_TRY(cm->fence(h->stream));  // no peer reads this rank's buffers after the call
     return LZ_OK;
+}
+
+// A rank that fails mid-solve wakes the others of a virtual-rank group (they
+// would otherwise wait at its next collective until the barrier timeout); for
+// RCCL the abort is a no-op and the caller's job control applies.
+template <typename T>
+static int dist_solve(lz_handle *h, int form, HaloPlan *hp, int64_t n, int64_t n_pad, int64_t nnz, const int64_t *rp,
+                      const int32_t *col, const T *val, int b, int m, int64_t lc, const T *B, T *q, T *alpha, T *beta,
+                      T *X0, T *X1)
+{
+    const int rc = dist_solve_impl<T>(h, form, hp, n, n_pad, nnz, rp, col, val, b, m, lc, B, q, alpha, beta, X0, X1);
+    if (rc != LZ_OK && h->comm) h->comm->abort();
+    return rc;
 }
 
 }  // namespace lz
