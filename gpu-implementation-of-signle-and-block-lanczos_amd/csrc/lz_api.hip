@@ -1117,7 +1117,7 @@ static int dist_args(lz_handle *h, lz_dtype dtype, int b, int m)
     return LZ_OK;
 }
 
-int lz_block_lanczos_dist(lz_handle *h, int64_t n_local, int64_t n_pad, int64_t n_global,
+static int lz_block_lanczos_dist_impl(lz_handle *h, int64_t n_local, int64_t n_pad, int64_t n_global,
                           int64_t nnz_local, const int64_t *rp, const int32_t *col,
                           const void *val, lz_dtype dtype, int b, int m, int64_t lc_local,
                           int lc_rank, const void *B_local, void *q, void *alpha, void *beta,
@@ -1141,6 +1141,18 @@ int lz_block_lanczos_dist(lz_handle *h, int64_t n_local, int64_t n_pad, int64_t 
     return dist_solve<float>(h, kFormAllgather, nullptr, n_local, n_pad, nnz_local, rp, col, (const float *)val, b, m,
                              lc, (const float *)B_local, (float *)q, (float *)alpha, (float *)beta, (float *)X_full,
                              (float *)W);
+}
+
+int lz_block_lanczos_dist(lz_handle *h, int64_t n_local, int64_t n_pad, int64_t n_global,
+                          int64_t nnz_local, const int64_t *rp, const int32_t *col,
+                          const void *val, lz_dtype dtype, int b, int m, int64_t lc_local,
+                          int lc_rank, const void *B_local, void *q, void *alpha, void *beta,
+                          void *Q0, void *Q1, void *W, void *X_full)
+{
+    const int rc = lz_block_lanczos_dist_impl(h, n_local, n_pad, n_global, nnz_local, rp, col, val, dtype, b, m,
+                                              lc_local, lc_rank, B_local, q, alpha, beta, Q0, Q1, W, X_full);
+    if (rc != LZ_OK && h && h->comm) h->comm->abort();  // peers must not wait for this rank
+    return rc;
 }
 
 static int halo_init_impl(lz_handle *h, int64_t row0, int64_t n_local, const int64_t *recv_counts,
@@ -1273,7 +1285,7 @@ int lz_halo_exchange(lz_handle *h, lz_dtype dtype, int b, void *X)
     return halo_exchange(h, hp, X, rowb, h->stream);
 }
 
-int lz_block_lanczos_halo(lz_handle *h, int64_t n_local, int64_t nnz_local, const int64_t *rp,
+static int lz_block_lanczos_halo_impl(lz_handle *h, int64_t n_local, int64_t nnz_local, const int64_t *rp,
                           const int32_t *col, const void *val, lz_dtype dtype, int b, int m,
                           int64_t lc_local, int lc_rank, const void *B_local, void *q, void *alpha,
                           void *beta, void *X0, void *X1)
@@ -1294,6 +1306,17 @@ int lz_block_lanczos_halo(lz_handle *h, int64_t n_local, int64_t nnz_local, cons
     return dist_solve<float>(h, kFormHalo, &hp, n_local, n_local, nnz_local, rp, col, (const float *)val, b, m, lc,
                              (const float *)B_local, (float *)q, (float *)alpha, (float *)beta, (float *)X0,
                              (float *)X1);
+}
+
+int lz_block_lanczos_halo(lz_handle *h, int64_t n_local, int64_t nnz_local, const int64_t *rp,
+                          const int32_t *col, const void *val, lz_dtype dtype, int b, int m,
+                          int64_t lc_local, int lc_rank, const void *B_local, void *q, void *alpha,
+                          void *beta, void *X0, void *X1)
+{
+    const int rc = lz_block_lanczos_halo_impl(h, n_local, nnz_local, rp, col, val, dtype, b, m, lc_local, lc_rank,
+                                              B_local, q, alpha, beta, X0, X1);
+    if (rc != LZ_OK && h && h->comm) h->comm->abort();  // peers must not wait for this rank
+    return rc;
 }
 
 }  // extern "C"
