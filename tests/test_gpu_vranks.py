@@ -224,3 +224,37 @@ def test_vranks_failing_rank_aborts_group(lz, torch_cuda):
     with pytest.raises(lz.LanczosError):
         lz.run_virtual_ranks(2, rank_fn)
     assert time.time() - t0 < 60
+
+
+def test_vranks_argument_error_aborts_group(lz, torch_cuda):
+    """A rank whose distributed call fails its argument checks aborts the group
+    inside the library (no Python-side abort involved): the rank waiting in the
+    first collective returns LZ_E_COMM at once instead of at the barrier timeout."""
+    import ctypes
+    import time
+    torch = torch_cuda
+    A = lz.gen_banded(4_000, 5.0, 100, seed=61)
+    bounds = np.array([0, 2000, 4000], np.int64)
+    codes = [None, None]
+
+    def rank_fn(r, h):
+        r0, r1 = int(bounds[r]), int(bounds[r + 1])
+        rp, col, val = _slab(A, r0, r1)
+        ccol, cnt, rows = lz.halo_plan(col, bounds, r)
+        h.halo_init(r0, r1 - r0, cnt, rows)
+        nh = int(rows.size)
+        Ad = lz.CsrDevice.from_host(lz.CsrHost(r1 - r0, rp, ccol, val), n_cols=r1 - r0 + nh)
+        kw = dict(dtype=torch.float64, device="cuda")
+        q, al, be = torch.zeros(4 * 16, **kw), torch.zeros(4, 16, 16, **kw), torch.zeros(5, 16, 16, **kw)
+        X0, X1 = torch.zeros(r1 - r0 + nh, 16, **kw), torch.zeros(r1 - r0 + nh, 16, **kw)
+        Bl = torch.ones(r1 - r0, 16, **kw)
+        m = 0 if r == 1 else 4  # rank 1: m = 0 fails the argument check
+        codes[r] = h.L.lz_block_lanczos_halo(h.ptr, r1 - r0, Ad.nnz, Ad.row_ptr.data_ptr(), Ad.col.data_ptr(),
+                                              Ad.val.data_ptr(), lz.LZ_F64, 16, m, 0, 0, Bl.data_ptr(),
+                                              q.data_ptr(), al.data_ptr(), be.data_ptr(), X0.data_ptr(),
+                                              X1.data_ptr())
+
+    t0 = time.time()
+    lz.run_virtual_ranks(2, rank_fn)
+    assert time.time() - t0 < 60
+    assert codes[1] == -1 and codes[0] == -3, codes  # LZ_E_ARG on rank 1, LZ_E_COMM on rank 0
