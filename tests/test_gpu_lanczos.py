@@ -238,6 +238,28 @@ def test_vector_lanczos(lz, orc, handle, torch_cuda, golden):
         assert np.max(np.abs(r - ro)) <= RITZ_TOL
 
 
+def test_vector_lanczos_c2_full_size(lz, orc, handle, torch_cuda):
+    """BASELINE config C2 as benchmarked: n = 1,000,000, ~1e7 nnz, half width
+    4096, fp64, lc = 84, 30 steps, against the oracle (alpha / beta / q and the
+    Ritz values of the 30 x 30 T)."""
+    torch = torch_cuda
+    A = lz.gen_banded(1_000_000, 10.0, 4096, 20261015)
+    bv = lz.uniform_B(A.n, 1, 20261015)[:, 0].copy()
+    m, lc = 30, 84
+    Ad = lz.CsrDevice.from_host(A)
+    kw = dict(dtype=torch.float64, device="cuda")
+    q, al, be = torch.zeros(m, **kw), torch.zeros(m, **kw), torch.zeros(m, **kw)
+    ws = [torch.empty(A.n, **kw) for _ in range(3)]
+    handle.vector_lanczos(Ad, torch.from_numpy(bv).cuda(), m, lc, q, al, be, *ws)
+    qo, ao, bo = orc.vector_lanczos(A, bv, m, lc)
+    assert np.allclose(al.cpu().numpy(), ao, rtol=1e-9, atol=1e-12)
+    assert np.allclose(be.cpu().numpy(), bo, rtol=1e-9)
+    assert np.allclose(q.cpu().numpy(), qo, rtol=1e-9, atol=1e-14)
+    r = lz.ritz_values(m, 1, al.cpu().numpy(), np.concatenate([be.cpu().numpy(), [0.0]]))
+    ro = lz.ritz_values(m, 1, ao, np.concatenate([bo, [0.0]]))
+    assert np.max(np.abs(r - ro)) <= RITZ_TOL
+
+
 @pytest.mark.parametrize("kernel", ["win", "row", "cs", "cs2"])
 def test_vector_lanczos_heavy_tiles(lz, orc, handle, torch_cuda, monkeypatch, kernel):
     """Power-law rows, every SpMV kernel (LZ_VL_KERNEL): tiles whose CSR run
