@@ -147,9 +147,10 @@ static int block_lanczos_unfused(lz_handle *h, int64_t n, int64_t nnz, const int
 struct Pass1Plan {
     const uint64_t *pairs = nullptr;
     int win = 0;
+    const int16_t *col16 = nullptr;  // 16-bit strip-relative columns when every column is in reach
 };
-static int pass1_plan(lz_handle *h, int64_t n, const int64_t *rp, const int32_t *col, int64_t nx, int64_t row_off,
-                      Pass1Plan *pl)
+static int pass1_plan(lz_handle *h, int64_t n, int64_t nnz, const int64_t *rp, const int32_t *col, int64_t nx,
+                      int64_t row_off, Pass1Plan *pl)
 {
     LZ_TRY(strip_pairs(h, n, rp, &pl->pairs));
     if (nx >= (1 << 24)) {
@@ -157,6 +158,7 @@ static int pass1_plan(lz_handle *h, int64_t n, const int64_t *rp, const int32_t 
         LZ_TRY(gather_window_ok(h, n, rp, col, nx, row_off, &ok));
         pl->win = ok ? 1 : 0;
     }
+    if (nx < (1 << 24) || pl->win) LZ_TRY(col16_plan(h, n, nnz, rp, col, row_off, &pl->col16));
     return LZ_OK;
 }
 
@@ -174,7 +176,7 @@ static int block_lanczos_fused16(lz_handle *h, int64_t n, int64_t nnz, const int
     QfreeBufs qb(h);
     int P = 0;
     Pass1Plan pl;
-    LZ_TRY(pass1_plan(h, n, rp, col, n, 0, &pl));
+    LZ_TRY(pass1_plan(h, n, nnz, rp, col, n, 0, &pl));
     LZ_TRY(gram_partials<double>(h, n, 16, B, B, 16, &P));
     LZ_TRY(sqrtm_pair<double>(h, 16, nullptr, P, beta, qb.binv[0], nullptr));
     const double *in = B, *prev = nullptr;
@@ -182,7 +184,7 @@ static int block_lanczos_fused16(lz_handle *h, int64_t n, int64_t nnz, const int
         double *out = j == 0 ? W : j == 1 ? Q1 : const_cast<double *>(prev);
         const double *bi = qb.binv[j & 1];
         LZ_TRY(fused_spmm16(h, n, rp, col, val, in, n, in, prev, out, bi, j ? qb.P : nullptr, lc, q + j * 16, &P,
-                            pl.pairs, nnz, 0, pl.win));
+                            pl.pairs, nnz, 0, pl.win, 0, pl.col16));
         // alpha_j and P2 = beta_j^-1 alpha_j in one kernel (P1 of this step is consumed)
         LZ_TRY(gram_finish<double>(h, 16, P, 1, alpha + j * bb, h->partials2, bi, qb.P));
         LZ_TRY(fused_update16(h, n, out, in, qb.P, &P));
@@ -608,7 +610,7 @@ static int dist_solve_impl(lz_handle *h, int form, HaloPlan *hp, int64_t n, int6
     if (!ag && hp && cm && h->nranks > 1)
         LZ_TRY(grow_ws(h, &hp->sendbuf, &hp->send_cap, (size_t)std::max<int64_t>(hp->n_send, 1) * rowb));
     Pass1Plan pl;
-    if (f16) LZ_TRY(pass1_plan(h, n, rp, col, nx, own_off, &pl));
+    if (f16) LZ_TRY(pass1_plan(h, n, nnz, rp, col, nx, own_off, &pl));
     SplitPlan sp;
     if (!f16 || fused16_direct(nx, pl.win)) LZ_TRY(split_plan(h, n, rp, col, own_off, own_off + n, &sp));
     h->last_split[0] = sp.on ? sp.i0 : -1;
@@ -631,7 +633,8 @@ static int dist_solve_impl(lz_handle *h, int form, HaloPlan *hp, int64_t n, int6
             int np = 0;
             LZ_TRY(fused_spmm16(h, r1 - r0, rp + r0, col, val, gsrc(jj), nx, wj(jj) + r0 * 16,
                                 jj ? wn(jj) + r0 * 16 : nullptr, wn(jj) + r0 * 16, binv[jj & 1], jj ? P : nullptr, lcr,
-                                q + (int64_t)jj * 16, &np, pl.pairs + r0 / 16, nnz_r, own_off + r0, pl.win, nslab));
+                                q + (int64_t)jj * 16, &np, pl.pairs + r0 / 16, nnz_r, own_off + r0, pl.win, nslab,
+                                pl.col16));
             nslab += np;
         }
         return LZ_OK;
@@ -804,6 +807,7 @@ int lz_finalize(lz_handle *h)
     (void)hipFree(h->longq);
     (void)hipFree(h->cm_buf);
     (void)hipFree(h->ybuf);
+    (void)hipFree(h->c16buf);
     (void)hipFree(h->fnz_colf);
     (void)hipFree(h->fnz_trow);
     if (h->ev_pool) {

@@ -83,6 +83,8 @@ struct lz_handle {
     int64_t last_split[2] = {-1, -1};  // lz_debug_last_split
     // fixed-nnz SpMM format (experiment, lz_spmm.hip fnz_prepare): the operator's
     // columns with row-end flags and each tile's first row, keyed by the operator
+    void *c16buf = nullptr;       // pass 1's 16-bit columns (col16_plan), nnz int16
+    size_t c16_cap = 0;           // bytes
     int32_t *fnz_colf = nullptr, *fnz_trow = nullptr;
     int64_t fnz_key[4] = {0, 0, 0, 0};
     bool fnz_ok = false;

@@ -452,18 +452,19 @@ __global__ __launch_bounds__(64 * NW) void k_fused_update16(int64_t n, double *_
 //   NL > 1: NL loader waves stage alternate tiles, each publishing its tile as
 //     soon as it lands.
 // Rows past n are out of range for the DMA and land as zeros.
-template <int NC, int CAP, bool QREG = false, bool PR = false>
+template <int NC, int CAP, bool QREG = false, bool PR = false, typename CT = int32_t>
 struct FwCfg {
     static constexpr int TR = 16 * NC;
     static constexpr int RP_PIECES = (TR + 2) * 8 / 16;
-    static constexpr int COL_PIECES = (CAP + 8) * 4 / 16;
+    static constexpr int CPP = 16 / (int)sizeof(CT);  // columns per 16-B piece
+    static constexpr int COL_PIECES = (CAP + 2 * CPP) * (int)sizeof(CT) / 16;
     static constexpr int VAL_PIECES = (CAP + 4) * 8 / 16;
     static constexpr int DMA_INSTR =
         ws_instr(RP_PIECES) + ws_instr(COL_PIECES) + ws_instr(VAL_PIECES) + (QREG ? 0 : 2 * NC);
     static_assert(DMA_INSTR <= 63, "vmcnt immediate");
     struct Stage {
         int64_t rp[ws_instr(RP_PIECES) * 128];
-        int32_t col[ws_instr(COL_PIECES) * 256];
+        CT col[ws_instr(COL_PIECES) * 64 * CPP];
         double val[ws_instr(VAL_PIECES) * 128];
         double qt[QREG ? 2 : TR * 16];  // Q_{j-1} rows, per strip in slot order; then scratch
         uint64_t pr[PR ? 128 : 1];        // PR: the tile's strips' row orders (k_strip_pairs)
@@ -554,9 +555,9 @@ __device__ __forceinline__ int fw_sw(int r, int c) { return r * 16 + (c ^ r); }
 //   gather_window_ok, proved every column of the strip lies inside it), so the
 //   buffer-addressed gather keeps working at any n (BASELINE config C4: 40M
 //   rows on one GPU, or the all-gathered block at N >= 2).
-template <int NC, int CAP, int K, int NL, bool WIN = false>
+template <int NC, int CAP, int K, int NL, bool WIN = false, bool C16 = false>
 __global__ __launch_bounds__(64 * (NC + NL)) void k_fused_pp16(
-    int64_t n, const int64_t *__restrict__ rp, const int32_t *__restrict__ col,
+    int64_t n, const int64_t *__restrict__ rp, const int32_t *__restrict__ col, const int16_t *__restrict__ col16,
     const double *__restrict__ val, const double *__restrict__ Wg, int64_t nx,
     const double *__restrict__ Wown, const double *Qbuf, double *Wn,
     const double *__restrict__ binv, const double *__restrict__ beta, int64_t lc,
@@ -564,7 +565,8 @@ __global__ __launch_bounds__(64 * (NC + NL)) void k_fused_pp16(
     const uint64_t *__restrict__ pairs, int64_t row_off)
 {
     constexpr bool BP = true;
-    using C = FwCfg<NC, CAP, true, BP>;
+    using CT = typename std::conditional<C16, int16_t, int32_t>::type;
+    using C = FwCfg<NC, CAP, true, BP, CT>;
     constexpr int TR = C::TR;
 #ifdef LZ_WS_PROBE
     const int dbg = lz_ws_dbg;  // timing masks: bit 0 skips the Q_{j-1} loads, bit 1 the W loads
@@ -625,11 +627,12 @@ __global__ __launch_bounds__(64 * (NC + NL)) void k_fused_pp16(
                 if (spin >= kWsSpin) { *err = 3; break; }
             }
             WS_TL(i, 0);
-            const int64_t ca = kA & ~(int64_t)3, va = kA & ~(int64_t)1;
-            const int64_t cb = (nnz - ca) * 4, vb = (nnz - va) * 8;
+            const int64_t ca = kA & ~(int64_t)(C::CPP - 1), va = kA & ~(int64_t)1;
+            const int64_t cb = (nnz - ca) * (int64_t)sizeof(CT), vb = (nnz - va) * 8;
             const auto rr = __builtin_amdgcn_make_buffer_rsrc(const_cast<int64_t *>(rp + r0), (short)0,
                                                               (int)((r1 - r0 + 1) * 8), 0x00020000);
-            const auto cr = __builtin_amdgcn_make_buffer_rsrc(const_cast<int32_t *>(col + ca), (short)0,
+            const CT *cbase = C16 ? reinterpret_cast<const CT *>(col16) : reinterpret_cast<const CT *>(col);
+            const auto cr = __builtin_amdgcn_make_buffer_rsrc(const_cast<CT *>(cbase + ca), (short)0,
                                                               (int)(cb < 0x7fffffff ? cb : 0x7fffffff), 0x00020000);
             const auto vr = __builtin_amdgcn_make_buffer_rsrc(const_cast<double *>(val + va), (short)0,
                                                               (int)(vb < 0x7fffffff ? vb : 0x7fffffff), 0x00020000);
@@ -740,7 +743,7 @@ __global__ __launch_bounds__(64 * (NC + NL)) void k_fused_pp16(
         asm volatile("" ::: "memory");
         typename C::Stage &S = st[s];
         const int64_t kA = S.rp[0];
-        const int co = (int)(kA & 3), vo = (int)(kA & 1);
+        const int co = (int)(kA & (C::CPP - 1)), vo = (int)(kA & 1);
         const int nrow = (int)(n - r0 < TR ? n - r0 : TR);
         const int runlen = (int)(S.rp[nrow] - kA);
         // the group's two rows of the strip: g and g + 8, or (BP) the rows of
@@ -760,7 +763,10 @@ __global__ __launch_bounds__(64 * (NC + NL)) void k_fused_pp16(
         const int cnt = len0 + len1;
         double y[4] = {0.0, 0.0, 0.0, 0.0};
         if (runlen <= CAP) {  // tile-uniform
-            const int32_t *cp = S.col + co;
+            const CT *cp = S.col + co;
+            // C16: a column is stored as its offset from the strip's first row in
+            // the gather source's numbering (row_off + s0); fold the window base in
+            const uint32_t cb16 = C16 ? (uint32_t)(s0 + row_off) - wb : 0u;
             const double *vp = S.val + vo;
             auto slot = [&](int ff) {
                 const int o = ff < len0 ? o0 + ff : o1 + (ff - len0);
@@ -773,7 +779,8 @@ __global__ __launch_bounds__(64 * (NC + NL)) void k_fused_pp16(
 #pragma unroll
                 for (int tt = 0; tt < 8; ++tt) {
                     const uint32_t off =
-                        f + tt < cnt ? __umul24((unsigned)c[tt] - wb, 128u) + lane_off : 0x80000000u;
+                        f + tt < cnt ? __umul24(C16 ? (unsigned)c[tt] + cb16 : (unsigned)c[tt] - wb, 128u) + lane_off
+                                     : 0x80000000u;
                     const auto u4 = __builtin_amdgcn_raw_buffer_load_b128(xr, off, 0, 0);
                     __builtin_memcpy(&xs[tt], &u4, 16);
                 }
@@ -934,10 +941,56 @@ int gather_window_ok(lz_handle *h, int64_t n, const int64_t *rp, const int32_t *
 // (gather_window_ok), else the 64-bit tile kernel.
 bool fused16_direct(int64_t nx, int win) { return nx < (1 << 24) || win; }
 
+// Pass 1's 16-bit columns (once per solve): col16[k] = col[k] - (first row of
+// row r's 16-row strip + row_off), the strip's own row in the gather source's
+// numbering; a column out of int16 reach sets *bad.
+__global__ __launch_bounds__(256) void k_col16(int64_t n, const int64_t *__restrict__ rp,
+                                               const int32_t *__restrict__ col, int64_t row_off,
+                                               int16_t *__restrict__ col16, int *__restrict__ bad)
+{
+    int out = 0;
+    for (int64_t r = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; r < n; r += (int64_t)gridDim.x * blockDim.x) {
+        const int64_t base = (r & ~(int64_t)15) + row_off;
+        for (int64_t k = rp[r], e = rp[r + 1]; k < e; ++k) {
+            const int64_t d = (int64_t)col[k] - base;
+            out |= (d < -32768) | (d > 32767);
+            col16[k] = (int16_t)d;
+        }
+    }
+    if (out) atomicOr(bad, 1);
+}
+
+int col16_plan(lz_handle *h, int64_t n, int64_t nnz, const int64_t *rp, const int32_t *col, int64_t row_off,
+               const int16_t **out)
+{
+    *out = nullptr;
+    const char *e = getenv("LZ_PASS1_C16");  // "0": 32-bit columns (A/B); read per call
+    if ((e && e[0] == '0') || n <= 0 || nnz <= 0) return LZ_OK;
+    if ((size_t)nnz * 2 > h->c16_cap) {
+        LZ_HIP_TRY(hipStreamSynchronize(h->stream));
+        (void)hipFree(h->c16buf);
+        h->c16buf = nullptr;
+        h->c16_cap = 0;
+        LZ_HIP_TRY(hipMalloc(&h->c16buf, (size_t)nnz * 2));
+        h->c16_cap = (size_t)nnz * 2;
+    }
+    int *flag = h->err_flag + 9;
+    LZ_HIP_TRY(hipMemsetAsync(flag, 0, sizeof(int), h->stream));
+    const int grid = (int)std::max<int64_t>(1, std::min<int64_t>(ceil_div(n, (int64_t)256), (int64_t)h->n_cu * 8));
+    hipLaunchKernelGGL(k_col16, dim3(grid), dim3(256), 0, h->stream, n, rp, col, row_off,
+                       static_cast<int16_t *>(h->c16buf), flag);
+    LZ_LAUNCH_CHECK();
+    int bad = 1;
+    LZ_HIP_TRY(hipMemcpyAsync(&bad, flag, sizeof(int), hipMemcpyDeviceToHost, h->stream));
+    LZ_HIP_TRY(hipStreamSynchronize(h->stream));
+    if (!bad) *out = static_cast<const int16_t *>(h->c16buf);
+    return LZ_OK;
+}
+
 int fused_spmm16(lz_handle *h, int64_t n, const int64_t *rp, const int32_t *col, const double *val,
                  const double *Wg, int64_t nx, const double *Wown, const double *Qbuf, double *Wn,
                  const double *binv, const double *beta, int64_t lc, double *qrow, int *nparts,
-                 const uint64_t *pairs, int64_t nnz, int64_t row_off, int win, int slab_off)
+                 const uint64_t *pairs, int64_t nnz, int64_t row_off, int win, int slab_off, const int16_t *col16)
 {
     const int64_t tiles = ceil_div(n, kFusedRows);
     LZ_ARG_CHECK(tiles >= 1 && tiles < (1LL << 31), "tile count");
@@ -951,11 +1004,13 @@ int fused_spmm16(lz_handle *h, int64_t n, const int64_t *rp, const int32_t *col,
         static_assert(kMaxB * kMaxB >= 256, "h->partials2 holds one 16 x 16 slab per pass-1 block");
         const int ev = prof_begin(h, PROF_SPMM_PASS);
         auto go = [&](auto kern) {  // one folded slab per block, at h->partials2
-            hipLaunchKernelGGL(kern, dim3(grid), dim3(64 * (nc + 2)), 0, h->stream, n, rp, col, val, Wg, nx, Wown,
+            hipLaunchKernelGGL(kern, dim3(grid), dim3(64 * (nc + 2)), 0, h->stream, n, rp, col, col16, val, Wg, nx, Wown,
                                Qbuf, Wn, binv, beta, lc, qrow, h->partials2 + (int64_t)slab_off * 256, h->err_flag,
                                pairs, row_off);
         };
-        if (!wide && buf) go(k_fused_pp16<14, 2376, 3, 2, false>);
+        if (!wide && buf && col16) go(k_fused_pp16<14, 2376, 3, 2, false, true>);
+        else if (!wide && col16) go(k_fused_pp16<14, 2376, 3, 2, true, true>);
+        else if (!wide && buf) go(k_fused_pp16<14, 2376, 3, 2, false>);
         else if (!wide) go(k_fused_pp16<14, 2376, 3, 2, true>);
         else if (buf) go(k_fused_pp16<10, 4400, 2, 2, false>);
         else go(k_fused_pp16<10, 4400, 2, 2, true>);

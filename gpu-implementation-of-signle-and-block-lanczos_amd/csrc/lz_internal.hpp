@@ -51,7 +51,13 @@ int copy_row(lz_handle *h, int b, const T *Q, int64_t ld, int col_major, int64_t
 int fused_spmm16(lz_handle *h, int64_t n, const int64_t *rp, const int32_t *col,
                  const double *val, const double *Wg, int64_t nx, const double *Wown, const double *Wprev,
                  double *Wn, const double *binv, const double *P1, int64_t lc, double *qrow, int *nparts,
-                 const uint64_t *pairs, int64_t nnz, int64_t row_off, int win, int slab_off = 0);
+                 const uint64_t *pairs, int64_t nnz, int64_t row_off, int win, int slab_off = 0,
+                 const int16_t *col16 = nullptr);
+// col16 (col16_plan, once per solve): the columns as int16 offsets from each
+// 16-row strip's own row (row_off + strip start); nullptr: 32-bit columns.
+// Stages 2 B per column instead of 4 (A: 10 B per nonzero instead of 12).
+int col16_plan(lz_handle *h, int64_t n, int64_t nnz, const int64_t *rp, const int32_t *col, int64_t row_off,
+               const int16_t **out);
 // slab_off: this launch's folded slabs go to h->partials2 + slab_off * 256 (a
 // pass split over row ranges writes its launches' slabs side by side); the
 // 64-bit fallback (gather source past 2^24 rows, no window) needs slab_off 0.

@@ -66,6 +66,20 @@ def test_block_b16_stale_lds(lz, orc, handle, torch_cuda, n):
     assert_close_run(lz, m, 16, got, orc.block_lanczos(A, B, m, lc))
 
 
+@pytest.mark.parametrize("c16", ["0", "1"])
+@pytest.mark.parametrize("n,hw", [(60_013, 2048), (100_003, 40_000)])
+def test_block_b16_col16(lz, orc, handle, torch_cuda, monkeypatch, c16, n, hw):
+    """Pass 1 with 16-bit strip-relative columns (LZ_PASS1_C16, default on) and
+    without; half width 40,000 puts columns out of int16 reach of their strip,
+    so that operator keeps 32-bit columns either way."""
+    monkeypatch.setenv("LZ_PASS1_C16", c16)
+    A = lz.gen_banded(n, 10.0, hw, seed=n % 101)
+    B = lz.uniform_B(A.n, 16, seed=9)
+    m, lc = 6, n - 100
+    got = gpu_block(lz, handle, torch_cuda, A, B, m, lc)
+    assert_close_run(lz, m, 16, got, orc.block_lanczos(A, B, m, lc))
+
+
 def test_block_b16_tail_rows(lz, orc, handle, torch_cuda):
     """n not a multiple of the 16-row tiles, lc in the last partial tile."""
     A = lz.gen_banded(1000 * 16 + 11, 7.0, 64, seed=2)
