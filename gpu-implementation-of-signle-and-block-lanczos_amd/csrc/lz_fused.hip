@@ -628,7 +628,10 @@ __global__ __launch_bounds__(64 * (NC + NL)) void k_fused_pp16(
             }
             WS_TL(i, 0);
             const int64_t ca = kA & ~(int64_t)(C::CPP - 1), va = kA & ~(int64_t)1;
-            const int64_t cb = (nnz - ca) * (int64_t)sizeof(CT), vb = (nnz - va) * 8;
+            // buffer range checks are per dword: with 2-B columns the last dword may
+            // hold one real column and one past nnz, so the range ends on a dword
+            // boundary (col16_plan allocates that slack)
+            const int64_t cb = ((nnz - ca) * (int64_t)sizeof(CT) + 3) & ~(int64_t)3, vb = (nnz - va) * 8;
             const auto rr = __builtin_amdgcn_make_buffer_rsrc(const_cast<int64_t *>(rp + r0), (short)0,
                                                               (int)((r1 - r0 + 1) * 8), 0x00020000);
             const CT *cbase = C16 ? reinterpret_cast<const CT *>(col16) : reinterpret_cast<const CT *>(col);
@@ -966,13 +969,14 @@ int col16_plan(lz_handle *h, int64_t n, int64_t nnz, const int64_t *rp, const in
     *out = nullptr;
     const char *e = getenv("LZ_PASS1_C16");  // "0": 32-bit columns (A/B); read per call
     if ((e && e[0] == '0') || n <= 0 || nnz <= 0) return LZ_OK;
-    if ((size_t)nnz * 2 > h->c16_cap) {
+    const size_t bytes = (size_t)nnz * 2 + 16;  // + the dword the kernel's range may end in
+    if (bytes > h->c16_cap) {
         LZ_HIP_TRY(hipStreamSynchronize(h->stream));
         (void)hipFree(h->c16buf);
         h->c16buf = nullptr;
         h->c16_cap = 0;
-        LZ_HIP_TRY(hipMalloc(&h->c16buf, (size_t)nnz * 2));
-        h->c16_cap = (size_t)nnz * 2;
+        LZ_HIP_TRY(hipMalloc(&h->c16buf, bytes));
+        h->c16_cap = bytes;
     }
     int *flag = h->err_flag + 9;
     LZ_HIP_TRY(hipMemsetAsync(flag, 0, sizeof(int), h->stream));

@@ -67,11 +67,14 @@ def test_block_b16_stale_lds(lz, orc, handle, torch_cuda, n):
 
 
 @pytest.mark.parametrize("c16", ["0", "1"])
-@pytest.mark.parametrize("n,hw", [(60_013, 2048), (100_003, 40_000)])
+@pytest.mark.parametrize("n,hw", [(60_013, 2048), (100_003, 40_000), (50_021, 16)])
 def test_block_b16_col16(lz, orc, handle, torch_cuda, monkeypatch, c16, n, hw):
     """Pass 1 with 16-bit strip-relative columns (LZ_PASS1_C16, default on) and
     without; half width 40,000 puts columns out of int16 reach of their strip,
-    so that operator keeps 32-bit columns either way."""
+    so that operator keeps 32-bit columns either way.  n = 50,021 has an odd
+    nnz whose last column is not its strip's first row: the last 4-B word of the
+    16-bit columns holds one real column (a buffer range ending mid-dword once
+    read it as 0)."""
     monkeypatch.setenv("LZ_PASS1_C16", c16)
     A = lz.gen_banded(n, 10.0, hw, seed=n % 101)
     B = lz.uniform_B(A.n, 16, seed=9)
