@@ -167,6 +167,45 @@ struct QfreeBufs {
     explicit QfreeBufs(lz_handle *h) : binv{h->scratch + 4 * 256, h->scratch + 5 * 256}, P(h->scratch + 6 * 256) {}
 };
 
+// The wavefront form of the same step (lz_wf.hip; default when it applies):
+// one launch runs pass 2 of step j and pass 1 of step j + 1, then the sqrtm of
+// G_{j+1} and the alpha kernel.  Buffers: Y_j in Q0 (every step, in place),
+// V_0 = B (read only), V_1 in W, V_2 in Q1, then V_{j+1} over V_{j-1}.
+static int block_lanczos_wf16(lz_handle *h, int64_t n, int64_t nnz, const int64_t *rp, const int32_t *col,
+                              const double *val, int m, int64_t lc, const double *B, double *q, double *alpha,
+                              double *beta, double *Q0, double *Q1, double *W, const Pass1Plan &pl,
+                              const WfPlan &wp)
+{
+    constexpr int64_t bb = 256;
+    (void)nnz;
+    double *binv[2] = {h->scratch + 4 * 256, h->scratch + 5 * 256};
+    double *P1 = h->scratch + 6 * 256, *P2 = h->scratch + 7 * 256;
+    int P = 0;
+    LZ_TRY(gram_partials<double>(h, n, 16, B, B, 16, &P));
+    LZ_TRY(sqrtm_pair<double>(h, 16, nullptr, P, beta, binv[0], nullptr));
+    LZ_TRY(wf_reset16(h, n));
+    // Y_0 = A B, S1_0 = B^T Y_0
+    LZ_TRY(wf_step16(h, n, rp, col, pl.col16, val, pl.pairs, wp, nullptr, nullptr, nullptr, nullptr, nullptr,
+                     nullptr, nullptr, B, Q0, 0, &P));
+    LZ_TRY(alpha_wf16(h, h->partials2, P, binv[0], nullptr, alpha, P2, B, lc, n, q));
+    const double *Vm1 = nullptr, *V0 = B;
+    for (int j = 0; j + 1 < m; ++j) {
+        double *Vn = j == 0 ? W : j == 1 ? Q1 : const_cast<double *>(Vm1);
+        LZ_TRY(wf_step16(h, n, rp, col, pl.col16, val, pl.pairs, wp, Q0, Vm1, V0, Vn, binv[j & 1], j ? P1 : nullptr,
+                         P2, Vn, Q0, j + 1, &P));
+        // beta_{j+1}, its inverse and P1 = beta_j^-1 beta_{j+1} from the G slabs
+        LZ_TRY(sqrtm_pair<double>(h, 16, nullptr, P, beta + (j + 1) * bb, binv[(j + 1) & 1], nullptr,
+                                  h->partials2 + 2 * (int64_t)P * 256, binv[j & 1], P1));
+        LZ_TRY(alpha_wf16(h, h->partials2, P, binv[(j + 1) & 1], P1, alpha + (j + 1) * bb, P2, Vn, lc, n,
+                          q + (j + 1) * 16));
+        Vm1 = V0;
+        V0 = Vn;
+    }
+    LZ_HIP_TRY(hipMemcpyAsync(beta + m * bb, binv[(m - 1) & 1], sizeof(double) * bb, hipMemcpyDeviceToDevice,
+                              h->stream));
+    return LZ_OK;
+}
+
 static int block_lanczos_fused16(lz_handle *h, int64_t n, int64_t nnz, const int64_t *rp, const int32_t *col,
                                  const double *val, int m, int64_t lc, const double *B, double *q,
                                  double *alpha, double *beta, double *Q0, double *Q1, double *W)
@@ -177,6 +216,11 @@ static int block_lanczos_fused16(lz_handle *h, int64_t n, int64_t nnz, const int
     int P = 0;
     Pass1Plan pl;
     LZ_TRY(pass1_plan(h, n, nnz, rp, col, n, 0, &pl));
+    if (!pl.win) {
+        WfPlan wp;
+        LZ_TRY(wf_plan16(h, n, rp, col, &wp));
+        if (wp.ok) return block_lanczos_wf16(h, n, nnz, rp, col, val, m, lc, B, q, alpha, beta, Q0, Q1, W, pl, wp);
+    }
     LZ_TRY(gram_partials<double>(h, n, 16, B, B, 16, &P));
     LZ_TRY(sqrtm_pair<double>(h, 16, nullptr, P, beta, qb.binv[0], nullptr));
     const double *in = B, *prev = nullptr;
@@ -808,6 +852,8 @@ int lz_finalize(lz_handle *h)
     (void)hipFree(h->cm_buf);
     (void)hipFree(h->ybuf);
     (void)hipFree(h->c16buf);
+    (void)hipFree(h->wf_deps);
+    (void)hipFree(h->wf_flags);
     (void)hipFree(h->fnz_colf);
     (void)hipFree(h->fnz_trow);
     if (h->ev_pool) {

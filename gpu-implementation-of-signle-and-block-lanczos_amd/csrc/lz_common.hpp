@@ -88,6 +88,11 @@ struct lz_handle {
     int32_t *fnz_colf = nullptr, *fnz_trow = nullptr;
     int64_t fnz_key[4] = {0, 0, 0, 0};
     bool fnz_ok = false;
+    // wavefront step (lz_wf.hip): per-tile dependency ranges (int2) and
+    // pass-2 tile flags, T + 64 entries each
+    void *wf_deps = nullptr;
+    int *wf_flags = nullptr;
+    size_t wf_cap = 0;
     void *ybuf = nullptr;         // distributed generic-b iteration: the local SpMM result
     size_t ybuf_cap = 0;          // bytes
     void *halo = nullptr;         // lz::HaloPlan when lz_halo_init was called

@@ -293,6 +293,68 @@ int alpha_b2(lz_handle *h, const double *part, int P, const float *binv, float *
     return LZ_OK;
 }
 
+// Wavefront step (lz_wf.hip), b = 16 fp64: S1 = sum of P slabs (V^T Y), S2 =
+// sum of the next P (V^T V_prev); X = S1 binv - S2 P1 (P1 null: S1 binv),
+// alpha = sym(binv X), P2 = binv alpha, q = V[lc] binv.  (alpha_j = Q_j^T W' =
+// beta_j^-1 V_j^T (Y beta_j^-1 - V_{j-1} P1_j), methods/block_lanczos.hpp:155.)
+__global__ __launch_bounds__(kRedThreads) void k_alpha_wf16(const double *__restrict__ part, int P,
+                                                            const double *__restrict__ binv,
+                                                            const double *__restrict__ P1, double *__restrict__ alpha,
+                                                            double *__restrict__ P2, const double *__restrict__ V,
+                                                            int64_t lc_row, double *__restrict__ qrow)
+{
+    constexpr int B = 16, BB = 256;
+    __shared__ double s1[BB], s2[BB], bi[BB], x[BB];
+    __shared__ double scratch[kRedThreads];
+    const int t = threadIdx.x;
+    reduce_slabs(part, P, BB, s1, scratch);
+    if (P1) reduce_slabs(part + (int64_t)P * BB, P, BB, s2, scratch);
+    if (t < BB) bi[t] = binv[t];
+    __syncthreads();
+    const int i = (t & 255) / B, j = t % B;
+    if (t < BB) {
+        double s = 0.0;
+        for (int k = 0; k < B; ++k) s = fma(s1[i * B + k], bi[k * B + j], s);
+        if (P1)
+            for (int k = 0; k < B; ++k) s = fma(-s2[i * B + k], P1[k * B + j], s);
+        x[t] = s;
+    }
+    __syncthreads();
+    double z = 0.0;
+    if (t < BB)
+        for (int k = 0; k < B; ++k) z = fma(bi[i * B + k], x[k * B + j], z);
+    __syncthreads();
+    if (t < BB) s1[t] = z;  // Z = binv X
+    __syncthreads();
+    if (t < BB) {
+        const double a = 0.5 * (s1[i * B + j] + s1[j * B + i]);
+        alpha[t] = a;
+        x[t] = a;
+    }
+    __syncthreads();
+    if (t < BB) {
+        double s = 0.0;
+        for (int k = 0; k < B; ++k) s = fma(bi[i * B + k], x[k * B + j], s);
+        P2[t] = s;
+    }
+    if (lc_row >= 0 && t < B) {
+        double q = 0.0;
+        for (int k = 0; k < B; ++k) q = fma(V[lc_row * B + k], bi[k * B + t], q);
+        qrow[t] = q;
+    }
+}
+
+int alpha_wf16(lz_handle *h, const double *part, int P, const double *binv, const double *P1, double *alpha,
+               double *P2, const double *V, int64_t lc, int64_t n, double *qrow)
+{
+    const int ev = prof_begin(h, PROF_SMALL);
+    hipLaunchKernelGGL(k_alpha_wf16, dim3(1), dim3(kRedThreads), 0, h->stream, part, P, binv, P1, alpha, P2, V,
+                       (lc >= 0 && lc < n) ? lc : (int64_t)-1, qrow);
+    prof_end(h, ev);
+    LZ_LAUNCH_CHECK();
+    return LZ_OK;
+}
+
 int m_b2(lz_handle *h, const double *part, int P, const float *binv, float *M)
 {
     const int ev = prof_begin(h, PROF_SMALL);

@@ -451,26 +451,7 @@ __global__ __launch_bounds__(64 * NW) void k_fused_update16(int64_t n, double *_
 //     scratch and releases the stage after the epilogue.
 //   NL > 1: NL loader waves stage alternate tiles, each publishing its tile as
 //     soon as it lands.
-// Rows past n are out of range for the DMA and land as zeros.
-template <int NC, int CAP, bool QREG = false, bool PR = false, typename CT = int32_t>
-struct FwCfg {
-    static constexpr int TR = 16 * NC;
-    static constexpr int RP_PIECES = (TR + 2) * 8 / 16;
-    static constexpr int CPP = 16 / (int)sizeof(CT);  // columns per 16-B piece
-    static constexpr int COL_PIECES = (CAP + 2 * CPP) * (int)sizeof(CT) / 16;
-    static constexpr int VAL_PIECES = (CAP + 4) * 8 / 16;
-    static constexpr int DMA_INSTR =
-        ws_instr(RP_PIECES) + ws_instr(COL_PIECES) + ws_instr(VAL_PIECES) + (QREG ? 0 : 2 * NC);
-    static_assert(DMA_INSTR <= 63, "vmcnt immediate");
-    struct Stage {
-        int64_t rp[ws_instr(RP_PIECES) * 128];
-        CT col[ws_instr(COL_PIECES) * 64 * CPP];
-        double val[ws_instr(VAL_PIECES) * 128];
-        double qt[QREG ? 2 : TR * 16];  // Q_{j-1} rows, per strip in slot order; then scratch
-        uint64_t pr[PR ? 128 : 1];        // PR: the tile's strips' row orders (k_strip_pairs)
-    };
-    static constexpr int PR_PIECES = NC * 8 / 16 > 0 ? (NC * 8 + 15) / 16 : 1;
-};
+// The stage layout (FwCfg), kPairPad and fw_sw are in lz_kernels.hpp.
 
 // Per 16-row strip: the strip's rows sorted by length (ties by row), packed
 // as 16 nibbles (nibble i = row of rank i; rows past n have length 0).
@@ -478,8 +459,6 @@ struct FwCfg {
 // lane group's two-row list is a long row plus a short one.  (C3 rows: 10 +-
 // 2.2 nnz; a wave steps as long as its longest list: 3.48 steps per strip for
 // the rows (g, g+8), 3.03 for the ranked pairs, 3.00 ideal.)
-constexpr int64_t kPairPad = 16;  // >= strips per pass-1 tile (14)
-
 __global__ __launch_bounds__(256) void k_strip_pairs(int64_t n, const int64_t *__restrict__ rp,
                                                      uint64_t *__restrict__ out)
 {
@@ -533,9 +512,6 @@ int strip_pairs(lz_handle *h, int64_t n, const int64_t *rp, const uint64_t **out
     return LZ_OK;
 }
 
-// 16x16 scratch with XOR swizzle: element (r, c) at r*16 + (c ^ r); the MFMA
-// operand read (16 rows, one column per lane group) hits 16 distinct banks.
-__device__ __forceinline__ int fw_sw(int r, int c) { return r * 16 + (c ^ r); }
 
 // ---------------------------------------------------------------------------
 // Pipelined wave-specialised pass 1.  Timelines of k_fused_ws16

@@ -77,6 +77,29 @@ int fused_update16_swap(lz_handle *h, int64_t n, double *Wn, double *Xown, const
 // C = A*B, 16 x 16 row-major fp64, on the stream
 int mm16(lz_handle *h, const double *A, const double *B, double *C);
 
+// ---- wavefront step, b = 16 fp64, one GPU (lz_wf.hip): pass 2 of step j and
+// pass 1 of step j + 1 in one launch (see the file header)
+struct WfPlan {
+    bool ok = false;       // the wavefront step applies (n < 2^24, narrow column spans)
+    int hback = 0, hfwd = 0;  // max tiles a tile's columns reach below / above it
+};
+// once per solve: per-tile dependency ranges; synchronises the stream once
+int wf_plan16(lz_handle *h, int64_t n, const int64_t *rp, const int32_t *col, WfPlan *pl);
+// zero the pass-2 flags (start of a solve; epochs 1, 2, ... follow)
+int wf_reset16(lz_handle *h, int64_t n);
+// P2 == nullptr: pass 1 only (Y = A Vg, S1 slabs).  Otherwise V_{j+1} = Yj binv
+// - Vprev P1 - Vj P2 into Vout (== Vg; P1 == nullptr: no Vprev term), Y_{j+1}
+// = A Vout into Yo (may be Yj).  Slabs at h->partials2: S1 [0, G), S2 [G, 2G),
+// G [2G, 3G) of 256 doubles, *nparts = G.
+int wf_step16(lz_handle *h, int64_t n, const int64_t *rp, const int32_t *col, const int16_t *col16,
+              const double *val, const uint64_t *pairs, const WfPlan &pl, const double *Yj, const double *Vprev,
+              const double *Vj, double *Vout, const double *binv, const double *P1, const double *P2,
+              const double *Vg, double *Yo, int epoch, int *nparts);
+// alpha = sym(binv (S1 binv - S2 P1)) (P1 == nullptr: no S2 term), P2 = binv alpha,
+// q = V[lc] binv; S1, S2 = the sums of the P slabs at part, part + 256 P
+int alpha_wf16(lz_handle *h, const double *part, int P, const double *binv, const double *P1, double *alpha,
+               double *P2, const double *V, int64_t lc, int64_t n, double *qrow);
+
 // ---- Q-free dense passes, b = 32 fp32 (lz_fused32.hip), around a separate SpMM Y = A W_j
 // pass E: Q_j = Wj binv (registers); Wn = Y binv - Wprev P1 (P1 == null: no
 // Wprev term); slabs (32 x 32 doubles, one per block, *nparts <= 2 n_cu) of

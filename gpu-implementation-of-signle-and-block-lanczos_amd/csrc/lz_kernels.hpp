@@ -166,7 +166,9 @@ __device__ __forceinline__ void ws_dma(__amdgpu_buffer_rsrc_t r, void *lds_base,
 
 // Y rows (g, g+8) of one group: the two rows' entries walked as one list, 8 per
 // step; masked slots read entry o0 and load nothing (out-of-range offset).
-template <typename CP, typename VP>
+// AUX: the gather loads' cache-policy bits (16 = sc1: L2-served, bypassing L1,
+// for a source written inside the same launch).
+template <typename CP, typename VP, int AUX = 0>
 __device__ __forceinline__ void ws_gather(CP cp, VP vp, int o0, int len0, int o1, int cnt,
                                           __amdgpu_buffer_rsrc_t xr, uint32_t lane_off, double y[4],
                                           uint32_t wb = 0)
@@ -186,7 +188,7 @@ __device__ __forceinline__ void ws_gather(CP cp, VP vp, int o0, int len0, int o1
 #pragma unroll
         for (int tt = 0; tt < 8; ++tt) {
             const uint32_t off = f + tt < cnt ? __umul24((unsigned)c[tt] - wb, 128u) + lane_off : 0x80000000u;
-            const auto u4 = __builtin_amdgcn_raw_buffer_load_b128(xr, off, 0, 0);
+            const auto u4 = __builtin_amdgcn_raw_buffer_load_b128(xr, off, 0, AUX);
             __builtin_memcpy(&xs[tt], &u4, 16);
         }
 #pragma unroll
@@ -201,5 +203,34 @@ __device__ __forceinline__ void ws_gather(CP cp, VP vp, int o0, int len0, int o1
         }
     }
 }
+
+// ---- pass-1 stage layout (k_fused_pp16 in lz_fused.hip, k_wf16 in lz_wf.hip) ----
+// Rows past n are out of range for the DMA and land as zeros.
+template <int NC, int CAP, bool QREG = false, bool PR = false, typename CT = int32_t>
+struct FwCfg {
+    static constexpr int TR = 16 * NC;
+    static constexpr int RP_PIECES = (TR + 2) * 8 / 16;
+    static constexpr int CPP = 16 / (int)sizeof(CT);  // columns per 16-B piece
+    static constexpr int COL_PIECES = (CAP + 2 * CPP) * (int)sizeof(CT) / 16;
+    static constexpr int VAL_PIECES = (CAP + 4) * 8 / 16;
+    static constexpr int DMA_INSTR =
+        ws_instr(RP_PIECES) + ws_instr(COL_PIECES) + ws_instr(VAL_PIECES) + (QREG ? 0 : 2 * NC);
+    static_assert(DMA_INSTR <= 63, "vmcnt immediate");
+    struct Stage {
+        int64_t rp[ws_instr(RP_PIECES) * 128];
+        CT col[ws_instr(COL_PIECES) * 64 * CPP];
+        double val[ws_instr(VAL_PIECES) * 128];
+        double qt[QREG ? 2 : TR * 16];  // Q_{j-1} rows, per strip in slot order; then scratch
+        uint64_t pr[PR ? 128 : 1];        // PR: the tile's strips' row orders (k_strip_pairs)
+    };
+    static constexpr int PR_PIECES = NC * 8 / 16 > 0 ? (NC * 8 + 15) / 16 : 1;
+};
+
+
+constexpr int64_t kPairPad = 16;  // >= strips per pass-1 tile (14)
+
+// 16x16 scratch with XOR swizzle: element (r, c) at r*16 + (c ^ r); the MFMA
+// operand read (16 rows, one column per lane group) hits 16 distinct banks.
+__device__ __forceinline__ int fw_sw(int r, int c) { return r * 16 + (c ^ r); }
 
 }  // namespace lz

@@ -1,0 +1,559 @@
+// lz_wf.hip -- the wavefront block-Lanczos step: b = 16, fp64, one GPU.
+//
+// The two-pass Q-free step (lz_fused.hip) runs pass 1 (the SpMM plus its MFMA
+// epilogue) and pass 2 (W'' = W' - W_j P2) as separate launches, because pass
+// 2 needs alpha_j, a sum over every row of pass 1's output.  Pass 1 of the
+// NEXT step needs no such global value if it is written in the unnormalised
+// (beta^2) form, so here one launch runs pass 2 of step j and pass 1 of step
+// j + 1 together, as a wavefront over the rows:
+//
+//   V_j  = W''_{j-1} (unnormalised; Q_j = V_j beta_j^-1), Y_j = A V_j,
+//   V_{j+1} = Y_j beta_j^-1 - V_{j-1} P1_j - V_j P2_j        (pass 2, "updaters")
+//   Y_{j+1} = A V_{j+1};  S1 = V_{j+1}^T Y_{j+1}              (pass 1, "consumers")
+//   G_{j+1} = V_{j+1}^T V_{j+1};  S2 = V_{j+1}^T V_j          (slabs, updaters)
+//
+// and after the launch (two one-workgroup kernels): beta_{j+1} = sqrtm(G),
+// P1_{j+1} = beta_j^-1 beta_{j+1}, alpha_{j+1} = sym(beta^-1 (S1 beta^-1 -
+// S2 P1)), P2 = beta^-1 alpha, q = V_{j+1}[lc] beta^-1.  The products are the
+// reference's (methods/block_lanczos.hpp:137-165: W = A Q1 - Q0 beta,
+// alpha = Q1^T W, W -= Q1 alpha, beta = sqrtm(W^T W)) reassociated:
+// A Q = (A V) beta^-1, Q_{j-1} beta_j = V_{j-1} (beta_{j-1}^-1 beta_j).
+//
+// Bytes per step: A + 5 n b s (Y_j, V_{j-1}, V_j read; V_{j+1}, Y_{j+1}
+// written) against A + 6 n b s for the two passes, and the V_{j+1} rows that
+// pass 1 gathers were written a few hundred rows earlier in the same launch.
+//
+// One 1024-thread block per CU, wave-specialised: NL loaders stage pass-1
+// tiles' CSR runs (k_fused_pp16's ring), NU updaters run pass 2 on a
+// register-prefetched stream of 16-row strips, NC consumers gather and run the
+// S1 epilogue.  Hand-off inside the launch (MI355X_MICROARCH.md, "Valid forms"
+// table, first row): updaters store V_{j+1} write-through (16-B sc1 stores),
+// drain (counted s_waitcnt vmcnt) and publish a per-tile flag with an sc1
+// store; a loader polls the flags of every pass-2 tile its pass-1 tile reads
+// (sc1 loads), then publishes the staged tile through its LDS ready word;
+// every load of V_{j+1} is an sc1 load.  Results do not depend on placement;
+// liveness needs every block resident (one block per CU, grid <= CUs), and
+// every wait is bounded (a timeout sets the device error word).
+#include <climits>
+
+#include "lz_internal.hpp"
+#include "lz_kernels.hpp"
+
+namespace lz {
+
+constexpr int kWfNC = 12, kWfCap = 2112, kWfK = 3, kWfNL = 2, kWfNU = 2;
+constexpr int kWfTR = 16 * kWfNC;   // rows per tile (pass 1 and pass 2)
+constexpr int kWfMaxSpan = 256;     // pass-2 tiles one pass-1 tile may read (flag polls per tile)
+constexpr int kWfAux = 16;          // buffer-instruction cache policy: sc1
+constexpr long kWfSpin = 1L << 21;  // flag polls per tile before the loader gives up (about 2 s)
+
+// Per pass-1 tile t: [lo, hi], the tiles holding its columns, t itself
+// included (pass 1 of tile t overwrites Y rows pass 2 of tile t reads).
+// spans: max(t - lo), max(hi - t), max(hi - lo + 1).
+__global__ __launch_bounds__(256) void k_wf_deps(int64_t n, const int64_t *__restrict__ rp,
+                                                 const int32_t *__restrict__ col, int2 *__restrict__ deps,
+                                                 int *__restrict__ spans)
+{
+    __shared__ int smin[4], smax[4];
+    const int64_t T = ceil_div(n, (int64_t)kWfTR);
+    const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+    for (int64_t t = blockIdx.x; t < T; t += gridDim.x) {
+        const int64_t r0 = t * kWfTR, r1 = r0 + kWfTR < n ? r0 + kWfTR : n;
+        int mn = INT_MAX, mx = -1;
+        for (int64_t k = rp[r0] + threadIdx.x, e = rp[r1]; k < e; k += 256) {
+            const int c = col[k];
+            mn = c < mn ? c : mn;
+            mx = c > mx ? c : mx;
+        }
+#pragma unroll
+        for (int o = 32; o > 0; o >>= 1) {
+            const int a = __shfl_xor(mn, o, 64), b = __shfl_xor(mx, o, 64);
+            mn = a < mn ? a : mn;
+            mx = b > mx ? b : mx;
+        }
+        if (lane == 0) {
+            smin[w] = mn;
+            smax[w] = mx;
+        }
+        __syncthreads();
+        if (threadIdx.x == 0) {
+            for (int i = 1; i < 4; ++i) {
+                mn = smin[i] < mn ? smin[i] : mn;
+                mx = smax[i] > mx ? smax[i] : mx;
+            }
+            int lo = (int)t, hi = (int)t;
+            if (mx >= 0) {
+                const int a = (int)(mn / kWfTR), b = (int)(mx / kWfTR);
+                lo = a < lo ? a : lo;
+                hi = b > hi ? b : hi;
+            }
+            deps[t] = make_int2(lo, hi);
+            atomicMax(&spans[0], (int)t - lo);
+            atomicMax(&spans[1], hi - (int)t);
+            atomicMax(&spans[2], hi - lo + 1);
+        }
+        __syncthreads();
+    }
+}
+
+typedef unsigned v4u32_t __attribute__((ext_vector_type(4)));
+
+// swap a double with the neighbouring lane (l ^ 1) by DPP (quad_perm 1,0,3,2)
+__device__ __forceinline__ double dpp_swap1(double x)
+{
+    int2 v;
+    __builtin_memcpy(&v, &x, 8);
+    v.x = __builtin_amdgcn_mov_dpp(v.x, 0xB1, 0xF, 0xF, false);
+    v.y = __builtin_amdgcn_mov_dpp(v.y, 0xB1, 0xF, 0xF, false);
+    double r;
+    __builtin_memcpy(&r, &v, 8);
+    return r;
+}
+
+// The step kernel.  P2 == nullptr: the first launch of a solve (pass 1 only,
+// on Vg = B; no flags).  P1 == nullptr: no V_{j-1} term (step 0).  Vprev and
+// Vout may alias (V_{j+1} over V_{j-1}: each strip is read, then written, by
+// one wave); Vg == Vout when P2 != nullptr.  part: S1 slabs at [0, G), S2 at
+// [G, 2G), G at [2G, 3G) (256 doubles each, one per block).
+template <int NC, int CAP, int K, int NL, int NU, bool C16>
+__global__ __launch_bounds__(64 * (NC + NL + NU)) void k_wf16(
+    int64_t n, const int64_t *__restrict__ rp, const int32_t *__restrict__ col, const int16_t *__restrict__ col16,
+    const double *__restrict__ val, const uint64_t *__restrict__ pairs, const double *Yj, const double *Vprev,
+    const double *__restrict__ Vj, double *Vout, const double *__restrict__ binv, const double *__restrict__ P1,
+    const double *__restrict__ P2, const double *Vg, double *Yo, const int2 *__restrict__ deps, int *flags, int epoch,
+    int64_t hback, double *__restrict__ part, int *__restrict__ err)
+{
+    using CT = typename std::conditional<C16, int16_t, int32_t>::type;
+    using C = FwCfg<NC, CAP, true, true, CT>;
+    constexpr int TR = C::TR;
+    static_assert(TR == kWfTR, "tile rows");
+    static_assert(NC > 3 && NC <= kPairPad, "strips per tile");
+    __shared__ typename C::Stage st[K];
+    __shared__ double scr[NC][256];     // per consumer: the parked Y tile (swizzled), then its slab
+    __shared__ double ops[3][256];      // beta^-1, -P1, -P2 in MFMA B-operand (permuted) order
+    __shared__ double uscr[NU][512];    // per updater: V_j transpose scratch, then its two slabs
+    __shared__ int ready[K], done[K], cons_in, upd_in;
+    const int lane = threadIdx.x & 63, w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    const bool has_p2 = P2 != nullptr, has_prev = P1 != nullptr;
+    if (threadIdx.x < K) {
+        ready[threadIdx.x] = -1;
+        done[threadIdx.x] = 0;
+    }
+    if (threadIdx.x == 0) {
+        cons_in = 0;
+        upd_in = 0;
+    }
+    if (has_p2)
+        for (int e = threadIdx.x; e < 256; e += blockDim.x) {
+            const int kc = e >> 6, l = e & 63;
+            const int idx = (4 * (l >> 4) + kc) * 16 + (l & 15);
+            ops[0][e] = binv[idx];
+            ops[1][e] = has_prev ? -P1[idx] : 0.0;
+            ops[2][e] = -P2[idx];
+        }
+    __syncthreads();  // the only block barrier
+    const int64_t T = ceil_div(n, (int64_t)TR);
+    const int64_t G = gridDim.x, bid = blockIdx.x;
+    // regions: pass-1 tiles [begin, end) of region x go to the blocks b = x
+    // (mod 8), interleaved; the region's pass-2 tiles are [pbeg, pend), the
+    // same range moved hback tiles down, so the pass-2 wavefront leads
+    int64_t begin, end, kb, KB, pbeg, pend;
+    if (G < 8) {
+        begin = 0; end = T; kb = bid; KB = G; pbeg = 0; pend = T;
+    } else {
+        const int64_t x = bid & 7;
+        begin = T * x / 8;
+        end = T * (x + 1) / 8;
+        kb = bid >> 3;
+        KB = (G - x + 7) >> 3;
+        pbeg = x == 0 ? 0 : (begin - hback > 0 ? begin - hback : 0);
+        pend = x == 7 ? T : (end - hback > 0 ? end - hback : 0);
+    }
+    const int64_t nt = (end - begin - kb + KB - 1) / KB > 0 ? (end - begin - kb + KB - 1) / KB : 0;
+    auto tile_of = [&](int64_t i) { return begin + kb + i * KB; };
+    if (w < NL) {
+        // ------------------------------------------------------------ loaders
+        __builtin_amdgcn_s_setprio(3);
+        const int64_t nnz = rp[n];
+        for (int64_t i = w; i < nt; i += NL) {
+            const int s = (int)(i % K);
+            const int64_t t = tile_of(i);
+            const int64_t r0 = t * TR, r1 = (r0 + TR < n) ? r0 + TR : n;
+            const int64_t kA = rp[r0];
+            if (i >= K) {
+                long spin = 0;
+                const uint32_t da = ws_lds_addr(&done[s]);
+                while (ws_lds_read(da) < NC * (int)(i / K) && ++spin < kWsSpin) __builtin_amdgcn_s_sleep(1);
+                if (spin >= kWsSpin) { *err = 3; break; }
+            }
+            const int64_t ca = kA & ~(int64_t)(C::CPP - 1), va = kA & ~(int64_t)1;
+            const int64_t cb = ((nnz - ca) * (int64_t)sizeof(CT) + 3) & ~(int64_t)3, vb = (nnz - va) * 8;
+            const auto rr = __builtin_amdgcn_make_buffer_rsrc(const_cast<int64_t *>(rp + r0), (short)0,
+                                                              (int)((r1 - r0 + 1) * 8), 0x00020000);
+            const CT *cbase = C16 ? reinterpret_cast<const CT *>(col16) : reinterpret_cast<const CT *>(col);
+            const auto cr = __builtin_amdgcn_make_buffer_rsrc(const_cast<CT *>(cbase + ca), (short)0,
+                                                              (int)(cb < 0x7fffffff ? cb : 0x7fffffff), 0x00020000);
+            const auto vr = __builtin_amdgcn_make_buffer_rsrc(const_cast<double *>(val + va), (short)0,
+                                                              (int)(vb < 0x7fffffff ? vb : 0x7fffffff), 0x00020000);
+            ws_dma(rr, st[s].rp, C::RP_PIECES, lane);
+            ws_dma(cr, st[s].col, C::COL_PIECES, lane);
+            ws_dma(vr, st[s].val, C::VAL_PIECES, lane);
+            {
+                const int64_t s0i = r0 / 16, ns = (n + 15) / 16 + kPairPad;
+                const auto pr = __builtin_amdgcn_make_buffer_rsrc(const_cast<uint64_t *>(pairs + s0i), (short)0,
+                                                                  (int)((ns - s0i) * 8), 0x00020000);
+                ws_dma(pr, st[s].pr, C::PR_PIECES, lane);
+            }
+            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+            if (has_p2) {
+                // every pass-2 tile this tile reads (and its own: its Y rows
+                // are overwritten below) must have published this epoch
+                const int2 d = deps[t];
+                long spin = 0;
+                for (int lo = d.x; lo <= d.y && spin < kWfSpin; lo += 64) {
+                    const int idx = lo + lane;
+                    for (;;) {
+                        const int f = idx <= d.y
+                                          ? __hip_atomic_load(flags + idx, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)
+                                          : epoch;
+                        if (__ballot(f != epoch) == 0) break;
+                        if (++spin >= kWfSpin) break;
+                        __builtin_amdgcn_s_sleep(2);
+                    }
+                }
+                if (spin >= kWfSpin) { *err = 5; break; }
+            }
+            if (lane == 0) ws_lds_write(ws_lds_addr(&ready[s]), (int)i);
+        }
+        return;
+    }
+    if (w < NL + NU) {
+        // ----------------------------------------------------------- updaters
+        const int uw = w - NL;
+        d4_t gacc = {0.0, 0.0, 0.0, 0.0}, sacc = {0.0, 0.0, 0.0, 0.0};
+        double *U = uscr[uw];
+        if (has_p2) {
+            __builtin_amdgcn_s_setprio(1);
+            const int64_t ut0 = pbeg + kb + uw * KB, ustep = (int64_t)NU * KB;
+            const int64_t ntl = ut0 < pend ? (pend - ut0 + ustep - 1) / ustep : 0;
+            const int64_t ns = ntl * NC;  // strips of this wave's tiles, in order
+            const int bytes = (int)(n * 128);
+            const auto Yr = __builtin_amdgcn_make_buffer_rsrc(const_cast<double *>(Yj), (short)0, bytes, 0x00020000);
+            const auto Pr = __builtin_amdgcn_make_buffer_rsrc(const_cast<double *>(has_prev ? Vprev : Vj), (short)0,
+                                                              has_prev ? bytes : 0, 0x00020000);
+            const auto Jr = __builtin_amdgcn_make_buffer_rsrc(const_cast<double *>(Vj), (short)0, bytes, 0x00020000);
+            const auto Or = __builtin_amdgcn_make_buffer_rsrc(Vout, (short)0, bytes, 0x00020000);
+            auto strip_r0 = [&](int64_t s) { return (ut0 + (s / NC) * ustep) * TR + 16 * (s % NC); };
+            struct Ld {
+                double y[4], p[4], j[4];
+            };
+            // A-operand rows (permuted contraction order, as k_fused_pp16):
+            // lane l holds row l & 15, doubles 4 (l >> 4) .. +3 -- two 16-B
+            // loads per matrix.  Six loads per strip, always issued (out of
+            // range past the stream or the rows), so the counted waits below hold.
+            auto fetch = [&](int64_t s, Ld &L) {
+                const uint32_t base =
+                    s < ns ? (uint32_t)(strip_r0(s) * 128) + (uint32_t)((lane & 15) * 128 + (lane >> 4) * 32)
+                           : 0x80000000u;
+#pragma unroll
+                for (int hh = 0; hh < 2; ++hh) {
+                    const auto a = __builtin_amdgcn_raw_buffer_load_b128(Yr, base + 16 * hh, 0, 0);
+                    const auto b = __builtin_amdgcn_raw_buffer_load_b128(Pr, base + 16 * hh, 0, 0);
+                    const auto c = __builtin_amdgcn_raw_buffer_load_b128(Jr, base + 16 * hh, 0, 0);
+                    __builtin_memcpy(&L.y[2 * hh], &a, 16);
+                    __builtin_memcpy(&L.p[2 * hh], &b, 16);
+                    __builtin_memcpy(&L.j[2 * hh], &c, 16);
+                }
+            };
+            const int c = lane & 15, g = lane >> 4;
+            const bool ev = (c & 1) == 0;
+            // strip s: compute on cur, prefetch strip s + 2 into nxt (the set
+            // strip s - 1 used); publish the tile whose last strip is s - 3
+            auto body = [&](int64_t s, Ld &cur, Ld &nxt) {
+                fetch(s + 2, nxt);
+                if (s >= ns) return;
+                d4_t acc = {0.0, 0.0, 0.0, 0.0};
+#pragma unroll
+                for (int kc = 0; kc < 4; ++kc) acc = mfma16(cur.p[kc], ops[1][64 * kc + lane], acc);
+#pragma unroll
+                for (int kc = 0; kc < 4; ++kc) acc = mfma16(cur.y[kc], ops[0][64 * kc + lane], acc);
+#pragma unroll
+                for (int kc = 0; kc < 4; ++kc) acc = mfma16(cur.j[kc], ops[2][64 * kc + lane], acc);
+                // V_j in the accumulator layout (row 4r + g, column c) for S2
+#pragma unroll
+                for (int kc = 0; kc < 4; ++kc) U[fw_sw(c, 4 * g + kc)] = cur.j[kc];
+                wave_lds_sync();
+                double vjc[4];
+#pragma unroll
+                for (int r = 0; r < 4; ++r) vjc[r] = U[fw_sw(4 * r + g, c)];
+#pragma unroll
+                for (int r = 0; r < 4; ++r) gacc = mfma16(acc[r], acc[r], gacc);
+#pragma unroll
+                for (int r = 0; r < 4; ++r) sacc = mfma16(acc[r], vjc[r], sacc);
+                // V_{j+1}: the lane pairs (c, c ^ 1) swap one value per row pair
+                // so each lane stores 16 contiguous bytes (write-through)
+                const uint32_t r0b = (uint32_t)(strip_r0(s) * 128);
+#pragma unroll
+                for (int h2 = 0; h2 < 2; ++h2) {
+                    const double a0 = acc[2 * h2], a1 = acc[2 * h2 + 1];
+                    const double y = dpp_swap1(ev ? a1 : a0);
+                    const double2 v = ev ? make_double2(a0, y) : make_double2(y, a1);
+                    const int row = 4 * (2 * h2 + (ev ? 0 : 1)) + g;
+                    const uint32_t off = r0b + (uint32_t)(row * 128 + (ev ? c : c - 1) * 8);
+                    __builtin_amdgcn_raw_buffer_store_b128(*reinterpret_cast<const v4u32_t *>(&v), Or, off, 0, kWfAux);
+                }
+                if (s % NC == 2 && s >= NC) {
+                    // the last strip of tile s / NC - 1 is s - 3; its two
+                    // stores are followed by at least 22 vector-memory ops
+                    // (three strips' six loads, two strips' two stores), so
+                    // vmcnt(16) has drained them
+                    asm volatile("s_waitcnt vmcnt(16)" ::: "memory");
+                    if (lane == 0)
+                        __hip_atomic_store(flags + ut0 + (s / NC - 1) * ustep, epoch, __ATOMIC_RELAXED,
+                                           __HIP_MEMORY_SCOPE_AGENT);
+                }
+            };
+            Ld R0, R1, R2;
+            fetch(0, R0);
+            fetch(1, R1);
+            for (int64_t s = 0; s < ns; s += 3) {
+                body(s, R0, R2);
+                body(s + 1, R1, R0);
+                body(s + 2, R2, R1);
+            }
+            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+            if (ntl > 0 && lane == 0)
+                __hip_atomic_store(flags + ut0 + (ntl - 1) * ustep, epoch, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        }
+        // the NU updater slabs folded by the last updater to finish
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+            U[((lane >> 4) + 4 * r) * 16 + (lane & 15)] = gacc[r];
+            U[256 + ((lane >> 4) + 4 * r) * 16 + (lane & 15)] = sacc[r];
+        }
+        int arrived = 0;
+        if (lane == 0) arrived = __hip_atomic_fetch_add(&upd_in, 1, __ATOMIC_ACQ_REL, __HIP_MEMORY_SCOPE_WORKGROUP);
+        arrived = __shfl(arrived, 0, 64);
+        if (arrived == NU - 1) {
+            __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
+            for (int e = lane; e < 512; e += 64) {
+                double a = 0.0;
+                for (int u = 0; u < NU; ++u) a += uscr[u][e];
+                // e < 256: G slab (at 2G), else S2 (at G)
+                part[(e < 256 ? 2 * G : G) * 256 + bid * 256 + (e & 255)] = a;
+            }
+        }
+        return;
+    }
+    // -------------------------------------------------------------- consumers
+    const int cw = w - NL - NU;
+    {
+        const int pr = (cw * 3) / NC;
+        if (pr == 1) __builtin_amdgcn_s_setprio(1);
+        else if (pr == 2) __builtin_amdgcn_s_setprio(2);
+    }
+    const int bytes = (int)(n * 128);
+    const auto xr = __builtin_amdgcn_make_buffer_rsrc(const_cast<double *>(Vg), (short)0, bytes, 0x00020000);
+    const auto yr = __builtin_amdgcn_make_buffer_rsrc(Yo, (short)0, bytes, 0x00020000);
+    double *S0 = scr[cw];
+    d4_t macc = {0.0, 0.0, 0.0, 0.0};
+    double v1[4] = {0.0, 0.0, 0.0, 0.0};  // the pending strip's own V_{j+1} rows, accumulator layout
+    int64_t s0p = -1;
+    // S1 += V_{j+1}^T Y over the pending strip (Y parked in S0, swizzled)
+    auto epilogue = [&]() {
+        double ya[4];
+#pragma unroll
+        for (int r = 0; r < 4; ++r) ya[r] = S0[fw_sw(4 * r + (lane >> 4), lane & 15)];
+#pragma unroll
+        for (int r = 0; r < 4; ++r) macc = mfma16(v1[r], ya[r], macc);
+    };
+    for (int64_t i = 0; i < nt; ++i) {
+        const int s = (int)(i % K);
+        const int64_t r0 = tile_of(i) * TR;
+        const int64_t s0 = r0 + 16 * cw;
+        const int g = lane >> 3, p = lane & 7;
+        const uint32_t lane_off = 16u * p;
+        long spin = 0;
+        while (__hip_atomic_load(&ready[s], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP) != (int)i &&
+               ++spin < kWsSpin)
+            __builtin_amdgcn_s_sleep(1);
+        if (spin >= kWsSpin) { *err = 4; break; }
+        asm volatile("" ::: "memory");
+        typename C::Stage &S = st[s];
+        const int64_t kA = S.rp[0];
+        const int co = (int)(kA & (C::CPP - 1)), vo = (int)(kA & 1);
+        const int nrow = (int)(n - r0 < TR ? n - r0 : TR);
+        const int runlen = (int)(S.rp[nrow] - kA);
+        const uint64_t pw = S.pr[cw];
+        const int ra = (int)(pw >> (4 * g)) & 15, rb = (int)(pw >> (4 * (15 - g))) & 15;
+        const int lra = 16 * cw + ra, lrb = 16 * cw + rb;
+        const int o0 = lra < nrow ? (int)(S.rp[lra] - kA) : 0;
+        const int len0 = lra < nrow ? (int)(S.rp[lra + 1] - kA) - o0 : 0;
+        const int o1 = lrb < nrow ? (int)(S.rp[lrb] - kA) : 0;
+        const int len1 = lrb < nrow ? (int)(S.rp[lrb + 1] - kA) - o1 : 0;
+        const int cnt = len0 + len1;
+        double y[4] = {0.0, 0.0, 0.0, 0.0};
+        if (runlen <= CAP) {  // tile-uniform
+            const CT *cp = S.col + co;
+            const uint32_t cb16 = C16 ? (uint32_t)s0 : 0u;
+            const double *vp = S.val + vo;
+            auto slot = [&](int ff) {
+                const int o = ff < len0 ? o0 + ff : o1 + (ff - len0);
+                return ff < cnt ? o : o0;
+            };
+            auto issue = [&](int f, double2 *xs) {
+                int32_t cc[8];
+#pragma unroll
+                for (int tt = 0; tt < 8; ++tt) cc[tt] = cp[slot(f + tt)];
+#pragma unroll
+                for (int tt = 0; tt < 8; ++tt) {
+                    const uint32_t off = f + tt < cnt
+                                             ? __umul24(C16 ? (unsigned)cc[tt] + cb16 : (unsigned)cc[tt], 128u) + lane_off
+                                             : 0x80000000u;
+                    const auto u4 = __builtin_amdgcn_raw_buffer_load_b128(xr, off, 0, kWfAux);
+                    __builtin_memcpy(&xs[tt], &u4, 16);
+                }
+            };
+            auto fmas = [&](int f, const double2 *xs) {
+#pragma unroll
+                for (int tt = 0; tt < 8; ++tt) {
+                    const double v = vp[slot(f + tt)];
+                    if (f + tt < len0) {
+                        y[0] = fma(v, xs[tt].x, y[0]);
+                        y[1] = fma(v, xs[tt].y, y[1]);
+                    } else {  // masked entries: x == 0, v finite
+                        y[2] = fma(v, xs[tt].x, y[2]);
+                        y[3] = fma(v, xs[tt].y, y[3]);
+                    }
+                }
+            };
+            double2 xs[8];
+            issue(0, xs);  // step 0 for every lane (masked past cnt)
+            if (s0p >= 0) epilogue();
+            fmas(0, xs);
+            for (int f = 8; f < cnt; f += 8) {  // group-uniform
+                issue(f, xs);
+                fmas(f, xs);
+            }
+        } else {  // long run (rare): epilogue first, then gather from global
+            if (s0p >= 0) epilogue();
+            ws_gather<const int32_t *, const double *, kWfAux>(col + kA, val + kA, o0, len0, o1, cnt, xr, lane_off,
+                                                               y, 0u);
+        }
+        // the CSR stage is no longer read by this wave
+        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+        if (lane == 0) atomicAdd(&done[s], 1);
+        // Y rows out (16 B per lane per row; rows past n out of range), Y
+        // parked for the S1 epilogue, the strip's own V_{j+1} rows loaded
+        {
+            const auto st0 = make_double2(y[0], y[1]), st1 = make_double2(y[2], y[3]);
+            const uint32_t oa = (uint32_t)((s0 + ra) * 128) + lane_off, ob = (uint32_t)((s0 + rb) * 128) + lane_off;
+            __builtin_amdgcn_raw_buffer_store_b128(*reinterpret_cast<const v4u32_t *>(&st0), yr,
+                                                   s0 + ra < n ? oa : 0x80000000u, 0, 0);
+            __builtin_amdgcn_raw_buffer_store_b128(*reinterpret_cast<const v4u32_t *>(&st1), yr,
+                                                   s0 + rb < n ? ob : 0x80000000u, 0, 0);
+        }
+        S0[fw_sw(ra, 2 * p)] = y[0];
+        S0[fw_sw(ra, 2 * p + 1)] = y[1];
+        S0[fw_sw(rb, 2 * p)] = y[2];
+        S0[fw_sw(rb, 2 * p + 1)] = y[3];
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+            const int64_t row = s0 + (lane >> 4) + 4 * r;
+            const uint32_t off = row < n ? (uint32_t)(row * 128 + (lane & 15) * 8) : 0x80000000u;
+            const auto u = __builtin_amdgcn_raw_buffer_load_b64(xr, off, 0, kWfAux);
+            __builtin_memcpy(&v1[r], &u, 8);
+        }
+        s0p = s0;
+        wave_lds_sync();
+    }
+    if (s0p >= 0) epilogue();
+    // the block's NC consumer slabs folded into one at part[bid] (S1) by the
+    // last consumer to finish, in a fixed order
+#pragma unroll
+    for (int r = 0; r < 4; ++r) S0[((lane >> 4) + 4 * r) * 16 + (lane & 15)] = macc[r];
+    int arrived = 0;
+    if (lane == 0) arrived = __hip_atomic_fetch_add(&cons_in, 1, __ATOMIC_ACQ_REL, __HIP_MEMORY_SCOPE_WORKGROUP);
+    arrived = __shfl(arrived, 0, 64);
+    if (arrived == NC - 1) {
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
+        double *slab = part + bid * 256;
+        for (int e = lane; e < 256; e += 64) {
+            double a[4] = {0.0, 0.0, 0.0, 0.0};
+            int sl = 0;
+            for (; sl + 3 < NC; sl += 4) {
+#pragma unroll
+                for (int q = 0; q < 4; ++q) a[q] += scr[sl + q][e];
+            }
+            for (; sl < NC; ++sl) a[0] += scr[sl][e];
+            slab[e] = (a[0] + a[1]) + (a[2] + a[3]);
+        }
+    }
+}
+
+int wf_plan16(lz_handle *h, int64_t n, const int64_t *rp, const int32_t *col, WfPlan *pl)
+{
+    pl->ok = false;
+    const char *e = getenv("LZ_PASS_WF");  // "1": the wavefront step (opt-in while it is slower); read per call
+    if (!(e && e[0] == '1') || n < kWfTR || n >= (1 << 24)) return LZ_OK;
+    const int64_t T = ceil_div(n, (int64_t)kWfTR);
+    if ((size_t)T + 64 > h->wf_cap) {
+        LZ_HIP_TRY(hipStreamSynchronize(h->stream));
+        (void)hipFree(h->wf_deps);
+        (void)hipFree(h->wf_flags);
+        h->wf_deps = nullptr;
+        h->wf_flags = nullptr;
+        h->wf_cap = 0;
+        LZ_HIP_TRY(hipMalloc(&h->wf_deps, sizeof(int2) * (size_t)(T + 64)));
+        LZ_HIP_TRY(hipMalloc(&h->wf_flags, sizeof(int) * (size_t)(T + 64)));
+        h->wf_cap = (size_t)T + 64;
+    }
+    int *spans = h->err_flag + 12;  // err_flag[0]: device error word; [8], [9]: other plans
+    LZ_HIP_TRY(hipMemsetAsync(spans, 0, 3 * sizeof(int), h->stream));
+    const int grid = (int)std::max<int64_t>(1, std::min<int64_t>(T, (int64_t)h->n_cu * 8));
+    hipLaunchKernelGGL(k_wf_deps, dim3(grid), dim3(256), 0, h->stream, n, rp, col,
+                       static_cast<int2 *>(h->wf_deps), spans);
+    LZ_LAUNCH_CHECK();
+    int sp[3] = {0, 0, 0};
+    LZ_HIP_TRY(hipMemcpyAsync(sp, spans, sizeof(sp), hipMemcpyDeviceToHost, h->stream));
+    LZ_HIP_TRY(hipStreamSynchronize(h->stream));
+    pl->hback = sp[0];
+    pl->hfwd = sp[1];
+    pl->ok = sp[2] <= kWfMaxSpan;
+    return LZ_OK;
+}
+
+int wf_step16(lz_handle *h, int64_t n, const int64_t *rp, const int32_t *col, const int16_t *col16,
+              const double *val, const uint64_t *pairs, const WfPlan &pl, const double *Yj, const double *Vprev,
+              const double *Vj, double *Vout, const double *binv, const double *P1, const double *P2,
+              const double *Vg, double *Yo, int epoch, int *nparts)
+{
+    LZ_ARG_CHECK(pl.ok && n < (1 << 24), "wavefront step: wf_plan16 first");
+    LZ_ARG_CHECK(pairs != nullptr, "strip row orders (strip_pairs) missing");
+    LZ_ARG_CHECK(P2 == nullptr || (Yj && Vj && Vout && binv && Vg == Vout), "wavefront step buffers");
+    static_assert(kWfNC <= kPairPad, "row orders must cover the last tile's strips");
+    const int grid = (int)std::max<int64_t>(1, std::min<int64_t>(ceil_div(n, (int64_t)kWfTR), h->n_cu));
+    const int ev = prof_begin(h, PROF_SPMM_PASS);
+    auto go = [&](auto kern) {
+        hipLaunchKernelGGL(kern, dim3(grid), dim3(64 * (kWfNC + kWfNL + kWfNU)), 0, h->stream, n, rp, col, col16, val,
+                           pairs, Yj, Vprev, Vj, Vout, binv, P1, P2, Vg, Yo,
+                           static_cast<const int2 *>(h->wf_deps), h->wf_flags, epoch, (int64_t)pl.hback,
+                           h->partials2, h->err_flag);
+    };
+    if (col16) go(k_wf16<kWfNC, kWfCap, kWfK, kWfNL, kWfNU, true>);
+    else go(k_wf16<kWfNC, kWfCap, kWfK, kWfNL, kWfNU, false>);
+    prof_end(h, ev);
+    LZ_LAUNCH_CHECK();
+    *nparts = grid;
+    return LZ_OK;
+}
+
+int wf_reset16(lz_handle *h, int64_t n)
+{
+    const int64_t T = ceil_div(n, (int64_t)kWfTR);
+    LZ_ARG_CHECK((size_t)T <= h->wf_cap, "wf_plan16 first");
+    LZ_HIP_TRY(hipMemsetAsync(h->wf_flags, 0, sizeof(int) * (size_t)T, h->stream));
+    return LZ_OK;
+}
+
+}  // namespace lz

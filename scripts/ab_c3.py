@@ -78,7 +78,7 @@ def main():
                 if not d < 1e-9:
                     raise RuntimeError(f"alpha differs under {c}: {d}")
                 r["p1"].append(p1 / c1)
-                r["p2"].append(p2 / c2)
+                r["p2"].append(p2 / c2 if c2 else 0.0)
                 r["it"].append(ev0.elapsed_time(ev1) / m)
             if args.spmm or args.spmm_only:
                 h.spmm(Ad, Bd, Y)
