@@ -56,10 +56,27 @@ def spmm_bytes(n, nnz, b, sv=8):
     return nnz * (sv + 4) + (n + 1) * 8 + 2 * n * b * sv
 
 
-def fused_pass_bytes(n, nnz, b, sv=8):
-    """Algorithmic bytes of one fused pass-1 launch (Q-free iteration): A, the
-    Krylov block W_j read once, W_{j-1} read, W' written."""
-    return nnz * (sv + 4) + (n + 1) * 8 + 3 * n * b * sv
+def col_bytes(n, hw):
+    """Bytes per stored column index in the fused passes: 2 when every column is
+    within int16 reach of its 16-row strip (col16_plan; banded operators with
+    half-width < 32752 below 2^24 rows, LZ_PASS1_C16 not 0), else 4."""
+    c16 = os.environ.get("LZ_PASS1_C16", "1") != "0" and hw + 15 <= 32767 and n < (1 << 24)
+    return 2 if c16 else 4
+
+
+def fused_pass_bytes(n, nnz, b, sv=8, cb=4):
+    """Algorithmic bytes of one fused pass-1 launch (Q-free iteration): A (cb-byte
+    columns), the Krylov block W_j read once, W_{j-1} read, W' written."""
+    return nnz * (sv + cb) + (n + 1) * 8 + 3 * n * b * sv
+
+
+def wf_bytes(n, nnz, b, launches, sv=8, cb=2):
+    """Algorithmic bytes of `launches` wavefront-step launches of one solve
+    (lz_wf.hip): the first is pass 1 only (A, B gathered once, Y written), each
+    later one A + 5 n b s (Y_j, V_{j-1}, V_j read; V_{j+1}, Y_{j+1} written)."""
+    a = nnz * (sv + cb) + (n + 1) * 8
+    nb = n * b * sv
+    return (a + 2 * nb) + max(launches - 1, 0) * (a + 5 * nb)
 
 
 # MFMA work of the dense step per row (b = 16, v_mfma_f64_16x16x4f64 = 2048 FLOP):
@@ -68,6 +85,17 @@ def fused_pass_bytes(n, nnz, b, sv=8):
 # slab W''^T W'' (4) = 8 MFMAs.
 PASS1_MFMA_FLOP_PER_ROW = 16 * 2048 // 16
 PASS2_MFMA_FLOP_PER_ROW = 8 * 2048 // 16
+
+
+def wf_kernel(n, hw):
+    """(full name, PMC short name) of the wavefront-step kernel (lz_wf.hip wf_step16)."""
+    c16 = col_bytes(n, hw) == 2
+    return f"k_wf16<12,2112,3,2,2,{3 if c16 else 2},{'true' if c16 else 'false'}>", "k_wf16"
+
+
+# MFMA work of the wavefront step per row: updaters 12 (V_{j+1}) + 4 (G) + 4 (S2),
+# consumers 4 (S1) per 16-row strip
+WF_MFMA_FLOP_PER_ROW = 24 * 2048 // 16
 
 
 def fused_kernel(nnz, n):
@@ -90,7 +118,7 @@ def spmm_kernel(nnz, n):
 
 # the source file of each profiled kernel: a committed counter file is used only
 # while that file is byte-identical to the one profiled (profiles record its sha256)
-KERNEL_SRC = {"k_fused_pp16": "lz_fused.hip", "k_fused_update16": "lz_fused.hip", "k_spmm_seg": "lz_spmm.hip",
+KERNEL_SRC = {"k_wf16": "lz_wf.hip", "k_fused_pp16": "lz_fused.hip", "k_fused_update16": "lz_fused.hip", "k_spmm_seg": "lz_spmm.hip",
               "k_fused_el32": "lz_fused32.hip", "k_fused_ub32": "lz_fused32.hip", "k_gram16_f64": "lz_dense.hip",
               "k_gram32_f32": "lz_dense.hip"}
 CSRC = os.path.join(ROOT, "gpu-implementation-of-signle-and-block-lanczos_amd", "csrc")
@@ -618,15 +646,43 @@ def main():
         t_upd = upd_ms / max(upd_cnt, 1) * 1e-3 if upd_cnt else None
         roof = mfma = None
         hw = args.halfwidth
-        if fused and t_pass:
-            ach = fused_pass_bytes(n, A.nnz, b) / t_pass / 1e9
+        cb = col_bytes(n, hw)
+        # the wavefront step (lz_wf.hip) has no separate update pass
+        wf = fused and world == 1 and spmm_cnt > 0 and upd_cnt == 0
+        if fused and wf:
+            # one solve of K steps: K launches, the first pass 1 only
+            tot = wf_bytes(n, A.nnz, b, spmm_cnt, cb=cb)
+            ach = tot / (spmm_ms * 1e-3) / 1e9
+            kname, kshort = wf_kernel(n, hw)
+            traffic, tsrc = pmc_traffic(kshort, n, A.nnz, hw, kname)
+            roof = {"bound": "hbm", "kernel": kname, "achieved": round(ach, 1),
+                    "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": round(ach / HBM_PEAK_GBS, 4),
+                    "traffic": traffic, "traffic_unit": "bytes/launch (mean over the profiled solve's launches)",
+                    "traffic_source": tsrc, "avg_ms": round(t_pass * 1e3, 4),
+                    "bytes_per_launch": round(tot / spmm_cnt),
+                    "bytes_note": f"{spmm_cnt} launches per solve: the first pass 1 only (A + 2nbs), the others "
+                                  f"pass 2 of step j + pass 1 of step j+1 (A + 5nbs); A with {cb}-byte columns"}
+            fl = WF_MFMA_FLOP_PER_ROW * n
+            tf = fl / t_pass / 1e12
+            ent = {"kernel": kshort, "mfma_flop_per_launch": fl, "avg_ms": round(t_pass * 1e3, 4),
+                   "achieved": round(tf, 3), "frac": round(tf / FP64_MFMA_PEAK_TFS, 4)}
+            d, src = pmc_record("mfma", kshort, n, A.nnz, hw, kname)
+            if d:
+                ent.update({"pmc_MfmaUtil_pct": d.get("MfmaUtil_pct"),
+                            "pmc_mfma_flop_per_launch": d.get("mfma_flop_per_launch"), "pmc_source": src})
+            else:
+                ent["pmc_note"] = src
+            mfma = {"unit": "TFLOP/s", "peak": FP64_MFMA_PEAK_TFS, "dtype": "f64 (v_mfma_f64_16x16x4f64)",
+                    "wavefront_step": ent}
+        elif fused and t_pass:
+            ach = fused_pass_bytes(n, A.nnz, b, cb=cb) / t_pass / 1e9
             kname, kshort = fused_kernel(A.nnz, n)
             traffic, tsrc = pmc_traffic(kshort, n, A.nnz, hw, kname)
             roof = {"bound": "hbm", "kernel": kname, "achieved": round(ach, 1),
                     "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": round(ach / HBM_PEAK_GBS, 4),
                     "traffic": traffic, "traffic_unit": "bytes/launch", "traffic_source": tsrc,
                     "avg_ms": round(t_pass * 1e3, 4),
-                    "bytes_per_launch": fused_pass_bytes(n, A.nnz, b)}
+                    "bytes_per_launch": fused_pass_bytes(n, A.nnz, b, cb=cb)}
             # MFMA utilisation of the dense step (north star): algorithmic MFMA FLOP / kernel time
             # against the fp64 MFMA peak, plus the rocprofv3 MfmaUtil counter of the same kernels
             mfma = {"unit": "TFLOP/s", "peak": FP64_MFMA_PEAK_TFS, "dtype": "f64 (v_mfma_f64_16x16x4f64)",
@@ -650,8 +706,9 @@ def main():
             roof = {"bound": "hbm", "kernel": plain["kernel"], "achieved": plain["achieved_GBs"],
                     "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": plain["frac_of_hbm_peak"], "traffic": None}
         # iteration roofline: SURVEY.md 8(d)'s fixed convention (A + 8 n b s) and the bytes the
-        # Q-free design actually moves (A + 6 n b s); per rank
+        # design actually moves (A + 6 n b s two-pass, A + 5 n b s wavefront); per rank
         a_bytes = A.nnz * 12 + (n + 1) * 8
+        step_nbs = 5 if wf else 6
         it_s = elapsed / K
         if c4:
             workload = (f"C4 block Lanczos b=16 fp64, banded-random symmetric CSR n={n_total} total "
@@ -695,10 +752,12 @@ def main():
                                                f"a separate {K_bd}-step run with every class recorded"},
                 "iteration_frac_of_roofline": round((a_bytes + 8 * n * b * 8) / it_s / 1e9 / HBM_PEAK_GBS, 4),
                 "iteration_min_bytes": a_bytes + 8 * n * b * 8,
-                "iteration_frac_qfree_bytes": round((a_bytes + 6 * n * b * 8) / it_s / 1e9 / HBM_PEAK_GBS, 4),
-                "iteration_qfree_bytes": a_bytes + 6 * n * b * 8,
+                "iteration_frac_qfree_bytes": round((a_bytes + step_nbs * n * b * 8) / it_s / 1e9 / HBM_PEAK_GBS, 4),
+                "iteration_qfree_bytes": a_bytes + step_nbs * n * b * 8,
                 "iteration_bytes_note": "min_bytes: SURVEY.md 8(d) convention A + 8nbs (fixed); qfree_bytes: "
-                                        "A + 6nbs, what the implemented Q-free iteration moves",
+                                        f"A + {step_nbs}nbs, what the implemented Q-free "
+                                        f"{'wavefront' if wf else 'two-pass'} step moves",
+                "step_form": "wavefront (lz_wf.hip)" if wf else ("two-pass (lz_fused.hip)" if fused else "unfused"),
                 # the gather-bound pass's natural unit: nonzeros (one 128-B X row gathered each) per second,
                 # comparable across C3 (10 nnz/row) and C4 (25 nnz/row)
                 "nnz_per_s_per_gpu": round(A.nnz * K / elapsed, 1),

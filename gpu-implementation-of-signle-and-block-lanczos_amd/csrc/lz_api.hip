@@ -218,7 +218,7 @@ static int block_lanczos_fused16(lz_handle *h, int64_t n, int64_t nnz, const int
     LZ_TRY(pass1_plan(h, n, nnz, rp, col, n, 0, &pl));
     if (!pl.win) {
         WfPlan wp;
-        LZ_TRY(wf_plan16(h, n, rp, col, &wp));
+        LZ_TRY(wf_plan16(h, n, nnz, rp, col, &wp));
         if (wp.ok) return block_lanczos_wf16(h, n, nnz, rp, col, val, m, lc, B, q, alpha, beta, Q0, Q1, W, pl, wp);
     }
     LZ_TRY(gram_partials<double>(h, n, 16, B, B, 16, &P));

@@ -84,7 +84,7 @@ struct WfPlan {
     int hback = 0, hfwd = 0;  // max tiles a tile's columns reach below / above it
 };
 // once per solve: per-tile dependency ranges; synchronises the stream once
-int wf_plan16(lz_handle *h, int64_t n, const int64_t *rp, const int32_t *col, WfPlan *pl);
+int wf_plan16(lz_handle *h, int64_t n, int64_t nnz, const int64_t *rp, const int32_t *col, WfPlan *pl);
 // zero the pass-2 flags (start of a solve; epochs 1, 2, ... follow)
 int wf_reset16(lz_handle *h, int64_t n);
 // P2 == nullptr: pass 1 only (Y = A Vg, S1 slabs).  Otherwise V_{j+1} = Yj binv

@@ -57,6 +57,7 @@ __global__ __launch_bounds__(256) void k_wf_deps(int64_t n, const int64_t *__res
     __shared__ int smin[4], smax[4];
     const int64_t T = ceil_div(n, (int64_t)kWfTR);
     const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+    int sb = 0, sf = 0, sw = 0;  // this block's span maxima (thread 0): one atomic each at the end
     for (int64_t t = blockIdx.x; t < T; t += gridDim.x) {
         const int64_t r0 = t * kWfTR, r1 = r0 + kWfTR < n ? r0 + kWfTR : n;
         int mn = INT_MAX, mx = -1;
@@ -88,15 +89,21 @@ __global__ __launch_bounds__(256) void k_wf_deps(int64_t n, const int64_t *__res
                 hi = b > hi ? b : hi;
             }
             deps[t] = make_int2(lo, hi);
-            atomicMax(&spans[0], (int)t - lo);
-            atomicMax(&spans[1], hi - (int)t);
-            atomicMax(&spans[2], hi - lo + 1);
+            sb = (int)t - lo > sb ? (int)t - lo : sb;
+            sf = hi - (int)t > sf ? hi - (int)t : sf;
+            sw = hi - lo + 1 > sw ? hi - lo + 1 : sw;
         }
         __syncthreads();
+    }
+    if (threadIdx.x == 0) {
+        atomicMax(&spans[0], sb);
+        atomicMax(&spans[1], sf);
+        atomicMax(&spans[2], sw);
     }
 }
 
 typedef unsigned v4u32_t __attribute__((ext_vector_type(4)));
+typedef double d2_t __attribute__((ext_vector_type(2)));
 
 // swap a double with the neighbouring lane (l ^ 1) by DPP (quad_perm 1,0,3,2)
 __device__ __forceinline__ double dpp_swap1(double x)
@@ -115,24 +122,25 @@ __device__ __forceinline__ double dpp_swap1(double x)
 // Vout may alias (V_{j+1} over V_{j-1}: each strip is read, then written, by
 // one wave); Vg == Vout when P2 != nullptr.  part: S1 slabs at [0, G), S2 at
 // [G, 2G), G at [2G, 3G) (256 doubles each, one per block).
-template <int NC, int CAP, int K, int NL, int NU, bool C16>
+template <int NC, int CAP, int K, int NL, int NU, int DU, bool C16>
 __global__ __launch_bounds__(64 * (NC + NL + NU)) void k_wf16(
     int64_t n, const int64_t *__restrict__ rp, const int32_t *__restrict__ col, const int16_t *__restrict__ col16,
     const double *__restrict__ val, const uint64_t *__restrict__ pairs, const double *Yj, const double *Vprev,
     const double *__restrict__ Vj, double *Vout, const double *__restrict__ binv, const double *__restrict__ P1,
     const double *__restrict__ P2, const double *Vg, double *Yo, const int2 *__restrict__ deps, int *flags, int epoch,
-    int64_t hback, double *__restrict__ part, int *__restrict__ err)
+    int64_t hback, int lead, double *__restrict__ part, int *__restrict__ err, int dbg)
 {
     using CT = typename std::conditional<C16, int16_t, int32_t>::type;
     using C = FwCfg<NC, CAP, true, true, CT>;
     constexpr int TR = C::TR;
     static_assert(TR == kWfTR, "tile rows");
+    constexpr int GA = kWfAux, SA = kWfAux;  // gathers / V stores: sc1
     static_assert(NC > 3 && NC <= kPairPad, "strips per tile");
     __shared__ typename C::Stage st[K];
     __shared__ double scr[NC][256];     // per consumer: the parked Y tile (swizzled), then its slab
-    __shared__ double ops[3][256];      // beta^-1, -P1, -P2 in MFMA B-operand (permuted) order
-    __shared__ double uscr[NU][512];    // per updater: V_j transpose scratch, then its two slabs
+    __shared__ double ust[NU][DU + 1][3][256];  // per updater: strip slots (Y_j, V_{j-1}, V_j rows)
     __shared__ int ready[K], done[K], cons_in, upd_in;
+    __shared__ int p1pub;  // pass-1 tiles this block's loaders have published
     const int lane = threadIdx.x & 63, w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
     const bool has_p2 = P2 != nullptr, has_prev = P1 != nullptr;
     if (threadIdx.x < K) {
@@ -141,16 +149,9 @@ __global__ __launch_bounds__(64 * (NC + NL + NU)) void k_wf16(
     }
     if (threadIdx.x == 0) {
         cons_in = 0;
+        p1pub = 0;
         upd_in = 0;
     }
-    if (has_p2)
-        for (int e = threadIdx.x; e < 256; e += blockDim.x) {
-            const int kc = e >> 6, l = e & 63;
-            const int idx = (4 * (l >> 4) + kc) * 16 + (l & 15);
-            ops[0][e] = binv[idx];
-            ops[1][e] = has_prev ? -P1[idx] : 0.0;
-            ops[2][e] = -P2[idx];
-        }
     __syncthreads();  // the only block barrier
     const int64_t T = ceil_div(n, (int64_t)TR);
     const int64_t G = gridDim.x, bid = blockIdx.x;
@@ -169,7 +170,8 @@ __global__ __launch_bounds__(64 * (NC + NL + NU)) void k_wf16(
         pbeg = x == 0 ? 0 : (begin - hback > 0 ? begin - hback : 0);
         pend = x == 7 ? T : (end - hback > 0 ? end - hback : 0);
     }
-    const int64_t nt = (end - begin - kb + KB - 1) / KB > 0 ? (end - begin - kb + KB - 1) / KB : 0;
+    int64_t nt = (end - begin - kb + KB - 1) / KB > 0 ? (end - begin - kb + KB - 1) / KB : 0;
+    if (dbg & 4) nt = 0;  // timing diagnostics (LZ_WF_DBG): no pass-1 tiles
     auto tile_of = [&](int64_t i) { return begin + kb + i * KB; };
     if (w < NL) {
         // ------------------------------------------------------------ loaders
@@ -205,7 +207,7 @@ __global__ __launch_bounds__(64 * (NC + NL + NU)) void k_wf16(
                 ws_dma(pr, st[s].pr, C::PR_PIECES, lane);
             }
             asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-            if (has_p2) {
+            if (has_p2 && !(dbg & 1)) {
                 // every pass-2 tile this tile reads (and its own: its Y rows
                 // are overwritten below) must have published this epoch
                 const int2 d = deps[t];
@@ -223,73 +225,151 @@ __global__ __launch_bounds__(64 * (NC + NL + NU)) void k_wf16(
                 }
                 if (spin >= kWfSpin) { *err = 5; break; }
             }
-            if (lane == 0) ws_lds_write(ws_lds_addr(&ready[s]), (int)i);
+            if (lane == 0) {
+                ws_lds_write(ws_lds_addr(&ready[s]), (int)i);
+                asm volatile("ds_add_u32 %0, %1" ::"v"(ws_lds_addr(&p1pub)), "v"(1) : "memory");
+            }
         }
         return;
     }
     if (w < NL + NU) {
         // ----------------------------------------------------------- updaters
+        // Each updater streams its tiles' 16-row strips through DU + 1 LDS
+        // slots (LDS-DMA: DU strips in flight without holding registers).  A
+        // slot holds the strip's Y_j, V_{j-1} and V_j rows, 16-B pieces
+        // XOR-swizzled (piece p of row r at p ^ ((r >> 1) & 7)), so both the
+        // MFMA A-operand reads (row l & 15, pieces 2 (l >> 4) + hh) and the
+        // accumulator-layout reads of V_j (row 4r + (l >> 4), column l & 15)
+        // are free of bank conflicts.  The slot reads are inline asm: after an
+        // LDS-DMA the compiler would put vmcnt(0) before any LDS access.
         const int uw = w - NL;
         d4_t gacc = {0.0, 0.0, 0.0, 0.0}, sacc = {0.0, 0.0, 0.0, 0.0};
-        double *U = uscr[uw];
-        if (has_p2) {
-            __builtin_amdgcn_s_setprio(1);
+        if (has_p2 && !(dbg & 2)) {
+            if (dbg & 8) __builtin_amdgcn_s_setprio(0);
+            else if (dbg & 64) __builtin_amdgcn_s_setprio(3);
+            else __builtin_amdgcn_s_setprio(2);
+            const int c = lane & 15, g = lane >> 4;
+            // B operands (permuted contraction order): beta^-1, -P1, -P2
+            double bq[3][4];
+#pragma unroll
+            for (int kc = 0; kc < 4; ++kc) {
+                const int idx = (4 * g + kc) * 16 + c;
+                bq[0][kc] = binv[idx];
+                bq[1][kc] = has_prev ? -P1[idx] : 0.0;
+                bq[2][kc] = -P2[idx];
+            }
             const int64_t ut0 = pbeg + kb + uw * KB, ustep = (int64_t)NU * KB;
             const int64_t ntl = ut0 < pend ? (pend - ut0 + ustep - 1) / ustep : 0;
             const int64_t ns = ntl * NC;  // strips of this wave's tiles, in order
             const int bytes = (int)(n * 128);
-            const auto Yr = __builtin_amdgcn_make_buffer_rsrc(const_cast<double *>(Yj), (short)0, bytes, 0x00020000);
-            const auto Pr = __builtin_amdgcn_make_buffer_rsrc(const_cast<double *>(has_prev ? Vprev : Vj), (short)0,
-                                                              has_prev ? bytes : 0, 0x00020000);
-            const auto Jr = __builtin_amdgcn_make_buffer_rsrc(const_cast<double *>(Vj), (short)0, bytes, 0x00020000);
+            const __amdgpu_buffer_rsrc_t rs[3] = {
+                __builtin_amdgcn_make_buffer_rsrc(const_cast<double *>(Yj), (short)0, bytes, 0x00020000),
+                __builtin_amdgcn_make_buffer_rsrc(const_cast<double *>(has_prev ? Vprev : Vj), (short)0,
+                                                  has_prev ? bytes : 0, 0x00020000),
+                __builtin_amdgcn_make_buffer_rsrc(const_cast<double *>(Vj), (short)0, bytes, 0x00020000)};
             const auto Or = __builtin_amdgcn_make_buffer_rsrc(Vout, (short)0, bytes, 0x00020000);
             auto strip_r0 = [&](int64_t s) { return (ut0 + (s / NC) * ustep) * TR + 16 * (s % NC); };
-            struct Ld {
-                double y[4], p[4], j[4];
-            };
-            // A-operand rows (permuted contraction order, as k_fused_pp16):
-            // lane l holds row l & 15, doubles 4 (l >> 4) .. +3 -- two 16-B
-            // loads per matrix.  Six loads per strip, always issued (out of
-            // range past the stream or the rows), so the counted waits below hold.
-            auto fetch = [&](int64_t s, Ld &L) {
-                const uint32_t base =
-                    s < ns ? (uint32_t)(strip_r0(s) * 128) + (uint32_t)((lane & 15) * 128 + (lane >> 4) * 32)
-                           : 0x80000000u;
+            // this lane's DMA pieces: LDS piece q = 64 k + lane holds row q >> 3,
+            // global piece (q & 7) ^ swizzle
+            uint32_t goff[2];
 #pragma unroll
-                for (int hh = 0; hh < 2; ++hh) {
-                    const auto a = __builtin_amdgcn_raw_buffer_load_b128(Yr, base + 16 * hh, 0, 0);
-                    const auto b = __builtin_amdgcn_raw_buffer_load_b128(Pr, base + 16 * hh, 0, 0);
-                    const auto c = __builtin_amdgcn_raw_buffer_load_b128(Jr, base + 16 * hh, 0, 0);
-                    __builtin_memcpy(&L.y[2 * hh], &a, 16);
-                    __builtin_memcpy(&L.p[2 * hh], &b, 16);
-                    __builtin_memcpy(&L.j[2 * hh], &c, 16);
-                }
+            for (int k = 0; k < 2; ++k) {
+                const int q = 64 * k + lane, row = q >> 3;
+                goff[k] = (uint32_t)(row * 128 + 16 * ((q & 7) ^ ((row >> 1) & 7)));
+            }
+            // six DMA instructions per strip, always issued (out of range past
+            // the stream), so the counted waits below hold
+            // pace: the strips of this wave's tile m (its m-th in the block's
+            // tile order) are fetched once the block's loaders have published
+            // pass-1 tile m - lead, so V_{j+1} rows are gathered soon after
+            // they are written (in L2 / the MALL), not a region later.  lead
+            // exceeds the tiles a pass-1 tile reaches ahead, so the pass-1
+            // tiles the wait is for never wait on this wave (no cycle).
+            int64_t paced = -1;  // last tile cleared
+            auto pace = [&](int64_t s) {
+                const int64_t m = uw + (s / NC) * NU;
+                if (s >= ns || s / NC <= paced) return;
+                paced = s / NC;
+                const uint32_t pa = ws_lds_addr(&p1pub);
+                long spin = 0;
+                while (ws_lds_read(pa) < (int)(m - lead) && ++spin < kWsSpin) __builtin_amdgcn_s_sleep(2);
+                if (spin >= kWsSpin) *err = 6;
             };
-            const int c = lane & 15, g = lane >> 4;
+            auto dma = [&](int64_t s) {
+                const int slot = (int)(s % (DU + 1));
+                const bool live = s < ns;
+                if (!(dbg & 32)) pace(s);
+                const uint32_t rb = live ? (uint32_t)(strip_r0(s) * 128) : 0u;
+#pragma unroll
+                for (int m = 0; m < 3; ++m)
+#pragma unroll
+                    for (int k = 0; k < 2; ++k)
+                        __builtin_amdgcn_raw_ptr_buffer_load_lds(
+                            rs[m], (ws_lds_t *)((char *)&ust[uw][slot][m][0] + 1024 * k), 16,
+                            live ? rb + goff[k] : 0x80000000u, 0, 0, 0);
+            };
+            // byte offsets of this lane's slot reads (from the slot base)
+            const int ra = c;
+            const uint32_t oa0 = (uint32_t)(ra * 128 + 16 * ((2 * g) ^ ((ra >> 1) & 7)));
+            const uint32_t oa1 = (uint32_t)(ra * 128 + 16 * ((2 * g + 1) ^ ((ra >> 1) & 7)));
+            uint32_t oc[4];
+#pragma unroll
+            for (int r = 0; r < 4; ++r) {
+                const int row = 4 * r + g;
+                oc[r] = (uint32_t)(2 * 2048 + row * 128 + 16 * ((c >> 1) ^ ((row >> 1) & 7)) + 8 * (c & 1));
+            }
             const bool ev = (c & 1) == 0;
-            // strip s: compute on cur, prefetch strip s + 2 into nxt (the set
-            // strip s - 1 used); publish the tile whose last strip is s - 3
-            auto body = [&](int64_t s, Ld &cur, Ld &nxt) {
-                fetch(s + 2, nxt);
-                if (s >= ns) return;
+#pragma unroll
+            for (int s = 0; s < DU; ++s) dma(s);
+            for (int64_t s = 0; s < ns; ++s) {
+                dma(s + DU);
+                // strip s landed: DU younger strips' six DMAs each, and from the
+                // steady state on also DU strips' two stores, were issued after it
+                if (s < DU) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(6 * DU) : "memory");
+                else asm volatile("s_waitcnt vmcnt(%0)" ::"n"(8 * DU) : "memory");
+                if (s % NC == DU && s >= NC && lane == 0)
+                    // tile s / NC - 1 ended with strip s - DU - 1, whose stores
+                    // are older than strip s's DMA: drained
+                    __hip_atomic_store(flags + ut0 + (s / NC - 1) * ustep, epoch, __ATOMIC_RELAXED,
+                                       __HIP_MEMORY_SCOPE_AGENT);
+                const uint32_t sb = ws_lds_addr(reinterpret_cast<int *>(&ust[uw][(int)(s % (DU + 1))][0][0]));
+                d2_t y0, y1, p0, p1, j0, j1;
+                double vc0, vc1, vc2, vc3;
+                asm volatile(
+                    "ds_read_b128 %0, %10\n\t"
+                    "ds_read_b128 %1, %11\n\t"
+                    "ds_read_b128 %2, %10 offset:2048\n\t"
+                    "ds_read_b128 %3, %11 offset:2048\n\t"
+                    "ds_read_b128 %4, %10 offset:4096\n\t"
+                    "ds_read_b128 %5, %11 offset:4096\n\t"
+                    "ds_read_b64 %6, %12\n\t"
+                    "ds_read_b64 %7, %13\n\t"
+                    "ds_read_b64 %8, %14\n\t"
+                    "ds_read_b64 %9, %15\n\t"
+                    "s_waitcnt lgkmcnt(0)"
+                    // early-clobber: the reads are issued before the inputs are dead
+                    : "=&v"(y0), "=&v"(y1), "=&v"(p0), "=&v"(p1), "=&v"(j0), "=&v"(j1), "=&v"(vc0), "=&v"(vc1),
+                      "=&v"(vc2), "=&v"(vc3)
+                    : "v"(sb + oa0), "v"(sb + oa1), "v"(sb + oc[0]), "v"(sb + oc[1]), "v"(sb + oc[2]),
+                      "v"(sb + oc[3])
+                    : "memory");
+                const double ya[4] = {y0.x, y0.y, y1.x, y1.y}, pa[4] = {p0.x, p0.y, p1.x, p1.y},
+                             ja[4] = {j0.x, j0.y, j1.x, j1.y}, vjc[4] = {vc0, vc1, vc2, vc3};
                 d4_t acc = {0.0, 0.0, 0.0, 0.0};
+                if (dbg & 16) {  // timing diagnostics: no MFMA work
+                    acc = d4_t{pa[0] + ya[0], pa[1] + ya[1], ja[2] + vjc[2], ja[3] + vjc[3]};
+                } else {
 #pragma unroll
-                for (int kc = 0; kc < 4; ++kc) acc = mfma16(cur.p[kc], ops[1][64 * kc + lane], acc);
+                for (int kc = 0; kc < 4; ++kc) acc = mfma16(pa[kc], bq[1][kc], acc);
 #pragma unroll
-                for (int kc = 0; kc < 4; ++kc) acc = mfma16(cur.y[kc], ops[0][64 * kc + lane], acc);
+                for (int kc = 0; kc < 4; ++kc) acc = mfma16(ya[kc], bq[0][kc], acc);
 #pragma unroll
-                for (int kc = 0; kc < 4; ++kc) acc = mfma16(cur.j[kc], ops[2][64 * kc + lane], acc);
-                // V_j in the accumulator layout (row 4r + g, column c) for S2
-#pragma unroll
-                for (int kc = 0; kc < 4; ++kc) U[fw_sw(c, 4 * g + kc)] = cur.j[kc];
-                wave_lds_sync();
-                double vjc[4];
-#pragma unroll
-                for (int r = 0; r < 4; ++r) vjc[r] = U[fw_sw(4 * r + g, c)];
+                for (int kc = 0; kc < 4; ++kc) acc = mfma16(ja[kc], bq[2][kc], acc);
 #pragma unroll
                 for (int r = 0; r < 4; ++r) gacc = mfma16(acc[r], acc[r], gacc);
 #pragma unroll
                 for (int r = 0; r < 4; ++r) sacc = mfma16(acc[r], vjc[r], sacc);
+                }
                 // V_{j+1}: the lane pairs (c, c ^ 1) swap one value per row pair
                 // so each lane stores 16 contiguous bytes (write-through)
                 const uint32_t r0b = (uint32_t)(strip_r0(s) * 128);
@@ -300,32 +380,16 @@ __global__ __launch_bounds__(64 * (NC + NL + NU)) void k_wf16(
                     const double2 v = ev ? make_double2(a0, y) : make_double2(y, a1);
                     const int row = 4 * (2 * h2 + (ev ? 0 : 1)) + g;
                     const uint32_t off = r0b + (uint32_t)(row * 128 + (ev ? c : c - 1) * 8);
-                    __builtin_amdgcn_raw_buffer_store_b128(*reinterpret_cast<const v4u32_t *>(&v), Or, off, 0, kWfAux);
+                    __builtin_amdgcn_raw_buffer_store_b128(*reinterpret_cast<const v4u32_t *>(&v), Or, off, 0, SA);
                 }
-                if (s % NC == 2 && s >= NC) {
-                    // the last strip of tile s / NC - 1 is s - 3; its two
-                    // stores are followed by at least 22 vector-memory ops
-                    // (three strips' six loads, two strips' two stores), so
-                    // vmcnt(16) has drained them
-                    asm volatile("s_waitcnt vmcnt(16)" ::: "memory");
-                    if (lane == 0)
-                        __hip_atomic_store(flags + ut0 + (s / NC - 1) * ustep, epoch, __ATOMIC_RELAXED,
-                                           __HIP_MEMORY_SCOPE_AGENT);
-                }
-            };
-            Ld R0, R1, R2;
-            fetch(0, R0);
-            fetch(1, R1);
-            for (int64_t s = 0; s < ns; s += 3) {
-                body(s, R0, R2);
-                body(s + 1, R1, R0);
-                body(s + 2, R2, R1);
             }
             asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
             if (ntl > 0 && lane == 0)
                 __hip_atomic_store(flags + ut0 + (ntl - 1) * ustep, epoch, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         }
-        // the NU updater slabs folded by the last updater to finish
+        // the NU updater slabs folded by the last updater to finish (slot 0
+        // of each updater is free now)
+        double *U = &ust[uw][0][0][0];
 #pragma unroll
         for (int r = 0; r < 4; ++r) {
             U[((lane >> 4) + 4 * r) * 16 + (lane & 15)] = gacc[r];
@@ -338,7 +402,7 @@ __global__ __launch_bounds__(64 * (NC + NL + NU)) void k_wf16(
             __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
             for (int e = lane; e < 512; e += 64) {
                 double a = 0.0;
-                for (int u = 0; u < NU; ++u) a += uscr[u][e];
+                for (int u = 0; u < NU; ++u) a += ust[u][0][0][e];
                 // e < 256: G slab (at 2G), else S2 (at G)
                 part[(e < 256 ? 2 * G : G) * 256 + bid * 256 + (e & 255)] = a;
             }
@@ -410,7 +474,7 @@ __global__ __launch_bounds__(64 * (NC + NL + NU)) void k_wf16(
                     const uint32_t off = f + tt < cnt
                                              ? __umul24(C16 ? (unsigned)cc[tt] + cb16 : (unsigned)cc[tt], 128u) + lane_off
                                              : 0x80000000u;
-                    const auto u4 = __builtin_amdgcn_raw_buffer_load_b128(xr, off, 0, kWfAux);
+                    const auto u4 = __builtin_amdgcn_raw_buffer_load_b128(xr, off, 0, GA);
                     __builtin_memcpy(&xs[tt], &u4, 16);
                 }
             };
@@ -437,7 +501,7 @@ __global__ __launch_bounds__(64 * (NC + NL + NU)) void k_wf16(
             }
         } else {  // long run (rare): epilogue first, then gather from global
             if (s0p >= 0) epilogue();
-            ws_gather<const int32_t *, const double *, kWfAux>(col + kA, val + kA, o0, len0, o1, cnt, xr, lane_off,
+            ws_gather<const int32_t *, const double *, GA>(col + kA, val + kA, o0, len0, o1, cnt, xr, lane_off,
                                                                y, 0u);
         }
         // the CSR stage is no longer read by this wave
@@ -461,7 +525,7 @@ __global__ __launch_bounds__(64 * (NC + NL + NU)) void k_wf16(
         for (int r = 0; r < 4; ++r) {
             const int64_t row = s0 + (lane >> 4) + 4 * r;
             const uint32_t off = row < n ? (uint32_t)(row * 128 + (lane & 15) * 8) : 0x80000000u;
-            const auto u = __builtin_amdgcn_raw_buffer_load_b64(xr, off, 0, kWfAux);
+            const auto u = __builtin_amdgcn_raw_buffer_load_b64(xr, off, 0, GA);
             __builtin_memcpy(&v1[r], &u, 8);
         }
         s0p = s0;
@@ -491,11 +555,13 @@ __global__ __launch_bounds__(64 * (NC + NL + NU)) void k_wf16(
     }
 }
 
-int wf_plan16(lz_handle *h, int64_t n, const int64_t *rp, const int32_t *col, WfPlan *pl)
+int wf_plan16(lz_handle *h, int64_t n, int64_t nnz, const int64_t *rp, const int32_t *col, WfPlan *pl)
 {
     pl->ok = false;
-    const char *e = getenv("LZ_PASS_WF");  // "1": the wavefront step (opt-in while it is slower); read per call
-    if (!(e && e[0] == '1') || n < kWfTR || n >= (1 << 24)) return LZ_OK;
+    const char *e = getenv("LZ_PASS_WF");  // "0": the two-pass step (A/B); read per call
+    // rows of about 11 entries or fewer on average: the tile's CSR run fits the
+    // kWfCap-entry stage (longer runs take a slow global-gather path)
+    if ((e && e[0] == '0') || n < kWfTR || n >= (1 << 24) || (double)nnz > 10.2 * (double)n) return LZ_OK;
     const int64_t T = ceil_div(n, (int64_t)kWfTR);
     if ((size_t)T + 64 > h->wf_cap) {
         LZ_HIP_TRY(hipStreamSynchronize(h->stream));
@@ -533,15 +599,27 @@ int wf_step16(lz_handle *h, int64_t n, const int64_t *rp, const int32_t *col, co
     LZ_ARG_CHECK(P2 == nullptr || (Yj && Vj && Vout && binv && Vg == Vout), "wavefront step buffers");
     static_assert(kWfNC <= kPairPad, "row orders must cover the last tile's strips");
     const int grid = (int)std::max<int64_t>(1, std::min<int64_t>(ceil_div(n, (int64_t)kWfTR), h->n_cu));
+    // LZ_WF_DBG (timing diagnostics only; results are wrong): bit 0 skips the
+    // loaders' flag polls, bit 1 the updaters' work, bit 2 the pass-1 tiles;
+    // bit 3 / bit 6 run the updaters at issue priority 0 / 3 (default 2)
+    const char *dg = getenv("LZ_WF_DBG");
+    const int dbg = dg ? atoi(dg) : 0;
+    // the updaters' pace (tiles ahead of the block's pass 1): at least the
+    // tiles a pass-1 tile reaches ahead in the block's order, plus two
+    const int KB = grid < 8 ? grid : grid / 8;
+    const int lmin = (int)((pl.hback + pl.hfwd + KB - 1) / KB) + 2;
+    const char *le = getenv("LZ_WF_LEAD");
+    const int lead = std::max(lmin, le ? atoi(le) : lmin + 3);  // C3: lmin 4; 6-8 measured best
     const int ev = prof_begin(h, PROF_SPMM_PASS);
     auto go = [&](auto kern) {
         hipLaunchKernelGGL(kern, dim3(grid), dim3(64 * (kWfNC + kWfNL + kWfNU)), 0, h->stream, n, rp, col, col16, val,
                            pairs, Yj, Vprev, Vj, Vout, binv, P1, P2, Vg, Yo,
-                           static_cast<const int2 *>(h->wf_deps), h->wf_flags, epoch, (int64_t)pl.hback,
-                           h->partials2, h->err_flag);
+                           static_cast<const int2 *>(h->wf_deps), h->wf_flags, epoch, (int64_t)pl.hback, lead,
+                           h->partials2, h->err_flag, dbg);
     };
-    if (col16) go(k_wf16<kWfNC, kWfCap, kWfK, kWfNL, kWfNU, true>);
-    else go(k_wf16<kWfNC, kWfCap, kWfK, kWfNL, kWfNU, false>);
+    // LDS: 16-bit columns leave room for four strip slots per updater, 32-bit three
+    if (col16) go(k_wf16<kWfNC, kWfCap, kWfK, kWfNL, kWfNU, 3, true>);
+    else go(k_wf16<kWfNC, kWfCap, kWfK, kWfNL, kWfNU, 2, false>);
     prof_end(h, ev);
     LZ_LAUNCH_CHECK();
     *nparts = grid;

@@ -83,6 +83,36 @@ def test_block_b16_col16(lz, orc, handle, torch_cuda, monkeypatch, c16, n, hw):
     assert_close_run(lz, m, 16, got, orc.block_lanczos(A, B, m, lc))
 
 
+@pytest.mark.parametrize("wf", ["0", "1"])
+@pytest.mark.parametrize("n,npr,hw", [(1000, 10.0, 16), (5_003, 10.0, 64), (60_013, 10.0, 4096),
+                                      (200_003, 8.0, 2048), (777_777, 10.0, 8192), (300_007, 10.0, 40_000)])
+def test_block_b16_wavefront(lz, orc, handle, torch_cuda, monkeypatch, wf, n, npr, hw):
+    """The wavefront step (lz_wf.hip, LZ_PASS_WF default on) and the two-pass
+    step against the oracle: fewer pass-1 tiles than XCD regions (n = 1000: 6
+    tiles), a partial last tile, bands of 1-2 tiles up to ~85 (the pass-2
+    wavefront leads by the widest), and half width 40,000 (32-bit columns and
+    a column span past the wavefront's limit: the two-pass step runs)."""
+    monkeypatch.setenv("LZ_PASS_WF", wf)
+    A = lz.gen_banded(n, npr, hw, seed=n % 97)
+    B = lz.uniform_B(A.n, 16, seed=5)
+    m, lc = 9, n // 3
+    got = gpu_block(lz, handle, torch_cuda, A, B, m, lc)
+    assert handle.device_error() == 0
+    assert_close_run(lz, m, 16, got, orc.block_lanczos(A, B, m, lc))
+
+
+def test_block_b16_wavefront_bitwise(lz, handle, torch_cuda, monkeypatch):
+    """The wavefront step is deterministic (static tile assignment, fixed-order
+    slabs): the same solve twice gives the same bits."""
+    monkeypatch.setenv("LZ_PASS_WF", "1")
+    A = lz.gen_banded(400_009, 10.0, 4096, seed=3)
+    B = lz.uniform_B(A.n, 16, seed=3)
+    r1 = gpu_block(lz, handle, torch_cuda, A, B, 12, 84)
+    r2 = gpu_block(lz, handle, torch_cuda, A, B, 12, 84)
+    for x, y in zip(r1, r2):
+        assert np.array_equal(x, y)
+
+
 def test_block_b16_tail_rows(lz, orc, handle, torch_cuda):
     """n not a multiple of the 16-row tiles, lc in the last partial tile."""
     A = lz.gen_banded(1000 * 16 + 11, 7.0, 64, seed=2)
@@ -445,10 +475,13 @@ def test_block_b16_long_runs(lz, orc, handle, torch_cuda):
     assert handle.device_error() == 0
 
 
-def test_prof_class_mask(lz, handle, torch_cuda):
+@pytest.mark.parametrize("wf", ["0", "1"])
+def test_prof_class_mask(lz, handle, torch_cuda, monkeypatch, wf):
     """lz_prof_enable_mask records only the selected kernel classes (the bench's
     timed region records pass 1 alone); lz_prof_enable(1) records all of them;
-    results do not depend on what is recorded."""
+    results do not depend on what is recorded.  The wavefront step (wf = 1) has
+    m launches in the pass-1 class and no update pass."""
+    monkeypatch.setenv("LZ_PASS_WF", wf)
     torch = torch_cuda
     A = lz.gen_banded(20011, 10.0, 1024, seed=5)
     B = lz.uniform_B(A.n, 16, seed=6)
@@ -464,7 +497,7 @@ def test_prof_class_mask(lz, handle, torch_cuda):
         ms2, c2 = handle.prof_read(handle.PROF_UPDATE_PASS)
         handle.prof_enable(False)
         assert c1 == m and ms1 > 0.0
-        assert (c2 == 0) if classes else (c2 == m)
+        assert (c2 == 0) if (classes or wf == "1") else (c2 == m)
         outs.append((q.cpu().numpy(), al.cpu().numpy(), be.cpu().numpy()))
     assert all(np.array_equal(x, y) for x, y in zip(outs[0], outs[1]))
     assert handle.device_error() == 0
