@@ -88,9 +88,13 @@ PASS2_MFMA_FLOP_PER_ROW = 8 * 2048 // 16
 
 
 def wf_kernel(n, hw):
-    """(full name, PMC short name) of the wavefront-step kernel (lz_wf.hip wf_step16)."""
+    """(full name, PMC short name) of the wavefront-step kernel (lz_wf.hip wf_step16):
+    <consumers, stage entries, stages, loaders, updaters, strip slots - 1, 16-bit columns>."""
     c16 = col_bytes(n, hw) == 2
-    return f"k_wf16<12,2112,3,2,2,{3 if c16 else 2},{'true' if c16 else 'false'}>", "k_wf16"
+    nc = os.environ.get("LZ_WF_SHAPE", "10")
+    nc = int(nc) if nc in ("11", "12") else 10
+    du = {10: 2 if c16 else 1, 11: 2, 12: 3 if c16 else 2}[nc]
+    return f"k_wf16<{nc},{nc * 16 * 11},3,2,{14 - nc},{du},{'true' if c16 else 'false'}>", "k_wf16"
 
 
 # MFMA work of the wavefront step per row: updaters 12 (V_{j+1}) + 4 (G) + 4 (S2),

@@ -183,7 +183,7 @@ static int block_lanczos_wf16(lz_handle *h, int64_t n, int64_t nnz, const int64_
     int P = 0;
     LZ_TRY(gram_partials<double>(h, n, 16, B, B, 16, &P));
     LZ_TRY(sqrtm_pair<double>(h, 16, nullptr, P, beta, binv[0], nullptr));
-    LZ_TRY(wf_reset16(h, n));
+    LZ_TRY(wf_reset16(h, n, wp));
     // Y_0 = A B, S1_0 = B^T Y_0
     LZ_TRY(wf_step16(h, n, rp, col, pl.col16, val, pl.pairs, wp, nullptr, nullptr, nullptr, nullptr, nullptr,
                      nullptr, nullptr, B, Q0, 0, &P));

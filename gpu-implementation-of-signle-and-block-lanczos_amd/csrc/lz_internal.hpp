@@ -82,11 +82,12 @@ int mm16(lz_handle *h, const double *A, const double *B, double *C);
 struct WfPlan {
     bool ok = false;       // the wavefront step applies (n < 2^24, narrow column spans)
     int hback = 0, hfwd = 0;  // max tiles a tile's columns reach below / above it
+    int nc = 12, tr = 192;    // consumers per block, rows per tile (16 nc)
 };
 // once per solve: per-tile dependency ranges; synchronises the stream once
 int wf_plan16(lz_handle *h, int64_t n, int64_t nnz, const int64_t *rp, const int32_t *col, WfPlan *pl);
 // zero the pass-2 flags (start of a solve; epochs 1, 2, ... follow)
-int wf_reset16(lz_handle *h, int64_t n);
+int wf_reset16(lz_handle *h, int64_t n, const WfPlan &pl);
 // P2 == nullptr: pass 1 only (Y = A Vg, S1 slabs).  Otherwise V_{j+1} = Yj binv
 // - Vprev P1 - Vj P2 into Vout (== Vg; P1 == nullptr: no Vprev term), Y_{j+1}
 // = A Vout into Yo (may be Yj).  Slabs at h->partials2: S1 [0, G), S2 [G, 2G),

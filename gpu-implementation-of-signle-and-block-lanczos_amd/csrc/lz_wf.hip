@@ -41,8 +41,12 @@
 
 namespace lz {
 
-constexpr int kWfNC = 12, kWfCap = 2112, kWfK = 3, kWfNL = 2, kWfNU = 2;
-constexpr int kWfTR = 16 * kWfNC;   // rows per tile (pass 1 and pass 2)
+// block shapes (LZ_WF_SHAPE "NC" for 2 loaders + NC consumers + 14 - NC
+// updaters): 10 (default: one updater per SIMD), 11, 12; tiles of 16 NC rows.
+// An updater wave is bound by its SIMD's MFMA pipe: at C3 2 + 13 + 1 took
+// 3.1 ms, 2 + 12 + 2 1.93, 2 + 11 + 3 1.87, 2 + 10 + 4 1.86 (scripts/ab_c3.py).
+constexpr int kWfK = 3, kWfNL = 2;
+constexpr int kWfCapPerRow = 11;  // stage entries per row (C3: 10 +- 2.2 nnz per row)
 constexpr int kWfMaxSpan = 256;     // pass-2 tiles one pass-1 tile may read (flag polls per tile)
 constexpr int kWfAux = 16;          // buffer-instruction cache policy: sc1
 constexpr long kWfSpin = 1L << 21;  // flag polls per tile before the loader gives up (about 2 s)
@@ -50,16 +54,16 @@ constexpr long kWfSpin = 1L << 21;  // flag polls per tile before the loader giv
 // Per pass-1 tile t: [lo, hi], the tiles holding its columns, t itself
 // included (pass 1 of tile t overwrites Y rows pass 2 of tile t reads).
 // spans: max(t - lo), max(hi - t), max(hi - lo + 1).
-__global__ __launch_bounds__(256) void k_wf_deps(int64_t n, const int64_t *__restrict__ rp,
+__global__ __launch_bounds__(256) void k_wf_deps(int64_t n, int TR, const int64_t *__restrict__ rp,
                                                  const int32_t *__restrict__ col, int2 *__restrict__ deps,
                                                  int *__restrict__ spans)
 {
     __shared__ int smin[4], smax[4];
-    const int64_t T = ceil_div(n, (int64_t)kWfTR);
+    const int64_t T = ceil_div(n, (int64_t)TR);
     const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
     int sb = 0, sf = 0, sw = 0;  // this block's span maxima (thread 0): one atomic each at the end
     for (int64_t t = blockIdx.x; t < T; t += gridDim.x) {
-        const int64_t r0 = t * kWfTR, r1 = r0 + kWfTR < n ? r0 + kWfTR : n;
+        const int64_t r0 = t * TR, r1 = r0 + TR < n ? r0 + TR : n;
         int mn = INT_MAX, mx = -1;
         for (int64_t k = rp[r0] + threadIdx.x, e = rp[r1]; k < e; k += 256) {
             const int c = col[k];
@@ -84,7 +88,7 @@ __global__ __launch_bounds__(256) void k_wf_deps(int64_t n, const int64_t *__res
             }
             int lo = (int)t, hi = (int)t;
             if (mx >= 0) {
-                const int a = (int)(mn / kWfTR), b = (int)(mx / kWfTR);
+                const int a = (int)(mn / TR), b = (int)(mx / TR);
                 lo = a < lo ? a : lo;
                 hi = b > hi ? b : hi;
             }
@@ -133,7 +137,6 @@ __global__ __launch_bounds__(64 * (NC + NL + NU)) void k_wf16(
     using CT = typename std::conditional<C16, int16_t, int32_t>::type;
     using C = FwCfg<NC, CAP, true, true, CT>;
     constexpr int TR = C::TR;
-    static_assert(TR == kWfTR, "tile rows");
     constexpr int GA = kWfAux, SA = kWfAux;  // gathers / V stores: sc1
     static_assert(NC > 3 && NC <= kPairPad, "strips per tile");
     __shared__ typename C::Stage st[K];
@@ -560,9 +563,13 @@ int wf_plan16(lz_handle *h, int64_t n, int64_t nnz, const int64_t *rp, const int
     pl->ok = false;
     const char *e = getenv("LZ_PASS_WF");  // "0": the two-pass step (A/B); read per call
     // rows of about 11 entries or fewer on average: the tile's CSR run fits the
-    // kWfCap-entry stage (longer runs take a slow global-gather path)
-    if ((e && e[0] == '0') || n < kWfTR || n >= (1 << 24) || (double)nnz > 10.2 * (double)n) return LZ_OK;
-    const int64_t T = ceil_div(n, (int64_t)kWfTR);
+    // kWfCapPerRow-entry-per-row stage (longer runs take a slow global-gather path)
+    const char *sh = getenv("LZ_WF_SHAPE");  // consumers per block (A/B); read per call
+    const int want = sh ? atoi(sh) : 10;
+    pl->nc = (want == 11 || want == 12) ? want : 10;
+    pl->tr = 16 * pl->nc;
+    if ((e && e[0] == '0') || n < pl->tr || n >= (1 << 24) || (double)nnz > 10.2 * (double)n) return LZ_OK;
+    const int64_t T = ceil_div(n, (int64_t)pl->tr);
     if ((size_t)T + 64 > h->wf_cap) {
         LZ_HIP_TRY(hipStreamSynchronize(h->stream));
         (void)hipFree(h->wf_deps);
@@ -577,7 +584,7 @@ int wf_plan16(lz_handle *h, int64_t n, int64_t nnz, const int64_t *rp, const int
     int *spans = h->err_flag + 12;  // err_flag[0]: device error word; [8], [9]: other plans
     LZ_HIP_TRY(hipMemsetAsync(spans, 0, 3 * sizeof(int), h->stream));
     const int grid = (int)std::max<int64_t>(1, std::min<int64_t>(T, (int64_t)h->n_cu * 8));
-    hipLaunchKernelGGL(k_wf_deps, dim3(grid), dim3(256), 0, h->stream, n, rp, col,
+    hipLaunchKernelGGL(k_wf_deps, dim3(grid), dim3(256), 0, h->stream, n, pl->tr, rp, col,
                        static_cast<int2 *>(h->wf_deps), spans);
     LZ_LAUNCH_CHECK();
     int sp[3] = {0, 0, 0};
@@ -597,8 +604,8 @@ int wf_step16(lz_handle *h, int64_t n, const int64_t *rp, const int32_t *col, co
     LZ_ARG_CHECK(pl.ok && n < (1 << 24), "wavefront step: wf_plan16 first");
     LZ_ARG_CHECK(pairs != nullptr, "strip row orders (strip_pairs) missing");
     LZ_ARG_CHECK(P2 == nullptr || (Yj && Vj && Vout && binv && Vg == Vout), "wavefront step buffers");
-    static_assert(kWfNC <= kPairPad, "row orders must cover the last tile's strips");
-    const int grid = (int)std::max<int64_t>(1, std::min<int64_t>(ceil_div(n, (int64_t)kWfTR), h->n_cu));
+    static_assert(12 <= kPairPad, "row orders must cover the last tile's strips");
+    const int grid = (int)std::max<int64_t>(1, std::min<int64_t>(ceil_div(n, (int64_t)pl.tr), h->n_cu));
     // LZ_WF_DBG (timing diagnostics only; results are wrong): bit 0 skips the
     // loaders' flag polls, bit 1 the updaters' work, bit 2 the pass-1 tiles;
     // bit 3 / bit 6 run the updaters at issue priority 0 / 3 (default 2)
@@ -609,26 +616,31 @@ int wf_step16(lz_handle *h, int64_t n, const int64_t *rp, const int32_t *col, co
     const int KB = grid < 8 ? grid : grid / 8;
     const int lmin = (int)((pl.hback + pl.hfwd + KB - 1) / KB) + 2;
     const char *le = getenv("LZ_WF_LEAD");
-    const int lead = std::max(lmin, le ? atoi(le) : lmin + 3);  // C3: lmin 4; 6-8 measured best
+    const int lead = std::max(lmin, le ? atoi(le) : lmin + 4);  // C3: lmin 4; 7-9 measured best
     const int ev = prof_begin(h, PROF_SPMM_PASS);
     auto go = [&](auto kern) {
-        hipLaunchKernelGGL(kern, dim3(grid), dim3(64 * (kWfNC + kWfNL + kWfNU)), 0, h->stream, n, rp, col, col16, val,
+        hipLaunchKernelGGL(kern, dim3(grid), dim3(1024), 0, h->stream, n, rp, col, col16, val,
                            pairs, Yj, Vprev, Vj, Vout, binv, P1, P2, Vg, Yo,
                            static_cast<const int2 *>(h->wf_deps), h->wf_flags, epoch, (int64_t)pl.hback, lead,
                            h->partials2, h->err_flag, dbg);
     };
-    // LDS: 16-bit columns leave room for four strip slots per updater, 32-bit three
-    if (col16) go(k_wf16<kWfNC, kWfCap, kWfK, kWfNL, kWfNU, 3, true>);
-    else go(k_wf16<kWfNC, kWfCap, kWfK, kWfNL, kWfNU, 2, false>);
+    // LDS (<= 160 KB): strip slots per updater DU + 1, fewer with 32-bit columns
+    constexpr int cap12 = 12 * 16 * kWfCapPerRow, cap11 = 11 * 16 * kWfCapPerRow, cap10 = 10 * 16 * kWfCapPerRow;
+    if (pl.nc == 11 && col16) go(k_wf16<11, cap11, kWfK, kWfNL, 3, 2, true>);
+    else if (col16) go(k_wf16<10, cap10, kWfK, kWfNL, 4, 2, true>);
+    else if (pl.nc == 12 && col16) go(k_wf16<12, cap12, kWfK, kWfNL, 2, 3, true>);
+    else if (pl.nc == 12) go(k_wf16<12, cap12, kWfK, kWfNL, 2, 2, false>);
+    else if (pl.nc == 11) go(k_wf16<11, cap11, kWfK, kWfNL, 3, 2, false>);
+    else go(k_wf16<10, cap10, kWfK, kWfNL, 4, 1, false>);
     prof_end(h, ev);
     LZ_LAUNCH_CHECK();
     *nparts = grid;
     return LZ_OK;
 }
 
-int wf_reset16(lz_handle *h, int64_t n)
+int wf_reset16(lz_handle *h, int64_t n, const WfPlan &pl)
 {
-    const int64_t T = ceil_div(n, (int64_t)kWfTR);
+    const int64_t T = ceil_div(n, (int64_t)pl.tr);
     LZ_ARG_CHECK((size_t)T <= h->wf_cap, "wf_plan16 first");
     LZ_HIP_TRY(hipMemsetAsync(h->wf_flags, 0, sizeof(int) * (size_t)T, h->stream));
     return LZ_OK;

@@ -101,6 +101,21 @@ def test_block_b16_wavefront(lz, orc, handle, torch_cuda, monkeypatch, wf, n, np
     assert_close_run(lz, m, 16, got, orc.block_lanczos(A, B, m, lc))
 
 
+@pytest.mark.parametrize("c16", ["0", "1"])
+@pytest.mark.parametrize("shape", ["10", "11", "12"])
+def test_block_b16_wavefront_shapes(lz, orc, handle, torch_cuda, monkeypatch, shape, c16):
+    """Every block shape of the wavefront step (2 loaders + NC consumers + 14 -
+    NC updaters, LZ_WF_SHAPE) with 16- and 32-bit columns."""
+    monkeypatch.setenv("LZ_WF_SHAPE", shape)
+    monkeypatch.setenv("LZ_PASS1_C16", c16)
+    A = lz.gen_banded(90_001, 10.0, 4096, seed=17)
+    B = lz.uniform_B(A.n, 16, seed=2)
+    m, lc = 8, 70_000
+    got = gpu_block(lz, handle, torch_cuda, A, B, m, lc)
+    assert handle.device_error() == 0
+    assert_close_run(lz, m, 16, got, orc.block_lanczos(A, B, m, lc))
+
+
 def test_block_b16_wavefront_bitwise(lz, handle, torch_cuda, monkeypatch):
     """The wavefront step is deterministic (static tile assignment, fixed-order
     slabs): the same solve twice gives the same bits."""
