@@ -193,11 +193,18 @@ static int block_lanczos_wf16(lz_handle *h, int64_t n, int64_t nnz, const int64_
         double *Vn = j == 0 ? W : j == 1 ? Q1 : const_cast<double *>(Vm1);
         LZ_TRY(wf_step16(h, n, rp, col, pl.col16, val, pl.pairs, wp, Q0, Vm1, V0, Vn, binv[j & 1], j ? P1 : nullptr,
                          P2, Vn, Q0, j + 1, &P));
-        // beta_{j+1}, its inverse and P1 = beta_j^-1 beta_{j+1} from the G slabs
+        // beta_{j+1}, its inverse and P1 = beta_j^-1 beta_{j+1} from the G slabs,
+        // then (same launch) alpha_{j+1}, P2 and the row probe from the S1, S2 slabs
+        WfAlpha wa;
+        wa.part = h->partials2;
+        wa.P = P;
+        wa.alpha = alpha + (j + 1) * bb;
+        wa.P2 = P2;
+        wa.V = Vn;
+        wa.lc = (lc >= 0 && lc < n) ? lc : -1;
+        wa.qrow = q + (j + 1) * 16;
         LZ_TRY(sqrtm_pair<double>(h, 16, nullptr, P, beta + (j + 1) * bb, binv[(j + 1) & 1], nullptr,
-                                  h->partials2 + 2 * (int64_t)P * 256, binv[j & 1], P1));
-        LZ_TRY(alpha_wf16(h, h->partials2, P, binv[(j + 1) & 1], P1, alpha + (j + 1) * bb, P2, Vn, lc, n,
-                          q + (j + 1) * 16));
+                                  h->partials2 + 2 * (int64_t)P * 256, binv[j & 1], P1, &wa));
         Vm1 = V0;
         V0 = Vn;
     }
@@ -215,12 +222,16 @@ static int block_lanczos_fused16(lz_handle *h, int64_t n, int64_t nnz, const int
     QfreeBufs qb(h);
     int P = 0;
     Pass1Plan pl;
-    LZ_TRY(pass1_plan(h, n, nnz, rp, col, n, 0, &pl));
-    if (!pl.win) {
+    {
         WfPlan wp;
-        LZ_TRY(wf_plan16(h, n, nnz, rp, col, &wp));
-        if (wp.ok) return block_lanczos_wf16(h, n, nnz, rp, col, val, m, lc, B, q, alpha, beta, Q0, Q1, W, pl, wp);
+        LZ_TRY(wf_plan16(h, n, nnz, rp, col, &wp));  // n < 2^24 only
+        if (wp.ok) {
+            LZ_TRY(strip_pairs(h, n, rp, &pl.pairs));
+            pl.col16 = wp.col16;
+            return block_lanczos_wf16(h, n, nnz, rp, col, val, m, lc, B, q, alpha, beta, Q0, Q1, W, pl, wp);
+        }
     }
+    LZ_TRY(pass1_plan(h, n, nnz, rp, col, n, 0, &pl));
     LZ_TRY(gram_partials<double>(h, n, 16, B, B, 16, &P));
     LZ_TRY(sqrtm_pair<double>(h, 16, nullptr, P, beta, qb.binv[0], nullptr));
     const double *in = B, *prev = nullptr;

@@ -644,7 +644,7 @@ __global__ __launch_bounds__(kRedThreads) void k_sqrtm_b(const T *__restrict__ G
                                                          const double *__restrict__ part, int P,
                                                          T *__restrict__ beta, T *__restrict__ binv,
                                                          T *__restrict__ eig, const T *__restrict__ L,
-                                                         T *__restrict__ LB)
+                                                         T *__restrict__ LB, WfAlpha wa)
 {
 #pragma clang fp contract(off)
     static_assert(B == 8 || B == 16 || B == 32, "B in {8, 16, 32}");
@@ -655,12 +655,21 @@ __global__ __launch_bounds__(kRedThreads) void k_sqrtm_b(const T *__restrict__ G
     __shared__ double scratch[kRedThreads];
     __shared__ double Abuf[2][B * LD], Ubuf[2][B * LD];
     __shared__ double cc[B], ss[B];
+    // the wavefront step's alpha kernel folded in (B = 16, wa.part != null):
+    // its slabs reduced by the whole block up front, the products at the end
+    constexpr int WB = B == 16 ? BB : 1;
+    __shared__ double ws1[WB], ws2[WB], wbi[WB], wp1[WB];
+    const bool wfa = B == 16 && wa.part != nullptr;
     const int tid = threadIdx.x;
     if (P > 0) {
         reduce_slabs(part, P, BB, g, scratch);
     } else {
         for (int e = tid; e < BB; e += kRedThreads) g[e] = (double)Gin[e];
         __syncthreads();
+    }
+    if (wfa) {
+        reduce_slabs(wa.part, wa.P, BB, ws1, scratch);
+        if (L) reduce_slabs(wa.part + (int64_t)wa.P * BB, wa.P, BB, ws2, scratch);
     }
     if (tid >= 64) return;  // one wave from here on
     const int j = tid % B, r0 = tid / B;  // column, first row of this lane
@@ -872,6 +881,8 @@ __global__ __launch_bounds__(kRedThreads) void k_sqrtm_b(const T *__restrict__ G
         if (beta) beta[i * B + j] = (T)s1;
         if (binv) binv[i * B + j] = (T)s2;
         if (L) g[i * B + j] = s1;  // g (the Gram) is dead: park beta for LB
+        if constexpr (B == 16)
+            if (wfa) wbi[i * B + j] = (double)(T)s2;
     }
     if (L) {  // LB = L * beta (the Q-free iteration's P1 = beta_{j-1}^-1 beta_j)
         wave_lds_sync();
@@ -882,6 +893,62 @@ __global__ __launch_bounds__(kRedThreads) void k_sqrtm_b(const T *__restrict__ G
 #pragma unroll 4
             for (int kk = 0; kk < B; ++kk) s = fma((double)L[i * B + kk], g[kk * B + j], s);
             LB[i * B + j] = (T)s;
+            if constexpr (B == 16)
+                if (wfa) wp1[i * B + j] = (double)(T)s;
+        }
+    }
+    if constexpr (B == 16) {
+        if (wfa) {  // k_alpha_wf16's products, same order (one wave)
+            wave_lds_sync();
+            double x[NE];
+#pragma unroll
+            for (int k = 0; k < NE; ++k) {  // X = S1 binv - S2 P1
+                const int i = r0 + RS * k;
+                double s = 0.0;
+                for (int kk = 0; kk < B; ++kk) s = fma(ws1[i * B + kk], wbi[kk * B + j], s);
+                if (L)
+                    for (int kk = 0; kk < B; ++kk) s = fma(-ws2[i * B + kk], wp1[kk * B + j], s);
+                x[k] = s;
+            }
+            wave_lds_sync();
+#pragma unroll
+            for (int k = 0; k < NE; ++k) ws2[(r0 + RS * k) * B + j] = x[k];
+            wave_lds_sync();
+#pragma unroll
+            for (int k = 0; k < NE; ++k) {  // Z = binv X
+                const int i = r0 + RS * k;
+                double z = 0.0;
+                for (int kk = 0; kk < B; ++kk) z = fma(wbi[i * B + kk], ws2[kk * B + j], z);
+                x[k] = z;
+            }
+#pragma unroll
+            for (int k = 0; k < NE; ++k) ws1[(r0 + RS * k) * B + j] = x[k];
+            wave_lds_sync();
+#pragma unroll
+            for (int k = 0; k < NE; ++k) {  // alpha = sym(Z)
+                const int i = r0 + RS * k;
+                x[k] = 0.5 * (ws1[i * B + j] + ws1[j * B + i]);
+            }
+            wave_lds_sync();
+#pragma unroll
+            for (int k = 0; k < NE; ++k) {
+                const int i = r0 + RS * k;
+                wa.alpha[i * B + j] = x[k];
+                ws2[i * B + j] = x[k];
+            }
+            wave_lds_sync();
+#pragma unroll
+            for (int k = 0; k < NE; ++k) {  // P2 = binv alpha
+                const int i = r0 + RS * k;
+                double s = 0.0;
+                for (int kk = 0; kk < B; ++kk) s = fma(wbi[i * B + kk], ws2[kk * B + j], s);
+                wa.P2[i * B + j] = s;
+            }
+            if (wa.lc >= 0 && tid < B) {
+                double q = 0.0;
+                for (int kk = 0; kk < B; ++kk) q = fma(wa.V[wa.lc * B + kk], wbi[kk * B + tid], q);
+                wa.qrow[tid] = q;
+            }
         }
     }
     if (eig && tid < B) {
@@ -897,16 +964,17 @@ __global__ __launch_bounds__(kRedThreads) void k_sqrtm_b(const T *__restrict__ G
 
 template <typename T>
 int sqrtm_pair(lz_handle *h, int b, const T *G, int nparts, T *beta, T *beta_inv, T *eig,
-               const double *slabs, const T *L, T *LB)
+               const double *slabs, const T *L, T *LB, const WfAlpha *wa)
 {
     LZ_ARG_CHECK(b >= 1 && b <= 32, "sqrtm supports b <= 32");
+    LZ_ARG_CHECK(!wa || (b == 16 && beta_inv), "the folded alpha products need b = 16 and beta_inv");
     {
     const int ev_ = prof_begin(h, PROF_SMALL);
     const double *sl = slabs ? slabs : h->partials;
 #define LZ_SQRTM_B(BV)                                                                        \
     case BV:                                                                                  \
         hipLaunchKernelGGL((k_sqrtm_b<T, BV>), dim3(1), dim3(kRedThreads), 0, h->stream, G, sl, \
-                           nparts, beta, beta_inv, eig, L, LB);                               \
+                           nparts, beta, beta_inv, eig, L, LB, wa ? *wa : WfAlpha{});          \
         break;
     switch (b) {
         LZ_SQRTM_B(8) LZ_SQRTM_B(16) LZ_SQRTM_B(32)
@@ -1119,7 +1187,8 @@ int copy_row(lz_handle *h, int b, const T *Q, int64_t ld, int col_major, int64_t
     template int gram_partials<T>(lz_handle *, int64_t, int, const T *, const T *, int64_t,    \
                                   int *);                                                      \
     template int gram_finish<T>(lz_handle *, int, int, int, T *, const double *, const T *, T *); \
-    template int sqrtm_pair<T>(lz_handle *, int, const T *, int, T *, T *, T *, const double *, const T *, T *);\
+    template int sqrtm_pair<T>(lz_handle *, int, const T *, int, T *, T *, T *, const double *, const T *, T *,  \
+                               const WfAlpha *);\
     template int tsmm<T>(lz_handle *, int64_t, int, T, T, const T *, const T *, T *, int64_t); \
     template int copy_row<T>(lz_handle *, int, const T *, int64_t, int, int64_t, T *);
 LZ_DENSE_INST(double)

@@ -29,12 +29,25 @@ int gram_partials(lz_handle *h, int64_t n, int b, const T *X, const T *Y, int64_
 template <typename T>
 int gram_finish(lz_handle *h, int b, int nparts, int mode, T *R, const double *slabs = nullptr,
                 const T *L = nullptr, T *LR = nullptr);
+// The wavefront step's alpha products (lz_wf.hip), folded into the sqrtm
+// launch: S1, S2 = sums of the P slabs at part, part + 256 P; alpha =
+// sym(binv (S1 binv - S2 P1)), P2 = binv alpha, qrow = V[lc] binv (lc < 0: none)
+struct WfAlpha {
+    const double *part = nullptr;
+    int P = 0;
+    double *alpha = nullptr, *P2 = nullptr;
+    const double *V = nullptr;
+    int64_t lc = -1;
+    double *qrow = nullptr;
+};
 // symmetric square root pair of G (device double b x b) or, when nparts > 0,
 // of the sum of the nparts slabs in h->partials.  L != null (b in {8,16,32}):
-// also LB = L * beta.
+// also LB = L * beta.  wa (b = 16): also the wavefront alpha products with
+// binv = beta_inv and P1 = LB.
 template <typename T>
 int sqrtm_pair(lz_handle *h, int b, const T *G, int nparts, T *beta, T *beta_inv, T *eig,
-               const double *slabs = nullptr, const T *L = nullptr, T *LB = nullptr);
+               const double *slabs = nullptr, const T *L = nullptr, T *LB = nullptr,
+               const WfAlpha *wa = nullptr);
 // W = sw*W + sq*Q*S
 template <typename T>
 int tsmm(lz_handle *h, int64_t n, int b, T sw, T sq, const T *Q, const T *S, T *W, int64_t ld);
@@ -83,8 +96,10 @@ struct WfPlan {
     bool ok = false;       // the wavefront step applies (n < 2^24, narrow column spans)
     int hback = 0, hfwd = 0;  // max tiles a tile's columns reach below / above it
     int nc = 12, tr = 192;    // consumers per block, rows per tile (16 nc)
+    const int16_t *col16 = nullptr;  // pass 1's 16-bit columns (made in the same pass), or null
 };
-// once per solve: per-tile dependency ranges; synchronises the stream once
+// once per solve: per-tile dependency ranges and the 16-bit columns in one pass
+// over the CSR columns; synchronises the stream once
 int wf_plan16(lz_handle *h, int64_t n, int64_t nnz, const int64_t *rp, const int32_t *col, WfPlan *pl);
 // zero the pass-2 flags (start of a solve; epochs 1, 2, ... follow)
 int wf_reset16(lz_handle *h, int64_t n, const WfPlan &pl);

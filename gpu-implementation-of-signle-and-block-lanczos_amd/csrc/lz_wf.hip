@@ -51,24 +51,38 @@ constexpr int kWfMaxSpan = 256;     // pass-2 tiles one pass-1 tile may read (fl
 constexpr int kWfAux = 16;          // buffer-instruction cache policy: sc1
 constexpr long kWfSpin = 1L << 21;  // flag polls per tile before the loader gives up (about 2 s)
 
-// Per pass-1 tile t: [lo, hi], the tiles holding its columns, t itself
-// included (pass 1 of tile t overwrites Y rows pass 2 of tile t reads).
-// spans: max(t - lo), max(hi - t), max(hi - lo + 1).
+// Once per solve, one pass over the CSR columns: per pass-1 tile t (TR rows)
+// [lo, hi], the tiles holding its columns, t itself included (pass 1 of tile t
+// overwrites Y rows pass 2 of tile t reads); spans[0..2] = max(t - lo),
+// max(hi - t), max(hi - lo + 1); and, when col16 != null, pass 1's 16-bit
+// columns (col16_plan's encoding: the offset from the row's 16-row strip),
+// spans[3] != 0 if one is out of int16 reach.  A wave walks one strip's run
+// (coalesced); one atomic per block and quantity.
 __global__ __launch_bounds__(256) void k_wf_deps(int64_t n, int TR, const int64_t *__restrict__ rp,
                                                  const int32_t *__restrict__ col, int2 *__restrict__ deps,
-                                                 int *__restrict__ spans)
+                                                 int16_t *__restrict__ col16, int *__restrict__ spans)
 {
     __shared__ int smin[4], smax[4];
     const int64_t T = ceil_div(n, (int64_t)TR);
     const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
-    int sb = 0, sf = 0, sw = 0;  // this block's span maxima (thread 0): one atomic each at the end
+    const int ns = TR / 16;
+    int sb = 0, sf = 0, sw = 0, bad = 0;  // this block's span maxima (thread 0) and range flag
     for (int64_t t = blockIdx.x; t < T; t += gridDim.x) {
-        const int64_t r0 = t * TR, r1 = r0 + TR < n ? r0 + TR : n;
         int mn = INT_MAX, mx = -1;
-        for (int64_t k = rp[r0] + threadIdx.x, e = rp[r1]; k < e; k += 256) {
-            const int c = col[k];
-            mn = c < mn ? c : mn;
-            mx = c > mx ? c : mx;
+        for (int s = w; s < ns; s += 4) {
+            const int64_t s0 = t * TR + 16 * s;
+            if (s0 >= n) break;
+            const int64_t s1 = s0 + 16 < n ? s0 + 16 : n;
+            for (int64_t k = rp[s0] + lane, e = rp[s1]; k < e; k += 64) {
+                const int c = col[k];
+                mn = c < mn ? c : mn;
+                mx = c > mx ? c : mx;
+                if (col16) {
+                    const int64_t d = (int64_t)c - s0;
+                    bad |= (d < -32768) | (d > 32767);
+                    col16[k] = (int16_t)d;
+                }
+            }
         }
 #pragma unroll
         for (int o = 32; o > 0; o >>= 1) {
@@ -99,6 +113,7 @@ __global__ __launch_bounds__(256) void k_wf_deps(int64_t n, int TR, const int64_
         }
         __syncthreads();
     }
+    if (__ballot(bad) != 0 && lane == 0) atomicOr(&spans[3], 1);
     if (threadIdx.x == 0) {
         atomicMax(&spans[0], sb);
         atomicMax(&spans[1], sf);
@@ -561,6 +576,7 @@ __global__ __launch_bounds__(64 * (NC + NL + NU)) void k_wf16(
 int wf_plan16(lz_handle *h, int64_t n, int64_t nnz, const int64_t *rp, const int32_t *col, WfPlan *pl)
 {
     pl->ok = false;
+    pl->col16 = nullptr;
     const char *e = getenv("LZ_PASS_WF");  // "0": the two-pass step (A/B); read per call
     // rows of about 11 entries or fewer on average: the tile's CSR run fits the
     // kWfCapPerRow-entry-per-row stage (longer runs take a slow global-gather path)
@@ -581,18 +597,34 @@ int wf_plan16(lz_handle *h, int64_t n, int64_t nnz, const int64_t *rp, const int
         LZ_HIP_TRY(hipMalloc(&h->wf_flags, sizeof(int) * (size_t)(T + 64)));
         h->wf_cap = (size_t)T + 64;
     }
+    // pass 1's 16-bit columns in the same pass (col16_plan's buffer and encoding)
+    const char *c = getenv("LZ_PASS1_C16");  // "0": 32-bit columns (A/B); read per call
+    int16_t *c16 = nullptr;
+    if (!(c && c[0] == '0') && nnz > 0) {
+        const size_t bytes = (size_t)nnz * 2 + 16;  // + the dword the kernel's range may end in
+        if (bytes > h->c16_cap) {
+            LZ_HIP_TRY(hipStreamSynchronize(h->stream));
+            (void)hipFree(h->c16buf);
+            h->c16buf = nullptr;
+            h->c16_cap = 0;
+            LZ_HIP_TRY(hipMalloc(&h->c16buf, bytes));
+            h->c16_cap = bytes;
+        }
+        c16 = static_cast<int16_t *>(h->c16buf);
+    }
     int *spans = h->err_flag + 12;  // err_flag[0]: device error word; [8], [9]: other plans
-    LZ_HIP_TRY(hipMemsetAsync(spans, 0, 3 * sizeof(int), h->stream));
+    LZ_HIP_TRY(hipMemsetAsync(spans, 0, 4 * sizeof(int), h->stream));
     const int grid = (int)std::max<int64_t>(1, std::min<int64_t>(T, (int64_t)h->n_cu * 8));
     hipLaunchKernelGGL(k_wf_deps, dim3(grid), dim3(256), 0, h->stream, n, pl->tr, rp, col,
-                       static_cast<int2 *>(h->wf_deps), spans);
+                       static_cast<int2 *>(h->wf_deps), c16, spans);
     LZ_LAUNCH_CHECK();
-    int sp[3] = {0, 0, 0};
+    int sp[4] = {0, 0, 0, 1};
     LZ_HIP_TRY(hipMemcpyAsync(sp, spans, sizeof(sp), hipMemcpyDeviceToHost, h->stream));
     LZ_HIP_TRY(hipStreamSynchronize(h->stream));
     pl->hback = sp[0];
     pl->hfwd = sp[1];
     pl->ok = sp[2] <= kWfMaxSpan;
+    if (c16 && sp[3] == 0) pl->col16 = c16;
     return LZ_OK;
 }
 
