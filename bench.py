@@ -658,7 +658,11 @@ def main():
             tot = wf_bytes(n, A.nnz, b, spmm_cnt, cb=cb)
             ach = tot / (spmm_ms * 1e-3) / 1e9
             kname, kshort = wf_kernel(n, hw)
-            traffic, tsrc = pmc_traffic(kshort, n, A.nnz, hw, kname)
+            d, tsrc = pmc_record("", kshort, n, A.nnz, hw, kname)
+            traffic = None
+            if d and d.get("hbm_bytes_first_launch"):  # the same launch mix as bytes_per_launch
+                traffic = round((d["hbm_bytes_first_launch"] + (spmm_cnt - 1) * d["hbm_bytes_per_launch"])
+                                / spmm_cnt)
             roof = {"bound": "hbm", "kernel": kname, "achieved": round(ach, 1),
                     "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": round(ach / HBM_PEAK_GBS, 4),
                     "traffic": traffic, "traffic_unit": "bytes/launch (mean over the profiled solve's launches)",

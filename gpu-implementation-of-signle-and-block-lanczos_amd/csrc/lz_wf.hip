@@ -439,15 +439,23 @@ __global__ __launch_bounds__(64 * (NC + NL + NU)) void k_wf16(
     const auto yr = __builtin_amdgcn_make_buffer_rsrc(Yo, (short)0, bytes, 0x00020000);
     double *S0 = scr[cw];
     d4_t macc = {0.0, 0.0, 0.0, 0.0};
-    double v1[4] = {0.0, 0.0, 0.0, 0.0};  // the pending strip's own V_{j+1} rows, accumulator layout
+    double v1[4] = {0.0, 0.0, 0.0, 0.0};  // the pending strip's own V_{j+1} rows (pair-swapped layout)
     int64_t s0p = -1;
     // S1 += V_{j+1}^T Y over the pending strip (Y parked in S0, swizzled)
     auto epilogue = [&]() {
-        double ya[4];
+        double ya[4], va[4];
+        const bool ev = (lane & 1) == 0;
+#pragma unroll
+        for (int h2 = 0; h2 < 2; ++h2) {  // to the accumulator layout (row 4r + g, column c)
+            const double x = v1[2 * h2], y = v1[2 * h2 + 1];
+            const double got = dpp_swap1(ev ? y : x);
+            va[2 * h2] = ev ? x : got;
+            va[2 * h2 + 1] = ev ? got : y;
+        }
 #pragma unroll
         for (int r = 0; r < 4; ++r) ya[r] = S0[fw_sw(4 * r + (lane >> 4), lane & 15)];
 #pragma unroll
-        for (int r = 0; r < 4; ++r) macc = mfma16(v1[r], ya[r], macc);
+        for (int r = 0; r < 4; ++r) macc = mfma16(va[r], ya[r], macc);
     };
     for (int64_t i = 0; i < nt; ++i) {
         const int s = (int)(i % K);
@@ -539,12 +547,17 @@ __global__ __launch_bounds__(64 * (NC + NL + NU)) void k_wf16(
         S0[fw_sw(ra, 2 * p + 1)] = y[1];
         S0[fw_sw(rb, 2 * p)] = y[2];
         S0[fw_sw(rb, 2 * p + 1)] = y[3];
+        // two 16-B loads per lane (the pair swap in the epilogue makes the
+        // accumulator layout): lane (g, c) loads row 8 h2 + g (c even) or
+        // 8 h2 + 4 + g (c odd), columns c & ~1, (c & ~1) + 1
+        // (four 8-B loads in the accumulator layout measured 0.4 % slower)
 #pragma unroll
-        for (int r = 0; r < 4; ++r) {
-            const int64_t row = s0 + (lane >> 4) + 4 * r;
-            const uint32_t off = row < n ? (uint32_t)(row * 128 + (lane & 15) * 8) : 0x80000000u;
-            const auto u = __builtin_amdgcn_raw_buffer_load_b64(xr, off, 0, GA);
-            __builtin_memcpy(&v1[r], &u, 8);
+        for (int h2 = 0; h2 < 2; ++h2) {
+            const int c = lane & 15;
+            const int64_t row = s0 + 8 * h2 + 4 * (c & 1) + (lane >> 4);
+            const uint32_t off = row < n ? (uint32_t)(row * 128 + (c & ~1) * 8) : 0x80000000u;
+            const auto u = __builtin_amdgcn_raw_buffer_load_b128(xr, off, 0, GA);
+            __builtin_memcpy(&v1[2 * h2], &u, 16);
         }
         s0p = s0;
         wave_lds_sync();
@@ -614,6 +627,7 @@ int wf_plan16(lz_handle *h, int64_t n, int64_t nnz, const int64_t *rp, const int
     }
     int *spans = h->err_flag + 12;  // err_flag[0]: device error word; [8], [9]: other plans
     LZ_HIP_TRY(hipMemsetAsync(spans, 0, 4 * sizeof(int), h->stream));
+    // (one tile per block measured slower: its per-block atomics contend)
     const int grid = (int)std::max<int64_t>(1, std::min<int64_t>(T, (int64_t)h->n_cu * 8));
     hipLaunchKernelGGL(k_wf_deps, dim3(grid), dim3(256), 0, h->stream, n, pl->tr, rp, col,
                        static_cast<int2 *>(h->wf_deps), c16, spans);
