@@ -492,6 +492,7 @@ static void detach_comm(lz_handle *h)
     h->xstream = nullptr;
     h->nranks = 1;
     h->rank = 0;
+    h->grid_cap = 0;
 }
 
 // grow a device workspace; never inside the steps (it synchronises)
@@ -622,6 +623,10 @@ static int split_plan(lz_handle *h, int64_t n, const int64_t *rp, const int32_t 
 
 enum { kFormHalo = 0, kFormAllgather = 1 };
 
+static int dist_solve_wf16(lz_handle *h, HaloPlan *hp, int64_t n, int64_t nnz, const int64_t *rp, const int32_t *col,
+                           const double *val, int m, int64_t lc, const double *B, double *q, double *alpha,
+                           double *beta, double *X0, double *X1, const WfPlan &wp, const SplitPlan &sp);
+
 // The distributed iteration, both exchange forms, any b <= 32, fp64 / fp32.
 //   b = 16 fp64: the fused Q-free passes of block_lanczos_fused16 (pass 1 =
 //     SpMM + epilogue, pass 2 update + Gram);
@@ -664,6 +669,27 @@ static int dist_solve_impl(lz_handle *h, int form, HaloPlan *hp, int64_t n, int6
     }
     if (!ag && hp && cm && h->nranks > 1)
         LZ_TRY(grow_ws(h, &hp->sendbuf, &hp->send_cap, (size_t)std::max<int64_t>(hp->n_send, 1) * rowb));
+    if constexpr (std::is_same<T, double>::value) {
+        if (f16 && !ag) {  // the wavefront step when it applies (LZ_PASS_WF=0: the two passes)
+            WfPlan wp;
+            LZ_TRY(wf_plan16(h, n, nnz, rp, col, &wp, nx));
+            if (cm && h->nranks > 1) {  // every rank takes the same form (their collectives must match)
+                double v = wp.ok ? 1.0 : 0.0;
+                LZ_HIP_TRY(hipMemcpyAsync(slab, &v, sizeof(double), hipMemcpyHostToDevice, h->stream));
+                LZ_TRY(cm->allreduce_sum(slab, 1, h->stream));
+                LZ_HIP_TRY(hipMemcpyAsync(&v, slab, sizeof(double), hipMemcpyDeviceToHost, h->stream));
+                LZ_HIP_TRY(hipStreamSynchronize(h->stream));
+                wp.ok = v == (double)h->nranks;
+            }
+            if (wp.ok) {
+                SplitPlan sp;
+                LZ_TRY(split_plan(h, n, rp, col, 0, n, &sp));
+                h->last_split[0] = sp.on ? sp.i0 : -1;
+                h->last_split[1] = sp.on ? sp.i1 : -1;
+                return dist_solve_wf16(h, hp, n, nnz, rp, col, val, m, lc, B, q, alpha, beta, X0, X1, wp, sp);
+            }
+        }
+    }
     Pass1Plan pl;
     if (f16) LZ_TRY(pass1_plan(h, n, nnz, rp, col, nx, own_off, &pl));
     SplitPlan sp;
@@ -762,6 +788,98 @@ static int dist_solve_impl(lz_handle *h, int form, HaloPlan *hp, int64_t n, int6
         }
     }
     LZ_HIP_TRY(hipMemcpyAsync(beta + m * bb, binv[(m - 1) & 1], sizeof(T) * bb, hipMemcpyDeviceToDevice, h->stream));
+    if (cm) LZ_TRY(cm->fence(h->stream));  // no peer reads this rank's buffers after the call
+    return LZ_OK;
+}
+
+// The wavefront step (lz_wf.hip) on a row-partitioned rank, halo form, b = 16
+// fp64.  Per step: one launch runs pass 2 over all own rows and pass 1 over the
+// interior tiles (their columns are own rows); the halo rows of V_{j+1} are
+// exchanged; pass 1 of the boundary tiles (head, tail) runs on the completed
+// gather source; the three sums [S1 | S2 | G] are folded and all-reduced in
+// one 768-double collective; one sqrtm launch makes beta, P1 and alpha, P2, q.
+// V_0 = B copied into X0 (with its halo); V_{j+1} over V_{j-1} in X1, X0, ...;
+// Y (own rows) in the handle's workspace.
+static int dist_solve_wf16(lz_handle *h, HaloPlan *hp, int64_t n, int64_t nnz, const int64_t *rp, const int32_t *col,
+                           const double *val, int m, int64_t lc, const double *B, double *q, double *alpha,
+                           double *beta, double *X0, double *X1, const WfPlan &wp, const SplitPlan &sp)
+{
+    Comm *cm = h->comm;
+    constexpr int64_t bb = 256;
+    const size_t rowb = 128;
+    const int64_t nx = n + (hp ? hp->n_halo : 0);
+    const int64_t T = ceil_div(n, (int64_t)wp.tr);
+    double *slab = h->scratch;  // [S1 | S2 | G], all-reduced in place
+    double *sc = h->scratch + 4 * kMaxB * kMaxB;
+    double *binv[2] = {sc, sc + bb}, *P1 = sc + 2 * bb, *P2 = sc + 3 * bb;
+    (void)nnz;
+    LZ_TRY(grow_ws(h, &h->ybuf, &h->ybuf_cap, (size_t)std::max<int64_t>(n, 1) * rowb));
+    double *Y = static_cast<double *>(h->ybuf);
+    const uint64_t *pairs = nullptr;
+    LZ_TRY(strip_pairs(h, n, rp, &pairs));
+    // interior pass-1 tiles: inside the split plan's interior rows (a single
+    // rank: every tile)
+    int64_t t0 = 0, t1 = T;
+    if (h->nranks > 1 && hp && hp->n_halo > 0) {
+        t0 = t1 = 0;
+        if (sp.on) {
+            t0 = ceil_div(sp.i0, (int64_t)wp.tr);
+            t1 = std::min<int64_t>(T, sp.i1 / wp.tr);
+            if (t1 <= t0) t0 = t1 = 0;
+        }
+    }
+    const bool reduce = cm && h->nranks > 1;
+    auto allreduce = [&](size_t cnt) -> int { return reduce ? cm->allreduce_sum(slab, cnt, h->stream) : LZ_OK; };
+    auto exchange = [&](double *X) -> int { return hp ? halo_exchange(h, *hp, X, rowb, h->stream) : LZ_OK; };
+    const int64_t lcl = (lc >= 0 && lc < n) ? lc : -1;
+    // ---- beta_0 from the global Gram of B; V_0 = B with its halo
+    int np = 0;
+    LZ_TRY(gram_partials<double>(h, n, 16, B, B, 16, &np));
+    LZ_TRY(gram_finish<double>(h, 16, np, 0, slab));
+    LZ_TRY(allreduce(bb));
+    LZ_TRY(sqrtm_pair<double>(h, 16, nullptr, 1, beta, binv[0], nullptr, slab));
+    LZ_HIP_TRY(hipMemcpyAsync(X0, B, (size_t)n * rowb, hipMemcpyDeviceToDevice, h->stream));
+    LZ_TRY(exchange(X0));
+    LZ_TRY(wf_reset16(h, n, wp));
+    // ---- Y_0 = A V_0 (pass 1 only, every tile), alpha_0
+    int G = 0;
+    LZ_TRY(wf_step16(h, n, rp, col, wp.col16, val, pairs, wp, nullptr, nullptr, nullptr, nullptr, nullptr, nullptr,
+                     nullptr, X0, Y, 0, &G, nx, 0, T, h->partials2));
+    LZ_TRY(wf_fold16(h, h->partials2, G, nullptr, 0, nullptr, 0, slab));
+    LZ_TRY(allreduce(3 * bb));
+    LZ_TRY(alpha_wf16(h, slab, 1, binv[0], nullptr, alpha, P2, X0, lcl, n, q));
+    const double *Vm1 = nullptr, *V0 = X0;
+    for (int j = 0; j + 1 < m; ++j) {
+        double *Vn = (j & 1) ? X0 : X1;
+        // pass 2 (every own tile) + pass 1 of the interior tiles
+        int Gk = 0, G1 = 0, G2 = 0;
+        LZ_TRY(wf_step16(h, n, rp, col, wp.col16, val, pairs, wp, Y, Vm1, V0, Vn, binv[j & 1], j ? P1 : nullptr, P2,
+                         Vn, Y, j + 1, &Gk, nx, t0, t1, h->partials2));
+        // V_{j+1}'s halo rows, then pass 1 of the boundary tiles
+        LZ_TRY(exchange(Vn));
+        double *p1 = h->partials2 + 3 * (int64_t)Gk * 256;
+        LZ_TRY(wf_step16(h, n, rp, col, wp.col16, val, pairs, wp, nullptr, nullptr, nullptr, nullptr, nullptr,
+                         nullptr, nullptr, Vn, Y, 0, &G1, nx, 0, t0, p1));
+        double *p2 = p1 + 3 * (int64_t)G1 * 256;
+        LZ_TRY(wf_step16(h, n, rp, col, wp.col16, val, pairs, wp, nullptr, nullptr, nullptr, nullptr, nullptr,
+                         nullptr, nullptr, Vn, Y, 0, &G2, nx, t1, T, p2));
+        LZ_TRY(wf_fold16(h, h->partials2, Gk, p1, G1, p2, G2, slab));
+        LZ_TRY(allreduce(3 * bb));
+        WfAlpha wa;
+        wa.part = slab;
+        wa.P = 1;
+        wa.alpha = alpha + (j + 1) * bb;
+        wa.P2 = P2;
+        wa.V = Vn;
+        wa.lc = lcl;
+        wa.qrow = q + (j + 1) * 16;
+        LZ_TRY(sqrtm_pair<double>(h, 16, nullptr, 1, beta + (j + 1) * bb, binv[(j + 1) & 1], nullptr, slab + 2 * bb,
+                                  binv[j & 1], P1, &wa));
+        Vm1 = V0;
+        V0 = Vn;
+    }
+    LZ_HIP_TRY(hipMemcpyAsync(beta + m * bb, binv[(m - 1) & 1], sizeof(double) * bb, hipMemcpyDeviceToDevice,
+                              h->stream));
     if (cm) LZ_TRY(cm->fence(h->stream));  // no peer reads this rank's buffers after the call
     return LZ_OK;
 }

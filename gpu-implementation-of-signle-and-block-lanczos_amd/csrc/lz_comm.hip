@@ -352,6 +352,9 @@ int lz_comm_init_local(lz_handle *h, lz_local_group *grp, int rank)
     int rc = make_events();
     if (rc == LZ_OK) rc = attach_comm(h, c);  // owns c from here, also on failure
     else delete c;
+    // the ranks share the device: a kernel whose blocks wait on each other (the
+    // wavefront step) gets a share of the CUs so every rank's grid is resident
+    if (rc == LZ_OK) h->grid_cap = std::max(1, h->n_cu / st->n);
     return rc;
 }
 

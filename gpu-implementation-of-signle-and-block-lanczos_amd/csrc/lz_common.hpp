@@ -66,6 +66,7 @@ struct lz_handle {
     hipStream_t side = nullptr;
     hipEvent_t ev_fork = nullptr, ev_join = nullptr;
     int n_cu = 256;
+    int grid_cap = 0;  // > 0: at most this many blocks for kernels whose blocks wait on each other
     // device workspace: per-workgroup partial b x b sums (double), b x b
     // scratch matrices and a few scalars.
     double *partials = nullptr;   // per-workgroup / per-tile slabs (grown on demand)

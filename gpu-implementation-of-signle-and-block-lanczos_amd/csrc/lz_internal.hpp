@@ -100,7 +100,8 @@ struct WfPlan {
 };
 // once per solve: per-tile dependency ranges and the 16-bit columns in one pass
 // over the CSR columns; synchronises the stream once
-int wf_plan16(lz_handle *h, int64_t n, int64_t nnz, const int64_t *rp, const int32_t *col, WfPlan *pl);
+int wf_plan16(lz_handle *h, int64_t n, int64_t nnz, const int64_t *rp, const int32_t *col, WfPlan *pl,
+              int64_t nx = -1);  // nx: rows of the gather source (a rank's own + halo rows), default n
 // zero the pass-2 flags (start of a solve; epochs 1, 2, ... follow)
 int wf_reset16(lz_handle *h, int64_t n, const WfPlan &pl);
 // P2 == nullptr: pass 1 only (Y = A Vg, S1 slabs).  Otherwise V_{j+1} = Yj binv
@@ -110,7 +111,13 @@ int wf_reset16(lz_handle *h, int64_t n, const WfPlan &pl);
 int wf_step16(lz_handle *h, int64_t n, const int64_t *rp, const int32_t *col, const int16_t *col16,
               const double *val, const uint64_t *pairs, const WfPlan &pl, const double *Yj, const double *Vprev,
               const double *Vj, double *Vout, const double *binv, const double *P1, const double *P2,
-              const double *Vg, double *Yo, int epoch, int *nparts);
+              const double *Vg, double *Yo, int epoch, int *nparts, int64_t nx = -1, int64_t p1a = 0,
+              int64_t p1b = -1, double *part = nullptr);
+// (nx: rows of Vg, default n; pass 1 over tiles [p1a, p1b), default all; slabs
+// at part, default h->partials2)
+// the distributed step's sums: out[0..768) = [S1 (step launch G slabs + G1 + G2
+// boundary slabs) | S2 | G]
+int wf_fold16(lz_handle *h, const double *kp, int G, const double *b1, int G1, const double *b2, int G2, double *out);
 // alpha = sym(binv (S1 binv - S2 P1)) (P1 == nullptr: no S2 term), P2 = binv alpha,
 // q = V[lc] binv; S1, S2 = the sums of the P slabs at part, part + 256 P
 int alpha_wf16(lz_handle *h, const double *part, int P, const double *binv, const double *P1, double *alpha,

@@ -56,11 +56,12 @@ constexpr long kWfSpin = 1L << 21;  // flag polls per tile before the loader giv
 // overwrites Y rows pass 2 of tile t reads); spans[0..2] = max(t - lo),
 // max(hi - t), max(hi - lo + 1); and, when col16 != null, pass 1's 16-bit
 // columns (col16_plan's encoding: the offset from the row's 16-row strip),
-// spans[3] != 0 if one is out of int16 reach.  A wave walks one strip's run
+// spans[3] != 0 if one is out of int16 reach.  Columns >= ncol (a rank's halo
+// rows) are left out of the ranges.  A wave walks one strip's run
 // (coalesced); one atomic per block and quantity.
 __global__ __launch_bounds__(256) void k_wf_deps(int64_t n, int TR, const int64_t *__restrict__ rp,
                                                  const int32_t *__restrict__ col, int2 *__restrict__ deps,
-                                                 int16_t *__restrict__ col16, int *__restrict__ spans)
+                                                 int16_t *__restrict__ col16, int *__restrict__ spans, int64_t ncol)
 {
     __shared__ int smin[4], smax[4];
     const int64_t T = ceil_div(n, (int64_t)TR);
@@ -75,8 +76,10 @@ __global__ __launch_bounds__(256) void k_wf_deps(int64_t n, int TR, const int64_
             const int64_t s1 = s0 + 16 < n ? s0 + 16 : n;
             for (int64_t k = rp[s0] + lane, e = rp[s1]; k < e; k += 64) {
                 const int c = col[k];
-                mn = c < mn ? c : mn;
-                mx = c > mx ? c : mx;
+                if (c < ncol) {  // (a distributed rank's halo columns: its boundary tiles, no flags)
+                    mn = c < mn ? c : mn;
+                    mx = c > mx ? c : mx;
+                }
                 if (col16) {
                     const int64_t d = (int64_t)c - s0;
                     bad |= (d < -32768) | (d > 32767);
@@ -147,7 +150,8 @@ __global__ __launch_bounds__(64 * (NC + NL + NU)) void k_wf16(
     const double *__restrict__ val, const uint64_t *__restrict__ pairs, const double *Yj, const double *Vprev,
     const double *__restrict__ Vj, double *Vout, const double *__restrict__ binv, const double *__restrict__ P1,
     const double *__restrict__ P2, const double *Vg, double *Yo, const int2 *__restrict__ deps, int *flags, int epoch,
-    int64_t hback, int lead, double *__restrict__ part, int *__restrict__ err, int dbg)
+    int64_t hback, int lead, double *__restrict__ part, int *__restrict__ err, int dbg, int64_t nx, int64_t p1a,
+    int64_t p1b)
 {
     using CT = typename std::conditional<C16, int16_t, int32_t>::type;
     using C = FwCfg<NC, CAP, true, true, CT>;
@@ -176,13 +180,16 @@ __global__ __launch_bounds__(64 * (NC + NL + NU)) void k_wf16(
     // regions: pass-1 tiles [begin, end) of region x go to the blocks b = x
     // (mod 8), interleaved; the region's pass-2 tiles are [pbeg, pend), the
     // same range moved hback tiles down, so the pass-2 wavefront leads
+    // (pass-1 tiles: [p1a, p1b) -- all of them, or the interior ones of a
+    // distributed rank; pass 2 covers every tile)
     int64_t begin, end, kb, KB, pbeg, pend;
+    const int64_t NP1 = p1b - p1a;
     if (G < 8) {
-        begin = 0; end = T; kb = bid; KB = G; pbeg = 0; pend = T;
+        begin = p1a; end = p1b; kb = bid; KB = G; pbeg = 0; pend = T;
     } else {
         const int64_t x = bid & 7;
-        begin = T * x / 8;
-        end = T * (x + 1) / 8;
+        begin = p1a + NP1 * x / 8;
+        end = p1a + NP1 * (x + 1) / 8;
         kb = bid >> 3;
         KB = (G - x + 7) >> 3;
         pbeg = x == 0 ? 0 : (begin - hback > 0 ? begin - hback : 0);
@@ -309,8 +316,11 @@ __global__ __launch_bounds__(64 * (NC + NL + NU)) void k_wf16(
                 if (s >= ns || s / NC <= paced) return;
                 paced = s / NC;
                 const uint32_t pa = ws_lds_addr(&p1pub);
+                // (never more than the block's pass-1 tiles: a distributed rank's
+                // pass 1 here covers only the interior)
+                const int target = (int)(m - lead < nt ? m - lead : nt);
                 long spin = 0;
-                while (ws_lds_read(pa) < (int)(m - lead) && ++spin < kWsSpin) __builtin_amdgcn_s_sleep(2);
+                while (ws_lds_read(pa) < target && ++spin < kWsSpin) __builtin_amdgcn_s_sleep(2);
                 if (spin >= kWsSpin) *err = 6;
             };
             auto dma = [&](int64_t s) {
@@ -435,7 +445,7 @@ __global__ __launch_bounds__(64 * (NC + NL + NU)) void k_wf16(
         else if (pr == 2) __builtin_amdgcn_s_setprio(2);
     }
     const int bytes = (int)(n * 128);
-    const auto xr = __builtin_amdgcn_make_buffer_rsrc(const_cast<double *>(Vg), (short)0, bytes, 0x00020000);
+    const auto xr = __builtin_amdgcn_make_buffer_rsrc(const_cast<double *>(Vg), (short)0, (int)(nx * 128), 0x00020000);
     const auto yr = __builtin_amdgcn_make_buffer_rsrc(Yo, (short)0, bytes, 0x00020000);
     double *S0 = scr[cw];
     d4_t macc = {0.0, 0.0, 0.0, 0.0};
@@ -586,8 +596,9 @@ __global__ __launch_bounds__(64 * (NC + NL + NU)) void k_wf16(
     }
 }
 
-int wf_plan16(lz_handle *h, int64_t n, int64_t nnz, const int64_t *rp, const int32_t *col, WfPlan *pl)
+int wf_plan16(lz_handle *h, int64_t n, int64_t nnz, const int64_t *rp, const int32_t *col, WfPlan *pl, int64_t nx)
 {
+    if (nx < 0) nx = n;
     pl->ok = false;
     pl->col16 = nullptr;
     const char *e = getenv("LZ_PASS_WF");  // "0": the two-pass step (A/B); read per call
@@ -597,7 +608,7 @@ int wf_plan16(lz_handle *h, int64_t n, int64_t nnz, const int64_t *rp, const int
     const int want = sh ? atoi(sh) : 10;
     pl->nc = (want == 11 || want == 12) ? want : 10;
     pl->tr = 16 * pl->nc;
-    if ((e && e[0] == '0') || n < pl->tr || n >= (1 << 24) || (double)nnz > 10.2 * (double)n) return LZ_OK;
+    if ((e && e[0] == '0') || n < pl->tr || nx >= (1 << 24) || (double)nnz > 10.2 * (double)n) return LZ_OK;
     const int64_t T = ceil_div(n, (int64_t)pl->tr);
     if ((size_t)T + 64 > h->wf_cap) {
         LZ_HIP_TRY(hipStreamSynchronize(h->stream));
@@ -630,7 +641,7 @@ int wf_plan16(lz_handle *h, int64_t n, int64_t nnz, const int64_t *rp, const int
     // (one tile per block measured slower: its per-block atomics contend)
     const int grid = (int)std::max<int64_t>(1, std::min<int64_t>(T, (int64_t)h->n_cu * 8));
     hipLaunchKernelGGL(k_wf_deps, dim3(grid), dim3(256), 0, h->stream, n, pl->tr, rp, col,
-                       static_cast<int2 *>(h->wf_deps), c16, spans);
+                       static_cast<int2 *>(h->wf_deps), c16, spans, n);
     LZ_LAUNCH_CHECK();
     int sp[4] = {0, 0, 0, 1};
     LZ_HIP_TRY(hipMemcpyAsync(sp, spans, sizeof(sp), hipMemcpyDeviceToHost, h->stream));
@@ -645,13 +656,26 @@ int wf_plan16(lz_handle *h, int64_t n, int64_t nnz, const int64_t *rp, const int
 int wf_step16(lz_handle *h, int64_t n, const int64_t *rp, const int32_t *col, const int16_t *col16,
               const double *val, const uint64_t *pairs, const WfPlan &pl, const double *Yj, const double *Vprev,
               const double *Vj, double *Vout, const double *binv, const double *P1, const double *P2,
-              const double *Vg, double *Yo, int epoch, int *nparts)
+              const double *Vg, double *Yo, int epoch, int *nparts, int64_t nx, int64_t p1a, int64_t p1b,
+              double *part)
 {
+    const int64_t T = ceil_div(n, (int64_t)pl.tr);
+    if (nx < 0) nx = n;
+    if (p1b < 0) p1b = T;
+    if (!part) part = h->partials2;
+    LZ_ARG_CHECK(nx >= n && nx < (1 << 24) && 0 <= p1a && p1a <= p1b && p1b <= T, "wavefront step ranges");
     LZ_ARG_CHECK(pl.ok && n < (1 << 24), "wavefront step: wf_plan16 first");
     LZ_ARG_CHECK(pairs != nullptr, "strip row orders (strip_pairs) missing");
     LZ_ARG_CHECK(P2 == nullptr || (Yj && Vj && Vout && binv && Vg == Vout), "wavefront step buffers");
     static_assert(12 <= kPairPad, "row orders must cover the last tile's strips");
-    const int grid = (int)std::max<int64_t>(1, std::min<int64_t>(ceil_div(n, (int64_t)pl.tr), h->n_cu));
+    // pass 2 covers every tile when it runs; a pass-1-only launch its range
+    const int64_t work = P2 ? T : p1b - p1a;
+    if (work <= 0) {
+        *nparts = 0;
+        return LZ_OK;
+    }
+    // (virtual ranks sharing the device: each rank's share, so every grid is resident)
+    const int grid = (int)std::max<int64_t>(1, std::min<int64_t>(work, h->grid_cap > 0 ? h->grid_cap : h->n_cu));
     // LZ_WF_DBG (timing diagnostics only; results are wrong): bit 0 skips the
     // loaders' flag polls, bit 1 the updaters' work, bit 2 the pass-1 tiles;
     // bit 3 / bit 6 run the updaters at issue priority 0 / 3 (default 2)
@@ -668,7 +692,7 @@ int wf_step16(lz_handle *h, int64_t n, const int64_t *rp, const int32_t *col, co
         hipLaunchKernelGGL(kern, dim3(grid), dim3(1024), 0, h->stream, n, rp, col, col16, val,
                            pairs, Yj, Vprev, Vj, Vout, binv, P1, P2, Vg, Yo,
                            static_cast<const int2 *>(h->wf_deps), h->wf_flags, epoch, (int64_t)pl.hback, lead,
-                           h->partials2, h->err_flag, dbg);
+                           part, h->err_flag, dbg, nx, p1a, p1b);
     };
     // LDS (<= 160 KB): strip slots per updater DU + 1, fewer with 32-bit columns
     constexpr int cap12 = 12 * 16 * kWfCapPerRow, cap11 = 11 * 16 * kWfCapPerRow, cap10 = 10 * 16 * kWfCapPerRow;
@@ -681,6 +705,33 @@ int wf_step16(lz_handle *h, int64_t n, const int64_t *rp, const int32_t *col, co
     prof_end(h, ev);
     LZ_LAUNCH_CHECK();
     *nparts = grid;
+    return LZ_OK;
+}
+
+// The distributed wavefront step's three sums (lz_api.hip dist_solve_wf16):
+// out[0, 256) = S1 over the step launch's G slabs, then the boundary launches'
+// G1 and G2; out[256, 512) = S2 and out[512, 768) = G of the step launch.
+// Fixed order: bitwise reproducible.
+__global__ __launch_bounds__(768) void k_wf_fold(const double *__restrict__ kp, int G, const double *__restrict__ b1,
+                                                 int G1, const double *__restrict__ b2, int G2,
+                                                 double *__restrict__ out)
+{
+    const int e = threadIdx.x, m = e >> 8, i = e & 255;
+    double s = 0.0;
+    for (int g = 0; g < G; ++g) s += kp[((int64_t)m * G + g) * 256 + i];
+    if (m == 0) {
+        for (int g = 0; g < G1; ++g) s += b1[(int64_t)g * 256 + i];
+        for (int g = 0; g < G2; ++g) s += b2[(int64_t)g * 256 + i];
+    }
+    out[e] = s;
+}
+
+int wf_fold16(lz_handle *h, const double *kp, int G, const double *b1, int G1, const double *b2, int G2, double *out)
+{
+    const int ev = prof_begin(h, PROF_SMALL);
+    hipLaunchKernelGGL(k_wf_fold, dim3(1), dim3(768), 0, h->stream, kp, G, b1, G1, b2, G2, out);
+    prof_end(h, ev);
+    LZ_LAUNCH_CHECK();
     return LZ_OK;
 }
 

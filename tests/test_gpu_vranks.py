@@ -110,6 +110,22 @@ def test_vranks_b16_banded(lz, orc, torch_cuda, form, nranks):
     assert_close_run(lz, m, 16, got, orc.block_lanczos(A, B, m, lc))
 
 
+@pytest.mark.parametrize("wf", ["0", "1"])
+@pytest.mark.parametrize("nranks", [1, 3, 4])
+def test_vranks_b16_halo_step_forms(lz, orc, torch_cuda, monkeypatch, wf, nranks):
+    """The halo form's two step forms: the wavefront step per rank (pass 2 +
+    interior pass 1 in one launch, then the exchange and the boundary tiles;
+    the default) and the two-pass step (LZ_PASS_WF=0), with the split on and
+    off (at 4 ranks the half width exceeds a rank's rows: no interior tiles)."""
+    monkeypatch.setenv("LZ_PASS_WF", wf)
+    hw = 30_000 if nranks == 4 else 2048
+    A = lz.gen_banded(100_003, 10.0, hw, seed=40 + nranks)
+    B = lz.uniform_B(A.n, 16, seed=3)
+    m, lc = 8, 77_777
+    got, _ = run_dist(lz, torch_cuda, A, B, m, lc, nranks, "halo")
+    assert_close_run(lz, m, 16, got, orc.block_lanczos(A, B, m, lc))
+
+
 @pytest.mark.parametrize("form", ["halo", "allgather"])
 def test_vranks_b16_overlap_off_equals_on(lz, orc, torch_cuda, form):
     """LZ_DIST_OVERLAP=0 (exchange, then the whole pass) against the split run:
