@@ -151,7 +151,7 @@ __global__ __launch_bounds__(64 * (NC + NL + NU)) void k_wf16(
     const double *__restrict__ Vj, double *Vout, const double *__restrict__ binv, const double *__restrict__ P1,
     const double *__restrict__ P2, const double *Vg, double *Yo, const int2 *__restrict__ deps, int *flags, int epoch,
     int64_t hback, int lead, double *__restrict__ part, int *__restrict__ err, int dbg, int64_t nx, int64_t p1a,
-    int64_t p1b)
+    int64_t p1b, int64_t Th)
 {
     using CT = typename std::conditional<C16, int16_t, int32_t>::type;
     using C = FwCfg<NC, CAP, true, true, CT>;
@@ -176,6 +176,10 @@ __global__ __launch_bounds__(64 * (NC + NL + NU)) void k_wf16(
     }
     __syncthreads();  // the only block barrier
     const int64_t T = ceil_div(n, (int64_t)TR);
+    if (T != Th) {  // the host planned other tiles (flags, ranges): refuse loudly
+        if (threadIdx.x == 0) *err = 7;
+        return;
+    }
     const int64_t G = gridDim.x, bid = blockIdx.x;
     // regions: pass-1 tiles [begin, end) of region x go to the blocks b = x
     // (mod 8), interleaved; the region's pass-2 tiles are [pbeg, pend), the
@@ -692,16 +696,20 @@ int wf_step16(lz_handle *h, int64_t n, const int64_t *rp, const int32_t *col, co
         hipLaunchKernelGGL(kern, dim3(grid), dim3(1024), 0, h->stream, n, rp, col, col16, val,
                            pairs, Yj, Vprev, Vj, Vout, binv, P1, P2, Vg, Yo,
                            static_cast<const int2 *>(h->wf_deps), h->wf_flags, epoch, (int64_t)pl.hback, lead,
-                           part, h->err_flag, dbg, nx, p1a, p1b);
+                           part, h->err_flag, dbg, nx, p1a, p1b, T);
     };
     // LDS (<= 160 KB): strip slots per updater DU + 1, fewer with 32-bit columns
     constexpr int cap12 = 12 * 16 * kWfCapPerRow, cap11 = 11 * 16 * kWfCapPerRow, cap10 = 10 * 16 * kWfCapPerRow;
-    if (pl.nc == 11 && col16) go(k_wf16<11, cap11, kWfK, kWfNL, 3, 2, true>);
-    else if (col16) go(k_wf16<10, cap10, kWfK, kWfNL, 4, 2, true>);
-    else if (pl.nc == 12 && col16) go(k_wf16<12, cap12, kWfK, kWfNL, 2, 3, true>);
-    else if (pl.nc == 12) go(k_wf16<12, cap12, kWfK, kWfNL, 2, 2, false>);
-    else if (pl.nc == 11) go(k_wf16<11, cap11, kWfK, kWfNL, 3, 2, false>);
-    else go(k_wf16<10, cap10, kWfK, kWfNL, 4, 1, false>);
+    // (the instantiation must match pl.tr: the tile count above is the host's)
+    if (col16) {
+        if (pl.nc == 12) go(k_wf16<12, cap12, kWfK, kWfNL, 2, 3, true>);
+        else if (pl.nc == 11) go(k_wf16<11, cap11, kWfK, kWfNL, 3, 2, true>);
+        else go(k_wf16<10, cap10, kWfK, kWfNL, 4, 2, true>);
+    } else {
+        if (pl.nc == 12) go(k_wf16<12, cap12, kWfK, kWfNL, 2, 2, false>);
+        else if (pl.nc == 11) go(k_wf16<11, cap11, kWfK, kWfNL, 3, 2, false>);
+        else go(k_wf16<10, cap10, kWfK, kWfNL, 4, 1, false>);
+    }
     prof_end(h, ev);
     LZ_LAUNCH_CHECK();
     *nparts = grid;
