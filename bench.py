@@ -652,24 +652,25 @@ def main():
         hw = args.halfwidth
         cb = col_bytes(n, hw)
         # the wavefront step (lz_wf.hip) has no separate update pass
-        wf = fused and world == 1 and spmm_cnt > 0 and upd_cnt == 0
+        wf = fused and spmm_cnt > 0 and upd_cnt == 0
         if fused and wf:
-            # one solve of K steps: K launches, the first pass 1 only
-            tot = wf_bytes(n, A.nnz, b, spmm_cnt, cb=cb)
+            # one solve of K steps: the first step pass 1 only, the others pass 2 + pass 1 (at N > 1 the
+            # boundary tiles' pass 1 is a launch of its own: same bytes, more launches)
+            tot = wf_bytes(n, A.nnz, b, K, cb=cb)
             ach = tot / (spmm_ms * 1e-3) / 1e9
             kname, kshort = wf_kernel(n, hw)
             d, tsrc = pmc_record("", kshort, n, A.nnz, hw, kname)
             traffic = None
-            if d and d.get("hbm_bytes_first_launch"):  # the same launch mix as bytes_per_launch
-                traffic = round((d["hbm_bytes_first_launch"] + (spmm_cnt - 1) * d["hbm_bytes_per_launch"])
-                                / spmm_cnt)
+            if d and d.get("hbm_bytes_first_launch") and spmm_cnt == K:  # the launch mix of bytes_per_launch
+                traffic = round((d["hbm_bytes_first_launch"] + (K - 1) * d["hbm_bytes_per_launch"]) / K)
             roof = {"bound": "hbm", "kernel": kname, "achieved": round(ach, 1),
                     "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": round(ach / HBM_PEAK_GBS, 4),
                     "traffic": traffic, "traffic_unit": "bytes/launch (mean over the profiled solve's launches)",
                     "traffic_source": tsrc, "avg_ms": round(t_pass * 1e3, 4),
                     "bytes_per_launch": round(tot / spmm_cnt),
-                    "bytes_note": f"{spmm_cnt} launches per solve: the first pass 1 only (A + 2nbs), the others "
-                                  f"pass 2 of step j + pass 1 of step j+1 (A + 5nbs); A with {cb}-byte columns"}
+                    "bytes_note": f"{K} steps per solve in {spmm_cnt} launches: the first step pass 1 only (A + 2nbs), "
+                                  f"the others pass 2 of step j + pass 1 of step j+1 (A + 5nbs); A with {cb}-byte "
+                                  f"columns"}
             fl = WF_MFMA_FLOP_PER_ROW * n
             tf = fl / t_pass / 1e12
             ent = {"kernel": kshort, "mfma_flop_per_launch": fl, "avg_ms": round(t_pass * 1e3, 4),
