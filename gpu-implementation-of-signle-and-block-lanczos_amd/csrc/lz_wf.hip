@@ -720,24 +720,41 @@ int wf_step16(lz_handle *h, int64_t n, const int64_t *rp, const int32_t *col, co
 // out[0, 256) = S1 over the step launch's G slabs, then the boundary launches'
 // G1 and G2; out[256, 512) = S2 and out[512, 768) = G of the step launch.
 // Fixed order: bitwise reproducible.
-__global__ __launch_bounds__(768) void k_wf_fold(const double *__restrict__ kp, int G, const double *__restrict__ b1,
-                                                 int G1, const double *__restrict__ b2, int G2,
-                                                 double *__restrict__ out)
+__global__ __launch_bounds__(1024) void k_wf_fold(const double *__restrict__ kp, int G, const double *__restrict__ b1,
+                                                  int G1, const double *__restrict__ b2, int G2,
+                                                  double *__restrict__ out)
 {
-    const int e = threadIdx.x, m = e >> 8, i = e & 255;
-    double s = 0.0;
-    for (int g = 0; g < G; ++g) s += kp[((int64_t)m * G + g) * 256 + i];
+    // block m sums matrix m: thread (q, i) adds slabs q, q + 4, ... with four
+    // independent accumulators (loads in flight), then the four partial sums
+    // are added in order q = 0..3 -- a fixed order, bitwise reproducible
+    __shared__ double ps[4][256];
+    const int m = blockIdx.x, q = threadIdx.x >> 8, i = threadIdx.x & 255;
+    auto sum = [&](const double *p, int P) {
+        double a0 = 0.0, a1 = 0.0, a2 = 0.0, a3 = 0.0;
+        int g = q;
+        for (; g + 12 < P; g += 16) {
+            a0 += p[(int64_t)g * 256 + i];
+            a1 += p[(int64_t)(g + 4) * 256 + i];
+            a2 += p[(int64_t)(g + 8) * 256 + i];
+            a3 += p[(int64_t)(g + 12) * 256 + i];
+        }
+        for (; g < P; g += 4) a0 += p[(int64_t)g * 256 + i];
+        return (a0 + a1) + (a2 + a3);
+    };
+    double s = sum(kp + (int64_t)m * G * 256, G);
     if (m == 0) {
-        for (int g = 0; g < G1; ++g) s += b1[(int64_t)g * 256 + i];
-        for (int g = 0; g < G2; ++g) s += b2[(int64_t)g * 256 + i];
+        s += sum(b1, G1);
+        s += sum(b2, G2);
     }
-    out[e] = s;
+    ps[q][i] = s;
+    __syncthreads();
+    if (q == 0) out[m * 256 + i] = (ps[0][i] + ps[1][i]) + (ps[2][i] + ps[3][i]);
 }
 
 int wf_fold16(lz_handle *h, const double *kp, int G, const double *b1, int G1, const double *b2, int G2, double *out)
 {
     const int ev = prof_begin(h, PROF_SMALL);
-    hipLaunchKernelGGL(k_wf_fold, dim3(1), dim3(768), 0, h->stream, kp, G, b1, G1, b2, G2, out);
+    hipLaunchKernelGGL(k_wf_fold, dim3(3), dim3(1024), 0, h->stream, kp, G, b1, G1, b2, G2, out);
     prof_end(h, ev);
     LZ_LAUNCH_CHECK();
     return LZ_OK;
