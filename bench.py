@@ -91,10 +91,13 @@ def wf_kernel(n, hw):
     """(full name, PMC short name) of the wavefront-step kernel (lz_wf.hip wf_step16):
     <consumers, stage entries, stages, loaders, updaters, strip slots - 1, 16-bit columns>."""
     c16 = col_bytes(n, hw) == 2
-    nc = os.environ.get("LZ_WF_SHAPE", "10")
-    nc = int(nc) if nc in ("11", "12") else 10
+    sh = os.environ.get("LZ_WF_SHAPE", "111")
+    tf = 'true' if c16 else 'false'
+    if sh not in ("10", "11", "12"):  # default: 1 loader + 11 consumers + 4 updaters
+        return f"k_wf16<11,{11 * 16 * 11},3,1,4,1,{tf}>", "k_wf16"
+    nc = int(sh)
     du = {10: 2 if c16 else 1, 11: 2, 12: 3 if c16 else 2}[nc]
-    return f"k_wf16<{nc},{nc * 16 * 11},3,2,{14 - nc},{du},{'true' if c16 else 'false'}>", "k_wf16"
+    return f"k_wf16<{nc},{nc * 16 * 11},3,2,{14 - nc},{du},{tf}>", "k_wf16"
 
 
 # MFMA work of the wavefront step per row: updaters 12 (V_{j+1}) + 4 (G) + 4 (S2),

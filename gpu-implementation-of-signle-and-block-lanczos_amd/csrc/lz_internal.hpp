@@ -96,6 +96,7 @@ struct WfPlan {
     bool ok = false;       // the wavefront step applies (n < 2^24, narrow column spans)
     int hback = 0, hfwd = 0;  // max tiles a tile's columns reach below / above it
     int nc = 12, tr = 192;    // consumers per block, rows per tile (16 nc)
+    int var = 0;              // measurement shape (LZ_WF_SHAPE 104 / 111), 0: the standard ones
     const int16_t *col16 = nullptr;  // pass 1's 16-bit columns (made in the same pass), or null
 };
 // once per solve: per-tile dependency ranges and the 16-bit columns in one pass

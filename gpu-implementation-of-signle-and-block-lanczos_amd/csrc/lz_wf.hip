@@ -41,10 +41,12 @@
 
 namespace lz {
 
-// block shapes (LZ_WF_SHAPE "NC" for 2 loaders + NC consumers + 14 - NC
-// updaters): 10 (default: one updater per SIMD), 11, 12; tiles of 16 NC rows.
-// An updater wave is bound by its SIMD's MFMA pipe: at C3 2 + 13 + 1 took
-// 3.1 ms, 2 + 12 + 2 1.93, 2 + 11 + 3 1.87, 2 + 10 + 4 1.86 (scripts/ab_c3.py).
+// block shapes (LZ_WF_SHAPE): 111 (default) = 1 loader + 11 consumers + 4
+// updaters (one per SIMD); "NC" = 10, 11, 12 for 2 loaders + NC consumers +
+// 14 - NC updaters; tiles of 16 NC rows. An updater wave is bound by its
+// SIMD's MFMA pipe: at C3 2 + 13 + 1 took 3.1 ms, 2 + 12 + 2 1.93, 2 + 11 + 3
+// 1.87, 2 + 10 + 4 1.86, 1 + 11 + 4 1.82, 1 + 12 + 3 1.87, 1 + 10 + 5 1.94
+// (scripts/ab_c3.py); one loader wave keeps up with 11 consumers.
 constexpr int kWfK = 3, kWfNL = 2;
 constexpr int kWfCapPerRow = 11;  // stage entries per row (C3: 10 +- 2.2 nnz per row)
 constexpr int kWfMaxSpan = 256;     // pass-2 tiles one pass-1 tile may read (flag polls per tile)
@@ -609,8 +611,11 @@ int wf_plan16(lz_handle *h, int64_t n, int64_t nnz, const int64_t *rp, const int
     // rows of about 11 entries or fewer on average: the tile's CSR run fits the
     // kWfCapPerRow-entry-per-row stage (longer runs take a slow global-gather path)
     const char *sh = getenv("LZ_WF_SHAPE");  // consumers per block (A/B); read per call
-    const int want = sh ? atoi(sh) : 10;
-    pl->nc = (want == 11 || want == 12) ? want : 10;
+    const int want = sh ? atoi(sh) : 111;
+    // 111 (default): 1 loader, 11 consumers, 4 updaters; 10 / 11 / 12: 2
+    // loaders, NC consumers, 14 - NC updaters
+    pl->var = (want == 10 || want == 11 || want == 12) ? 0 : 111;
+    pl->nc = pl->var ? 11 : want;
     pl->tr = 16 * pl->nc;
     if ((e && e[0] == '0') || n < pl->tr || nx >= (1 << 24) || (double)nnz > 10.2 * (double)n) return LZ_OK;
     const int64_t T = ceil_div(n, (int64_t)pl->tr);
@@ -690,7 +695,9 @@ int wf_step16(lz_handle *h, int64_t n, const int64_t *rp, const int32_t *col, co
     const int KB = grid < 8 ? grid : grid / 8;
     const int lmin = (int)((pl.hback + pl.hfwd + KB - 1) / KB) + 2;
     const char *le = getenv("LZ_WF_LEAD");
-    const int lead = std::max(lmin, le ? atoi(le) : lmin + 4);  // C3: lmin 4; 7-9 measured best
+    // C3 (lmin 4): shape 111 best at 7 (5: 3.07 ms, 6: 1.90, 7: 1.82, 8: 1.84, 10: 1.87);
+    // the 2-loader shapes at 8
+    const int lead = std::max(lmin, le ? atoi(le) : lmin + (pl.var == 111 ? 3 : 4));
     const int ev = prof_begin(h, PROF_SPMM_PASS);
     auto go = [&](auto kern) {
         hipLaunchKernelGGL(kern, dim3(grid), dim3(1024), 0, h->stream, n, rp, col, col16, val,
@@ -701,7 +708,9 @@ int wf_step16(lz_handle *h, int64_t n, const int64_t *rp, const int32_t *col, co
     // LDS (<= 160 KB): strip slots per updater DU + 1, fewer with 32-bit columns
     constexpr int cap12 = 12 * 16 * kWfCapPerRow, cap11 = 11 * 16 * kWfCapPerRow, cap10 = 10 * 16 * kWfCapPerRow;
     // (the instantiation must match pl.tr: the tile count above is the host's)
-    if (col16) {
+    if (pl.var == 111 && col16) go(k_wf16<11, cap11, kWfK, 1, 4, 1, true>);
+    else if (pl.var == 111) go(k_wf16<11, cap11, kWfK, 1, 4, 1, false>);
+    else if (col16) {
         if (pl.nc == 12) go(k_wf16<12, cap12, kWfK, kWfNL, 2, 3, true>);
         else if (pl.nc == 11) go(k_wf16<11, cap11, kWfK, kWfNL, 3, 2, true>);
         else go(k_wf16<10, cap10, kWfK, kWfNL, 4, 2, true>);

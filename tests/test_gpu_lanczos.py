@@ -102,10 +102,11 @@ def test_block_b16_wavefront(lz, orc, handle, torch_cuda, monkeypatch, wf, n, np
 
 
 @pytest.mark.parametrize("c16", ["0", "1"])
-@pytest.mark.parametrize("shape", ["10", "11", "12"])
+@pytest.mark.parametrize("shape", ["111", "10", "11", "12"])
 def test_block_b16_wavefront_shapes(lz, orc, handle, torch_cuda, monkeypatch, shape, c16):
-    """Every block shape of the wavefront step (2 loaders + NC consumers + 14 -
-    NC updaters, LZ_WF_SHAPE) with 16- and 32-bit columns."""
+    """Every block shape of the wavefront step (111: 1 loader + 11 consumers + 4
+    updaters; NC: 2 loaders + NC consumers + 14 - NC updaters; LZ_WF_SHAPE)
+    with 16- and 32-bit columns."""
     monkeypatch.setenv("LZ_WF_SHAPE", shape)
     monkeypatch.setenv("LZ_PASS1_C16", c16)
     A = lz.gen_banded(90_001, 10.0, 4096, seed=17)
