@@ -180,6 +180,7 @@ static int block_lanczos_wf16(lz_handle *h, int64_t n, int64_t nnz, const int64_
     (void)nnz;
     double *binv[2] = {h->scratch + 4 * 256, h->scratch + 5 * 256};
     double *P1 = h->scratch + 6 * 256, *P2 = h->scratch + 7 * 256;
+    double *slab = h->scratch + 8 * 256;  // [S1 | S2 | G], 768
     int P = 0;
     LZ_TRY(gram_partials<double>(h, n, 16, B, B, 16, &P));
     LZ_TRY(sqrtm_pair<double>(h, 16, nullptr, P, beta, binv[0], nullptr));
@@ -193,18 +194,20 @@ static int block_lanczos_wf16(lz_handle *h, int64_t n, int64_t nnz, const int64_
         double *Vn = j == 0 ? W : j == 1 ? Q1 : const_cast<double *>(Vm1);
         LZ_TRY(wf_step16(h, n, rp, col, pl.col16, val, pl.pairs, wp, Q0, Vm1, V0, Vn, binv[j & 1], j ? P1 : nullptr,
                          P2, Vn, Q0, j + 1, &P));
-        // beta_{j+1}, its inverse and P1 = beta_j^-1 beta_{j+1} from the G slabs,
-        // then (same launch) alpha_{j+1}, P2 and the row probe from the S1, S2 slabs
+        // the block slabs folded by 12 workgroups (one workgroup reading all
+        // 1.5 MB took ~20 us), then beta_{j+1}, its inverse and P1 = beta_j^-1
+        // beta_{j+1} from G, and (same launch) alpha_{j+1}, P2 and the row probe
+        LZ_TRY(wf_fold16(h, h->partials2, P, nullptr, 0, nullptr, 0, slab));
         WfAlpha wa;
-        wa.part = h->partials2;
-        wa.P = P;
+        wa.part = slab;
+        wa.P = 1;
         wa.alpha = alpha + (j + 1) * bb;
         wa.P2 = P2;
         wa.V = Vn;
         wa.lc = (lc >= 0 && lc < n) ? lc : -1;
         wa.qrow = q + (j + 1) * 16;
-        LZ_TRY(sqrtm_pair<double>(h, 16, nullptr, P, beta + (j + 1) * bb, binv[(j + 1) & 1], nullptr,
-                                  h->partials2 + 2 * (int64_t)P * 256, binv[j & 1], P1, &wa));
+        LZ_TRY(sqrtm_pair<double>(h, 16, nullptr, 1, beta + (j + 1) * bb, binv[(j + 1) & 1], nullptr, slab + 512,
+                                  binv[j & 1], P1, &wa));
         Vm1 = V0;
         V0 = Vn;
     }

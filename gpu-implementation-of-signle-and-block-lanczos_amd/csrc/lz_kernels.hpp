@@ -153,6 +153,7 @@ __device__ __forceinline__ void ws_lds_write(uint32_t a, int v)
     asm volatile("ds_write_b32 %0, %1" ::"v"(a), "v"(v) : "memory");
 }
 
+template <int AUX = 0>
 __device__ __forceinline__ void ws_dma(__amdgpu_buffer_rsrc_t r, void *lds_base, int pieces, int lane)
 {
 #pragma unroll
@@ -160,7 +161,7 @@ __device__ __forceinline__ void ws_dma(__amdgpu_buffer_rsrc_t r, void *lds_base,
         const int piece = 64 * q + lane;
         // pieces past the end get an out-of-range offset (no memory access)
         const uint32_t off = piece < pieces ? 16u * piece : 0x80000000u;
-        __builtin_amdgcn_raw_ptr_buffer_load_lds(r, (ws_lds_t *)((char *)lds_base + 1024 * q), 16, off, 0, 0, 0);
+        __builtin_amdgcn_raw_ptr_buffer_load_lds(r, (ws_lds_t *)((char *)lds_base + 1024 * q), 16, off, 0, 0, AUX);
     }
 }
 

@@ -153,7 +153,7 @@ __global__ __launch_bounds__(64 * (NC + NL + NU)) void k_wf16(
     const double *__restrict__ Vj, double *Vout, const double *__restrict__ binv, const double *__restrict__ P1,
     const double *__restrict__ P2, const double *Vg, double *Yo, const int2 *__restrict__ deps, int *flags, int epoch,
     int64_t hback, int lead, double *__restrict__ part, int *__restrict__ err, int dbg, int64_t nx, int64_t p1a,
-    int64_t p1b, int64_t Th)
+    int64_t p1b, int64_t Th, int cpol)
 {
     using CT = typename std::conditional<C16, int16_t, int32_t>::type;
     using C = FwCfg<NC, CAP, true, true, CT>;
@@ -228,13 +228,18 @@ __global__ __launch_bounds__(64 * (NC + NL + NU)) void k_wf16(
                                                               (int)(cb < 0x7fffffff ? cb : 0x7fffffff), 0x00020000);
             const auto vr = __builtin_amdgcn_make_buffer_rsrc(const_cast<double *>(val + va), (short)0,
                                                               (int)(vb < 0x7fffffff ? vb : 0x7fffffff), 0x00020000);
-            ws_dma(rr, st[s].rp, C::RP_PIECES, lane);
-            ws_dma(cr, st[s].col, C::COL_PIECES, lane);
-            ws_dma(vr, st[s].val, C::VAL_PIECES, lane);
-            {
-                const int64_t s0i = r0 / 16, ns = (n + 15) / 16 + kPairPad;
-                const auto pr = __builtin_amdgcn_make_buffer_rsrc(const_cast<uint64_t *>(pairs + s0i), (short)0,
-                                                                  (int)((ns - s0i) * 8), 0x00020000);
+            const int64_t s0i = r0 / 16, ns = (n + 15) / 16 + kPairPad;
+            const auto pr = __builtin_amdgcn_make_buffer_rsrc(const_cast<uint64_t *>(pairs + s0i), (short)0,
+                                                              (int)((ns - s0i) * 8), 0x00020000);
+            if (cpol & 2) {  // streaming (nt) CSR reads
+                ws_dma<2>(rr, st[s].rp, C::RP_PIECES, lane);
+                ws_dma<2>(cr, st[s].col, C::COL_PIECES, lane);
+                ws_dma<2>(vr, st[s].val, C::VAL_PIECES, lane);
+                ws_dma<2>(pr, st[s].pr, C::PR_PIECES, lane);
+            } else {
+                ws_dma(rr, st[s].rp, C::RP_PIECES, lane);
+                ws_dma(cr, st[s].col, C::COL_PIECES, lane);
+                ws_dma(vr, st[s].val, C::VAL_PIECES, lane);
                 ws_dma(pr, st[s].pr, C::PR_PIECES, lane);
             }
             asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
@@ -337,10 +342,12 @@ __global__ __launch_bounds__(64 * (NC + NL + NU)) void k_wf16(
 #pragma unroll
                 for (int m = 0; m < 3; ++m)
 #pragma unroll
-                    for (int k = 0; k < 2; ++k)
-                        __builtin_amdgcn_raw_ptr_buffer_load_lds(
-                            rs[m], (ws_lds_t *)((char *)&ust[uw][slot][m][0] + 1024 * k), 16,
-                            live ? rb + goff[k] : 0x80000000u, 0, 0, 0);
+                    for (int k = 0; k < 2; ++k) {
+                        ws_lds_t *dst = (ws_lds_t *)((char *)&ust[uw][slot][m][0] + 1024 * k);
+                        const uint32_t off = live ? rb + goff[k] : 0x80000000u;
+                        if (cpol & 1) __builtin_amdgcn_raw_ptr_buffer_load_lds(rs[m], dst, 16, off, 0, 0, 2);
+                        else __builtin_amdgcn_raw_ptr_buffer_load_lds(rs[m], dst, 16, off, 0, 0, 0);
+                    }
             };
             // byte offsets of this lane's slot reads (from the slot base)
             const int ra = c;
@@ -414,7 +421,8 @@ __global__ __launch_bounds__(64 * (NC + NL + NU)) void k_wf16(
                     const double2 v = ev ? make_double2(a0, y) : make_double2(y, a1);
                     const int row = 4 * (2 * h2 + (ev ? 0 : 1)) + g;
                     const uint32_t off = r0b + (uint32_t)(row * 128 + (ev ? c : c - 1) * 8);
-                    __builtin_amdgcn_raw_buffer_store_b128(*reinterpret_cast<const v4u32_t *>(&v), Or, off, 0, SA);
+                    if (cpol & 8) __builtin_amdgcn_raw_buffer_store_b128(*reinterpret_cast<const v4u32_t *>(&v), Or, off, 0, SA | 2);
+                    else __builtin_amdgcn_raw_buffer_store_b128(*reinterpret_cast<const v4u32_t *>(&v), Or, off, 0, SA);
                 }
             }
             asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
@@ -554,10 +562,14 @@ __global__ __launch_bounds__(64 * (NC + NL + NU)) void k_wf16(
         {
             const auto st0 = make_double2(y[0], y[1]), st1 = make_double2(y[2], y[3]);
             const uint32_t oa = (uint32_t)((s0 + ra) * 128) + lane_off, ob = (uint32_t)((s0 + rb) * 128) + lane_off;
-            __builtin_amdgcn_raw_buffer_store_b128(*reinterpret_cast<const v4u32_t *>(&st0), yr,
-                                                   s0 + ra < n ? oa : 0x80000000u, 0, 0);
-            __builtin_amdgcn_raw_buffer_store_b128(*reinterpret_cast<const v4u32_t *>(&st1), yr,
-                                                   s0 + rb < n ? ob : 0x80000000u, 0, 0);
+            const uint32_t fa = s0 + ra < n ? oa : 0x80000000u, fb = s0 + rb < n ? ob : 0x80000000u;
+            if (cpol & 4) {  // streaming (nt) Y stores
+                __builtin_amdgcn_raw_buffer_store_b128(*reinterpret_cast<const v4u32_t *>(&st0), yr, fa, 0, 2);
+                __builtin_amdgcn_raw_buffer_store_b128(*reinterpret_cast<const v4u32_t *>(&st1), yr, fb, 0, 2);
+            } else {
+                __builtin_amdgcn_raw_buffer_store_b128(*reinterpret_cast<const v4u32_t *>(&st0), yr, fa, 0, 0);
+                __builtin_amdgcn_raw_buffer_store_b128(*reinterpret_cast<const v4u32_t *>(&st1), yr, fb, 0, 0);
+            }
         }
         S0[fw_sw(ra, 2 * p)] = y[0];
         S0[fw_sw(ra, 2 * p + 1)] = y[1];
@@ -697,13 +709,19 @@ int wf_step16(lz_handle *h, int64_t n, const int64_t *rp, const int32_t *col, co
     const char *le = getenv("LZ_WF_LEAD");
     // C3 (lmin 4): shape 111 best at 7 (5: 3.07 ms, 6: 1.90, 7: 1.82, 8: 1.84, 10: 1.87);
     // the 2-loader shapes at 8
-    const int lead = std::max(lmin, le ? atoi(le) : lmin + (pl.var == 111 ? 3 : 4));
+    const int lead = std::max(lmin, le ? atoi(le) : lmin + (pl.var ? 3 : 4));
+    // LZ_WF_CPOL: streaming (nt) hints, bit 0 the updaters' reads, bit 1 the CSR
+    // stages, bit 2 the Y stores, bit 3 the V_{j+1} stores.  Default 7: every
+    // stream touched once is nt, so the V_{j+1} rows stay in L2 for the gathers
+    // (C3: 1.74-1.81 -> 1.69-1.70 ms; 8, nt on V_{j+1}, 1.84)
+    const char *cp = getenv("LZ_WF_CPOL");
+    const int cpol = cp ? atoi(cp) : 7;
     const int ev = prof_begin(h, PROF_SPMM_PASS);
     auto go = [&](auto kern) {
         hipLaunchKernelGGL(kern, dim3(grid), dim3(1024), 0, h->stream, n, rp, col, col16, val,
                            pairs, Yj, Vprev, Vj, Vout, binv, P1, P2, Vg, Yo,
                            static_cast<const int2 *>(h->wf_deps), h->wf_flags, epoch, (int64_t)pl.hback, lead,
-                           part, h->err_flag, dbg, nx, p1a, p1b, T);
+                           part, h->err_flag, dbg, nx, p1a, p1b, T, cpol);
     };
     // LDS (<= 160 KB): strip slots per updater DU + 1, fewer with 32-bit columns
     constexpr int cap12 = 12 * 16 * kWfCapPerRow, cap11 = 11 * 16 * kWfCapPerRow, cap10 = 10 * 16 * kWfCapPerRow;
@@ -725,29 +743,29 @@ int wf_step16(lz_handle *h, int64_t n, const int64_t *rp, const int32_t *col, co
     return LZ_OK;
 }
 
-// The distributed wavefront step's three sums (lz_api.hip dist_solve_wf16):
-// out[0, 256) = S1 over the step launch's G slabs, then the boundary launches'
-// G1 and G2; out[256, 512) = S2 and out[512, 768) = G of the step launch.
-// Fixed order: bitwise reproducible.
+// The wavefront step's three sums: out[0, 256) = S1 over the step launch's G
+// slabs (and, distributed, the boundary launches' G1 and G2), out[256, 512) =
+// S2 and out[512, 768) = G of the step launch.  12 blocks, so that no CU pulls
+// more than an eighth of a megabyte (one CU alone reads ~64 B per clock):
+// block (m, r) sums entries [64 r, 64 r + 64) of matrix m; thread (q, i) adds
+// slabs q, q + 16, ... with four independent accumulators, then the 16 partial
+// sums are added in a fixed tree -- bitwise reproducible.
 __global__ __launch_bounds__(1024) void k_wf_fold(const double *__restrict__ kp, int G, const double *__restrict__ b1,
                                                   int G1, const double *__restrict__ b2, int G2,
                                                   double *__restrict__ out)
 {
-    // block m sums matrix m: thread (q, i) adds slabs q, q + 4, ... with four
-    // independent accumulators (loads in flight), then the four partial sums
-    // are added in order q = 0..3 -- a fixed order, bitwise reproducible
-    __shared__ double ps[4][256];
-    const int m = blockIdx.x, q = threadIdx.x >> 8, i = threadIdx.x & 255;
+    __shared__ double ps[16][64];
+    const int m = blockIdx.x >> 2, q = threadIdx.x >> 6, i = (blockIdx.x & 3) * 64 + (threadIdx.x & 63);
     auto sum = [&](const double *p, int P) {
         double a0 = 0.0, a1 = 0.0, a2 = 0.0, a3 = 0.0;
         int g = q;
-        for (; g + 12 < P; g += 16) {
+        for (; g + 48 < P; g += 64) {
             a0 += p[(int64_t)g * 256 + i];
-            a1 += p[(int64_t)(g + 4) * 256 + i];
-            a2 += p[(int64_t)(g + 8) * 256 + i];
-            a3 += p[(int64_t)(g + 12) * 256 + i];
+            a1 += p[(int64_t)(g + 16) * 256 + i];
+            a2 += p[(int64_t)(g + 32) * 256 + i];
+            a3 += p[(int64_t)(g + 48) * 256 + i];
         }
-        for (; g < P; g += 4) a0 += p[(int64_t)g * 256 + i];
+        for (; g < P; g += 16) a0 += p[(int64_t)g * 256 + i];
         return (a0 + a1) + (a2 + a3);
     };
     double s = sum(kp + (int64_t)m * G * 256, G);
@@ -755,15 +773,21 @@ __global__ __launch_bounds__(1024) void k_wf_fold(const double *__restrict__ kp,
         s += sum(b1, G1);
         s += sum(b2, G2);
     }
-    ps[q][i] = s;
+    ps[q][threadIdx.x & 63] = s;
     __syncthreads();
-    if (q == 0) out[m * 256 + i] = (ps[0][i] + ps[1][i]) + (ps[2][i] + ps[3][i]);
+    if (q == 0) {
+        const int l = threadIdx.x & 63;
+        double t[4];
+#pragma unroll
+        for (int k = 0; k < 4; ++k) t[k] = (ps[4 * k][l] + ps[4 * k + 1][l]) + (ps[4 * k + 2][l] + ps[4 * k + 3][l]);
+        out[m * 256 + i] = (t[0] + t[1]) + (t[2] + t[3]);
+    }
 }
 
 int wf_fold16(lz_handle *h, const double *kp, int G, const double *b1, int G1, const double *b2, int G2, double *out)
 {
     const int ev = prof_begin(h, PROF_SMALL);
-    hipLaunchKernelGGL(k_wf_fold, dim3(3), dim3(1024), 0, h->stream, kp, G, b1, G1, b2, G2, out);
+    hipLaunchKernelGGL(k_wf_fold, dim3(12), dim3(1024), 0, h->stream, kp, G, b1, G1, b2, G2, out);
     prof_end(h, ev);
     LZ_LAUNCH_CHECK();
     return LZ_OK;

@@ -43,11 +43,11 @@ static void run(double cond)
     hipMemcpy(dG, G.data(), B * B * 8, hipMemcpyHostToDevice);
     hipEvent_t e0, e1;
     hipEventCreate(&e0); hipEventCreate(&e1);
-    hipLaunchKernelGGL((lzprobe::k_sqrtm_b<double, B>), dim3(1), dim3(1024), 0, 0, dG, nullptr, 0, db, dbi, nullptr, nullptr, nullptr);
+    hipLaunchKernelGGL((lzprobe::k_sqrtm_b<double, B>), dim3(1), dim3(1024), 0, 0, dG, nullptr, 0, db, dbi, nullptr, nullptr, nullptr, lzprobe::WfAlpha{});
     hipEventRecord(e0);
     const int R = 20;
     for (int r = 0; r < R; ++r)
-        hipLaunchKernelGGL((lzprobe::k_sqrtm_b<double, B>), dim3(1), dim3(1024), 0, 0, dG, nullptr, 0, db, dbi, nullptr, nullptr, nullptr);
+        hipLaunchKernelGGL((lzprobe::k_sqrtm_b<double, B>), dim3(1), dim3(1024), 0, 0, dG, nullptr, 0, db, dbi, nullptr, nullptr, nullptr, lzprobe::WfAlpha{});
     hipEventRecord(e1);
     hipEventSynchronize(e1);
     float ms; hipEventElapsedTime(&ms, e0, e1);
@@ -58,8 +58,57 @@ static void run(double cond)
     hipFree(dG); hipFree(db); hipFree(dbi);
 }
 
+// The wavefront step's call (B = 16): G, S1 and S2 from P slabs each, then the
+// alpha products; against the same G from 1 slab and from the matrix itself.
+static void run_wf(int P, bool alpha)
+{
+    constexpr int B = 16;
+    std::mt19937_64 rng(2);
+    std::normal_distribution<double> nd;
+    std::vector<double> part(3 * (size_t)P * 256), X(B * B);
+    for (auto &x : X) x = nd(rng);
+    for (int p = 0; p < P; ++p)
+        for (int i = 0; i < B; ++i)
+            for (int j = 0; j < B; ++j) {
+                double g = 0;
+                for (int k = 0; k < B; ++k) g += X[i * B + k] * X[j * B + k];
+                part[(2 * (size_t)P + p) * 256 + i * B + j] = (g + (i == j ? 1.0 : 0.0)) / P;
+                part[(size_t)p * 256 + i * B + j] = nd(rng) / P;
+                part[((size_t)P + p) * 256 + i * B + j] = nd(rng) / P;
+            }
+    double *dp, *db, *dbi, *dL, *dLB, *da, *dP2, *dV, *dq;
+    hipMalloc(&dp, part.size() * 8);
+    hipMalloc(&db, 2048); hipMalloc(&dbi, 2048); hipMalloc(&dL, 2048); hipMalloc(&dLB, 2048);
+    hipMalloc(&da, 2048); hipMalloc(&dP2, 2048); hipMalloc(&dV, 16 * 128); hipMalloc(&dq, 128);
+    hipMemcpy(dp, part.data(), part.size() * 8, hipMemcpyHostToDevice);
+    hipMemset(dL, 0, 2048); hipMemset(dV, 0, 16 * 128);
+    lzprobe::WfAlpha wa{};
+    if (alpha) {
+        wa.part = dp; wa.P = P; wa.alpha = da; wa.P2 = dP2; wa.V = dV; wa.lc = 3; wa.qrow = dq;
+    }
+    auto go = [&]() {
+        hipLaunchKernelGGL((lzprobe::k_sqrtm_b<double, B>), dim3(1), dim3(1024), 0, 0, nullptr,
+                           dp + 2 * (size_t)P * 256, P, db, dbi, nullptr, dL, dLB, wa);
+    };
+    go();
+    hipEvent_t e0, e1;
+    hipEventCreate(&e0); hipEventCreate(&e1);
+    hipEventRecord(e0);
+    const int R = 20;
+    for (int r = 0; r < R; ++r) go();
+    hipEventRecord(e1);
+    hipEventSynchronize(e1);
+    float ms; hipEventElapsedTime(&ms, e0, e1);
+    long long pr[2];
+    hipMemcpyFromSymbol(pr, HIP_SYMBOL(lzprobe::lz_sqrtm_probe), sizeof(pr));
+    std::printf("wf B=16 P=%d alpha=%d  %.2f us/launch  sweeps=%lld  jacobi_cycles=%lld\n", P, (int)alpha,
+                ms * 1e3 / R, pr[0], pr[1]);
+    hipFree(dp);
+}
+
 int main()
 {
+    for (int P : {1, 256}) { run_wf(P, false); run_wf(P, true); }
     for (double c : {1e2, 1e12}) { run<8>(c); run<16>(c); run<32>(c); }
     // empty-ish launch floor
     return 0;
