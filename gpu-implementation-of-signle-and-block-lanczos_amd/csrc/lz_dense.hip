@@ -199,43 +199,6 @@ __device__ void reduce_slabs(const double *__restrict__ part, int P, int bb, dou
     __syncthreads();
 }
 
-// Three 256-entry sums of P slabs each (the wavefront step's S1, S2 and G) in
-// one pass: thread (q, e) adds slabs q, q + 4, ... of all three with eight
-// loads of each in flight (24 per thread; a slab past P adds 0.0), its eight
-// partial sums in a fixed tree, then the four q in order -- deterministic for
-// a given P.  scratch: 3 x 1024 doubles (LDS); all threads must call it.
-__device__ void reduce_slabs3(const double *__restrict__ p0, const double *__restrict__ p1,
-                              const double *__restrict__ p2, int P, double *o0, double *o1, double *o2,
-                              double *scratch)
-{
-    const int t = threadIdx.x, e = t & 255, q = t >> 8;
-    const double *src[3] = {p0, p1, p2};
-    double a[3][8];
-#pragma unroll
-    for (int m = 0; m < 3; ++m)
-#pragma unroll
-        for (int u = 0; u < 8; ++u) a[m][u] = 0.0;
-    for (int p = q; p < P; p += 32) {
-#pragma unroll
-        for (int u = 0; u < 8; ++u) {
-            const int s = p + 4 * u;
-#pragma unroll
-            for (int m = 0; m < 3; ++m) a[m][u] += s < P ? src[m][(int64_t)s * 256 + e] : 0.0;
-        }
-    }
-#pragma unroll
-    for (int m = 0; m < 3; ++m)
-        scratch[m * 1024 + t] = ((a[m][0] + a[m][1]) + (a[m][2] + a[m][3])) + ((a[m][4] + a[m][5]) + (a[m][6] + a[m][7]));
-    __syncthreads();
-    if (t < 768) {
-        const int m = t >> 8;
-        const double *s = scratch + m * 1024;
-        double *o = m == 0 ? o0 : m == 1 ? o1 : o2;
-        o[e] = (s[e] + s[256 + e]) + (s[512 + e] + s[768 + e]);
-    }
-    __syncthreads();
-}
-
 template <typename T>
 __global__ __launch_bounds__(kRedThreads) void k_gram_finish(int b, const double *__restrict__ part,
                                                              int P, int mode, T *__restrict__ R,
@@ -696,16 +659,8 @@ __global__ __launch_bounds__(kRedThreads) void k_sqrtm_b(const T *__restrict__ G
     // its slabs reduced by the whole block up front, the products at the end
     constexpr int WB = B == 16 ? BB : 1;
     __shared__ double ws1[WB], ws2[WB], wbi[WB], wp1[WB];
-    __shared__ double scr3[B == 16 ? 3 * kRedThreads : 1];
     const bool wfa = B == 16 && wa.part != nullptr;
     const int tid = threadIdx.x;
-    if constexpr (B == 16) {
-        if (wfa && P > 0 && wa.P == P) {
-            // the three sums in one pass (S2 is unused without L, summed anyway)
-            reduce_slabs3(wa.part, wa.part + (int64_t)P * BB, part, P, ws1, ws2, g, scr3);
-            goto reduced;
-        }
-    }
     if (P > 0) {
         reduce_slabs(part, P, BB, g, scratch);
     } else {
@@ -716,7 +671,6 @@ __global__ __launch_bounds__(kRedThreads) void k_sqrtm_b(const T *__restrict__ G
         reduce_slabs(wa.part, wa.P, BB, ws1, scratch);
         if (L) reduce_slabs(wa.part + (int64_t)wa.P * BB, wa.P, BB, ws2, scratch);
     }
-reduced:
     if (tid >= 64) return;  // one wave from here on
     const int j = tid % B, r0 = tid / B;  // column, first row of this lane
     const int jq = B - 1 - j;                      // partner position of j
