@@ -87,12 +87,14 @@ PASS1_MFMA_FLOP_PER_ROW = 16 * 2048 // 16
 PASS2_MFMA_FLOP_PER_ROW = 8 * 2048 // 16
 
 
-def wf_kernel(n, hw):
+def wf_kernel(n, hw, nnz=None):
     """(full name, PMC short name) of the wavefront-step kernel (lz_wf.hip wf_step16):
     <consumers, stage entries, stages, loaders, updaters, strip slots - 1, 16-bit columns>."""
     c16 = col_bytes(n, hw) == 2
     sh = os.environ.get("LZ_WF_SHAPE", "111")
     tf = 'true' if c16 else 'false'
+    if nnz is not None and nnz > 10.2 * n:  # the wide shape (C4's density)
+        return f"k_wf16<10,4400,2,1,{3 if c16 else 2},1,{tf}>", "k_wf16"
     if sh not in ("10", "11", "12"):  # default: 1 loader + 11 consumers + 4 updaters
         return f"k_wf16<11,{11 * 16 * 11},3,1,4,1,{tf}>", "k_wf16"
     nc = int(sh)
@@ -661,7 +663,7 @@ def main():
             # boundary tiles' pass 1 is a launch of its own: same bytes, more launches)
             tot = wf_bytes(n, A.nnz, b, K, cb=cb)
             ach = tot / (spmm_ms * 1e-3) / 1e9
-            kname, kshort = wf_kernel(n, hw)
+            kname, kshort = wf_kernel(n, hw, A.nnz)
             d, tsrc = pmc_record("", kshort, n, A.nnz, hw, kname)
             traffic = None
             if d and d.get("hbm_bytes_first_launch") and spmm_cnt == K:  # the launch mix of bytes_per_launch

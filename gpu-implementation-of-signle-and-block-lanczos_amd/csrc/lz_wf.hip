@@ -12,7 +12,8 @@
 //   Y_{j+1} = A V_{j+1};  S1 = V_{j+1}^T Y_{j+1}              (pass 1, "consumers")
 //   G_{j+1} = V_{j+1}^T V_{j+1};  S2 = V_{j+1}^T V_j          (slabs, updaters)
 //
-// and after the launch (two one-workgroup kernels): beta_{j+1} = sqrtm(G),
+// and after the launch (a 12-workgroup fold of the block slabs, then one
+// one-workgroup kernel): beta_{j+1} = sqrtm(G),
 // P1_{j+1} = beta_j^-1 beta_{j+1}, alpha_{j+1} = sym(beta^-1 (S1 beta^-1 -
 // S2 P1)), P2 = beta^-1 alpha, q = V_{j+1}[lc] beta^-1.  The products are the
 // reference's (methods/block_lanczos.hpp:137-165: W = A Q1 - Q0 beta,
@@ -23,10 +24,9 @@
 // written) against A + 6 n b s for the two passes, and the V_{j+1} rows that
 // pass 1 gathers were written a few hundred rows earlier in the same launch.
 //
-// One 1024-thread block per CU, wave-specialised: NL loaders stage pass-1
-// tiles' CSR runs (k_fused_pp16's ring), NU updaters run pass 2 on a
-// register-prefetched stream of 16-row strips, NC consumers gather and run the
-// S1 epilogue.  Hand-off inside the launch (MI355X_MICROARCH.md, "Valid forms"
+// One block per CU, wave-specialised: NL loaders stage pass-1 tiles' CSR runs
+// (k_fused_pp16's ring), NU updaters run pass 2 on 16-row strips streamed
+// into LDS slots by LDS-DMA, NC consumers gather and run the S1 epilogue.  Hand-off inside the launch (MI355X_MICROARCH.md, "Valid forms"
 // table, first row): updaters store V_{j+1} write-through (16-B sc1 stores),
 // drain (counted s_waitcnt vmcnt) and publish a per-tile flag with an sc1
 // store; a loader polls the flags of every pass-2 tile its pass-1 tile reads
@@ -49,7 +49,17 @@ namespace lz {
 // (scripts/ab_c3.py); one loader wave keeps up with 11 consumers.
 constexpr int kWfK = 3, kWfNL = 2;
 constexpr int kWfCapPerRow = 11;  // stage entries per row (C3: 10 +- 2.2 nnz per row)
-constexpr int kWfMaxSpan = 256;     // pass-2 tiles one pass-1 tile may read (flag polls per tile)
+// the wide shape (rows of up to ~27 entries on average, C4's density): 1 loader
+// + 10 consumers + 2 (32-bit columns) or 3 (16-bit) updaters, two stages of
+// 4400 entries (k_fused_pp16's wide stage).  At C4's per-rank share (n = 5M,
+// 25 per row, half width 65,536) 2.52-2.55 ms per step against 2.67 for the
+// two passes: the launch takes pass 1 + pass 2 (2.37-2.40 against 2.08 +
+// 0.35), the gain is the kernels it replaces.  Its gathers miss L2 (a 16 MB
+// window per XCD) and share the fabric with the updaters' streams; 2 loaders,
+// or 9 consumers + 3 updaters, measured the same.
+constexpr int kWfWideCap = 4400;
+constexpr double kWfWideRow = 27.0;
+constexpr int kWfMaxSpan = 1024;    // pass-2 tiles one pass-1 tile may read (flag polls per tile)
 constexpr int kWfAux = 16;          // buffer-instruction cache policy: sc1
 constexpr long kWfSpin = 1L << 21;  // flag polls per tile before the loader gives up (about 2 s)
 
@@ -178,7 +188,9 @@ __global__ __launch_bounds__(64 * (NC + NL + NU)) void k_wf16(
     }
     __syncthreads();  // the only block barrier
     const int64_t T = ceil_div(n, (int64_t)TR);
-    if (T != Th) {  // the host planned other tiles (flags, ranges): refuse loudly
+    if (T != Th || blockDim.x != 64 * (NC + NL + NU)) {
+        // the host planned other tiles (flags, ranges) or launched another
+        // block shape (waves past the roles would index past the tile): refuse loudly
         if (threadIdx.x == 0) *err = 7;
         return;
     }
@@ -621,15 +633,17 @@ int wf_plan16(lz_handle *h, int64_t n, int64_t nnz, const int64_t *rp, const int
     pl->col16 = nullptr;
     const char *e = getenv("LZ_PASS_WF");  // "0": the two-pass step (A/B); read per call
     // rows of about 11 entries or fewer on average: the tile's CSR run fits the
-    // kWfCapPerRow-entry-per-row stage (longer runs take a slow global-gather path)
+    // kWfCapPerRow-entry-per-row stage; up to kWfWideRow: the wide shape (longer
+    // runs take a slow global-gather path)
     const char *sh = getenv("LZ_WF_SHAPE");  // consumers per block (A/B); read per call
     const int want = sh ? atoi(sh) : 111;
     // 111 (default): 1 loader, 11 consumers, 4 updaters; 10 / 11 / 12: 2
     // loaders, NC consumers, 14 - NC updaters
-    pl->var = (want == 10 || want == 11 || want == 12) ? 0 : 111;
-    pl->nc = pl->var ? 11 : want;
+    const bool wide = (double)nnz > 10.2 * (double)n;
+    pl->var = wide ? 200 : (want == 10 || want == 11 || want == 12) ? 0 : 111;
+    pl->nc = pl->var == 200 ? 10 : pl->var ? 11 : want;
     pl->tr = 16 * pl->nc;
-    if ((e && e[0] == '0') || n < pl->tr || nx >= (1 << 24) || (double)nnz > 10.2 * (double)n) return LZ_OK;
+    if ((e && e[0] == '0') || n < pl->tr || nx >= (1 << 24) || (double)nnz > kWfWideRow * (double)n) return LZ_OK;
     const int64_t T = ceil_div(n, (int64_t)pl->tr);
     if ((size_t)T + 64 > h->wf_cap) {
         LZ_HIP_TRY(hipStreamSynchronize(h->stream));
@@ -709,7 +723,7 @@ int wf_step16(lz_handle *h, int64_t n, const int64_t *rp, const int32_t *col, co
     const char *le = getenv("LZ_WF_LEAD");
     // C3 (lmin 4): shape 111 best at 7 (5: 3.07 ms, 6: 1.90, 7: 1.82, 8: 1.84, 10: 1.87);
     // the 2-loader shapes at 8
-    const int lead = std::max(lmin, le ? atoi(le) : lmin + (pl.var ? 3 : 4));
+    const int lead = std::max(lmin, le ? atoi(le) : lmin + (pl.var ? 3 : 4));  // (wide: to be tuned)
     // LZ_WF_CPOL: streaming (nt) hints, bit 0 the updaters' reads, bit 1 the CSR
     // stages, bit 2 the Y stores, bit 3 the V_{j+1} stores.  Default 7: every
     // stream touched once is nt, so the V_{j+1} rows stay in L2 for the gathers
@@ -717,8 +731,9 @@ int wf_step16(lz_handle *h, int64_t n, const int64_t *rp, const int32_t *col, co
     const char *cp = getenv("LZ_WF_CPOL");
     const int cpol = cp ? atoi(cp) : 7;
     const int ev = prof_begin(h, PROF_SPMM_PASS);
-    auto go = [&](auto kern) {
-        hipLaunchKernelGGL(kern, dim3(grid), dim3(1024), 0, h->stream, n, rp, col, col16, val,
+    // (the block is 64 (NC + NL + NU) threads: the kernel refuses any other size)
+    auto go = [&](auto kern, int waves) {
+        hipLaunchKernelGGL(kern, dim3(grid), dim3(64 * waves), 0, h->stream, n, rp, col, col16, val,
                            pairs, Yj, Vprev, Vj, Vout, binv, P1, P2, Vg, Yo,
                            static_cast<const int2 *>(h->wf_deps), h->wf_flags, epoch, (int64_t)pl.hback, lead,
                            part, h->err_flag, dbg, nx, p1a, p1b, T, cpol);
@@ -726,16 +741,18 @@ int wf_step16(lz_handle *h, int64_t n, const int64_t *rp, const int32_t *col, co
     // LDS (<= 160 KB): strip slots per updater DU + 1, fewer with 32-bit columns
     constexpr int cap12 = 12 * 16 * kWfCapPerRow, cap11 = 11 * 16 * kWfCapPerRow, cap10 = 10 * 16 * kWfCapPerRow;
     // (the instantiation must match pl.tr: the tile count above is the host's)
-    if (pl.var == 111 && col16) go(k_wf16<11, cap11, kWfK, 1, 4, 1, true>);
-    else if (pl.var == 111) go(k_wf16<11, cap11, kWfK, 1, 4, 1, false>);
+    if (pl.var == 200 && col16) go(k_wf16<10, kWfWideCap, 2, 1, 3, 1, true>, 10 + 1 + 3);
+    else if (pl.var == 200) go(k_wf16<10, kWfWideCap, 2, 1, 2, 1, false>, 10 + 1 + 2);
+    else if (pl.var == 111 && col16) go(k_wf16<11, cap11, kWfK, 1, 4, 1, true>, 11 + 1 + 4);
+    else if (pl.var == 111) go(k_wf16<11, cap11, kWfK, 1, 4, 1, false>, 11 + 1 + 4);
     else if (col16) {
-        if (pl.nc == 12) go(k_wf16<12, cap12, kWfK, kWfNL, 2, 3, true>);
-        else if (pl.nc == 11) go(k_wf16<11, cap11, kWfK, kWfNL, 3, 2, true>);
-        else go(k_wf16<10, cap10, kWfK, kWfNL, 4, 2, true>);
+        if (pl.nc == 12) go(k_wf16<12, cap12, kWfK, kWfNL, 2, 3, true>, 12 + kWfNL + 2);
+        else if (pl.nc == 11) go(k_wf16<11, cap11, kWfK, kWfNL, 3, 2, true>, 11 + kWfNL + 3);
+        else go(k_wf16<10, cap10, kWfK, kWfNL, 4, 2, true>, 10 + kWfNL + 4);
     } else {
-        if (pl.nc == 12) go(k_wf16<12, cap12, kWfK, kWfNL, 2, 2, false>);
-        else if (pl.nc == 11) go(k_wf16<11, cap11, kWfK, kWfNL, 3, 2, false>);
-        else go(k_wf16<10, cap10, kWfK, kWfNL, 4, 1, false>);
+        if (pl.nc == 12) go(k_wf16<12, cap12, kWfK, kWfNL, 2, 2, false>, 12 + kWfNL + 2);
+        else if (pl.nc == 11) go(k_wf16<11, cap11, kWfK, kWfNL, 3, 2, false>, 11 + kWfNL + 3);
+        else go(k_wf16<10, cap10, kWfK, kWfNL, 4, 1, false>, 10 + kWfNL + 4);
     }
     prof_end(h, ev);
     LZ_LAUNCH_CHECK();

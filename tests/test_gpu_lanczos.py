@@ -90,8 +90,8 @@ def test_block_b16_wavefront(lz, orc, handle, torch_cuda, monkeypatch, wf, n, np
     """The wavefront step (lz_wf.hip, LZ_PASS_WF default on) and the two-pass
     step against the oracle: fewer pass-1 tiles than XCD regions (n = 1000: 6
     tiles), a partial last tile, bands of 1-2 tiles up to ~85 (the pass-2
-    wavefront leads by the widest), and half width 40,000 (32-bit columns and
-    a column span past the wavefront's limit: the two-pass step runs)."""
+    wavefront leads by the widest), and half width 40,000 (32-bit columns, a
+    tile reaching ~455 tiles)."""
     monkeypatch.setenv("LZ_PASS_WF", wf)
     A = lz.gen_banded(n, npr, hw, seed=n % 97)
     B = lz.uniform_B(A.n, 16, seed=5)
@@ -114,6 +114,35 @@ def test_block_b16_wavefront_shapes(lz, orc, handle, torch_cuda, monkeypatch, sh
     m, lc = 8, 70_000
     got = gpu_block(lz, handle, torch_cuda, A, B, m, lc)
     assert handle.device_error() == 0
+    assert_close_run(lz, m, 16, got, orc.block_lanczos(A, B, m, lc))
+
+
+def _update_launches(lz, handle, torch, Ad, Bd, m, lc):
+    """(result, update-pass launches) of one solve: the wavefront step has none."""
+    handle.prof_enable(True)
+    q, al, be = lz.run_block_lanczos(handle, Ad, Bd, m, lc)
+    torch.cuda.synchronize()
+    _, c2 = handle.prof_read(handle.PROF_UPDATE_PASS)
+    handle.prof_enable(False)
+    return (q.cpu().numpy(), al.cpu().numpy(), be.cpu().numpy()), c2
+
+
+@pytest.mark.parametrize("c16", ["0", "1"])
+@pytest.mark.parametrize("n,npr,hw", [(40_009, 25.0, 2048), (300_007, 25.0, 20_000), (150_001, 26.5, 65_536),
+                                      (20_011, 30.0, 1024)])
+def test_block_b16_wavefront_wide(lz, orc, handle, torch_cuda, monkeypatch, c16, n, npr, hw):
+    """The wide wavefront shape (rows of 10.2-27 entries on average, config C4's
+    density: 10 consumers, two 4400-entry stages) against the oracle, with 16-
+    and 32-bit columns; half width 65,536 reaches ~820 tiles (C4's band); 30
+    entries per row is past the wide stage: the two-pass step runs."""
+    monkeypatch.setenv("LZ_PASS1_C16", c16)
+    A = lz.gen_banded(n, npr, hw, seed=n % 89)
+    B = lz.uniform_B(A.n, 16, seed=4)
+    m, lc = 7, n // 2
+    got, upd = _update_launches(lz, handle, torch_cuda, lz.CsrDevice.from_host(A),
+                                torch_cuda.from_numpy(B).cuda(), m, lc)
+    assert handle.device_error() == 0
+    assert (upd == 0) == (A.nnz <= 27.0 * n), (upd, A.nnz / n)
     assert_close_run(lz, m, 16, got, orc.block_lanczos(A, B, m, lc))
 
 

@@ -126,6 +126,17 @@ def test_vranks_b16_halo_step_forms(lz, orc, torch_cuda, monkeypatch, wf, nranks
     assert_close_run(lz, m, 16, got, orc.block_lanczos(A, B, m, lc))
 
 
+@pytest.mark.parametrize("nranks", [2, 4])
+def test_vranks_b16_halo_wide_rows(lz, orc, torch_cuda, nranks):
+    """Config C4's density (25 entries per row) on the halo form: each rank runs
+    the wavefront step's wide shape (two 4400-entry stages)."""
+    A = lz.gen_banded(120_011, 25.0, 6000, seed=50 + nranks)
+    B = lz.uniform_B(A.n, 16, seed=6)
+    m, lc = 7, 1_234
+    got, _ = run_dist(lz, torch_cuda, A, B, m, lc, nranks, "halo")
+    assert_close_run(lz, m, 16, got, orc.block_lanczos(A, B, m, lc))
+
+
 @pytest.mark.parametrize("form", ["halo", "allgather"])
 def test_vranks_b16_overlap_off_equals_on(lz, orc, torch_cuda, form):
     """LZ_DIST_OVERLAP=0 (exchange, then the whole pass) against the split run:
