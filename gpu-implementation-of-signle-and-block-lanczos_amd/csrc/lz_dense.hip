@@ -20,6 +20,7 @@
 #include "lz_common.hpp"
 #include "lz_internal.hpp"
 #include "lz_kernels.hpp"
+#include "lz_sqrtm.hpp"
 
 namespace lz {
 
@@ -619,26 +620,6 @@ __global__ __launch_bounds__(kRedThreads) void k_sqrtm(int b, const T *__restric
 __device__ long long lz_sqrtm_probe[2];  // sweeps, Jacobi clock cycles (scripts/probe)
 #endif
 
-// Jacobi rotation for the pair (p, q): c, s with R[p][p] = R[q][q] = c,
-// R[p][q] = -s, R[q][p] = s annihilating a_pq (Numerical Recipes' t with
-// tau = (a_qq - a_pp) / 2 a_pq, rewritten without the tau division).
-__device__ __forceinline__ void jacobi_rot(double app, double aqq, double apq, double &c, double &s)
-{
-#pragma clang fp contract(off)
-    constexpr double kTol2 = 2.220446049250313e-16 * 2.220446049250313e-16;
-    c = 1.0;
-    s = 0.0;
-    if (apq != 0.0 && apq * apq > kTol2 * (fabs(app) * fabs(aqq))) {
-        const double d = aqq - app, a2 = 2.0 * apq;
-        const double t = (d >= 0.0 ? a2 : -a2) / (fabs(d) + sqrt(d * d + a2 * a2));
-        const double x = 1.0 + t * t;
-        double y = __builtin_amdgcn_rsq(x);
-        y = y * (1.5 - 0.5 * x * y * y);
-        c = y;
-        s = t * y;
-    }
-}
-
 template <typename T, int B>
 __global__ __launch_bounds__(kRedThreads) void k_sqrtm_b(const T *__restrict__ Gin,
                                                          const double *__restrict__ part, int P,
@@ -689,107 +670,11 @@ __global__ __launch_bounds__(kRedThreads) void k_sqrtm_b(const T *__restrict__ G
     int nsw = 0;
 #endif
     if constexpr (B == 16 || B == 32) {
-        // Register-resident form.  The NPB = B/2 pairs (p, B-1-p) cut A into
-        // NPB x NPB 2x2 pair-blocks; lane L owns QS = NPB^2/64 of them: position
-        // rows {P, B-1-P} x columns {Q_t, B-1-Q_t}, t < QS (P = L / LPP,
-        // Q_t = (L % LPP) QS + t, LPP = NPB / QS lanes per row pair), and the
-        // same rows x index columns of U.  Per round: the lanes holding a
-        // diagonal block form that pair's rotation, every lane fetches its row
-        // and column rotations by lane shuffles and updates its blocks in
-        // registers (same products, same order as the LDS form, so A stays
-        // bit-symmetric); the circle move is one scatter to the LDS copy (moved
-        // positions) and one gather back -- no LDS round trip for the rotation
-        // parameters and about half the LDS accesses of the LDS form.
-        constexpr int NPB = B / 2, QS = NPB * NPB / 64, LPP = NPB / QS;
-        const int P = tid / LPP, Q0 = (tid % LPP) * QS;
-        auto owner = [](int p) { return p * LPP + p / QS; };  // lane holding pair p's diagonal block
-        auto mv = [](int x) { return x == 0 ? 0 : (x == 1 ? B - 1 : x - 1); };
-        const int X[2] = {P, B - 1 - P}, XM[2] = {mv(X[0]), mv(X[1])};
-        int Y[QS][2], YM[QS][2];
-#pragma unroll
-        for (int t = 0; t < QS; ++t) {
-            Y[t][0] = Q0 + t;
-            Y[t][1] = B - 1 - (Q0 + t);
-            YM[t][0] = mv(Y[t][0]);
-            YM[t][1] = mv(Y[t][1]);
-        }
-        const bool has_diag = (tid % LPP) == P / QS;  // slot P % QS holds block (P, P)
-        double a[QS][2][2], u[QS][2][2];
-#pragma unroll
-        for (int t = 0; t < QS; ++t)
-#pragma unroll
-            for (int ii = 0; ii < 2; ++ii)
-#pragma unroll
-                for (int jj = 0; jj < 2; ++jj) {
-                    a[t][ii][jj] = Am[X[ii] * LD + Y[t][jj]];
-                    u[t][ii][jj] = Um[X[ii] * LD + Y[t][jj]];
-                }
-        for (int sweep = 0; sweep < 60; ++sweep) {
 #ifdef LZ_SQRTM_PROBE
-            nsw = sweep;
+        nsw = jacobi_rr<B>(Am, Um, tid);
+#else
+        (void)jacobi_rr<B>(Am, Um, tid);
 #endif
-            bool need = false;  // the LDS copy holds this sweep's matrix in index order
-#pragma unroll
-            for (int t = 0; t < QS; ++t)
-#pragma unroll
-                for (int ii = 0; ii < 2; ++ii)
-#pragma unroll
-                    for (int jj = 0; jj < 2; ++jj) {
-                        const int x = X[ii], y = Y[t][jj];
-                        const double aij = a[t][ii][jj];
-                        if (x != y && aij != 0.0 &&
-                            aij * aij > kTol2 * (fabs(Am[x * LD + x]) * fabs(Am[y * LD + y])))
-                            need = true;
-                    }
-            if (__ballot(need) == 0) break;  // wave-uniform
-#pragma unroll 1
-            for (int rnd = 0; rnd < B - 1; ++rnd) {
-                double c = 1.0, sn = 0.0;
-                if (has_diag) {
-                    double d00 = a[0][0][0], d11 = a[0][1][1], d01 = a[0][0][1];
-#pragma unroll
-                    for (int t = 1; t < QS; ++t)
-                        if (P % QS == t) {
-                            d00 = a[t][0][0];
-                            d11 = a[t][1][1];
-                            d01 = a[t][0][1];
-                        }
-                    jacobi_rot(d00, d11, d01, c, sn);
-                }
-                const double cP = __shfl(c, owner(P), 64), sP = __shfl(sn, owner(P), 64);
-                // R[x0][x0] = R[x1][x1] = c, R[x0][x1] = -s, R[x1][x0] = s
-                const double ci[2] = {cP, cP}, si[2] = {-sP, sP};
-#pragma unroll
-                for (int t = 0; t < QS; ++t) {
-                    const int Qt = Q0 + t;
-                    const double cQ = __shfl(c, owner(Qt), 64), sQ = __shfl(sn, owner(Qt), 64);
-                    const double cj[2] = {cQ, cQ}, sj[2] = {-sQ, sQ};
-#pragma unroll
-                    for (int ii = 0; ii < 2; ++ii)
-#pragma unroll
-                        for (int jj = 0; jj < 2; ++jj) {
-                            const double x1 = a[t][ii][jj] * (ci[ii] * cj[jj]);
-                            const double x2 = a[t][ii][1 - jj] * (ci[ii] * sj[jj]);
-                            const double x3 = a[t][1 - ii][jj] * (si[ii] * cj[jj]);
-                            const double x4 = a[t][1 - ii][1 - jj] * (si[ii] * sj[jj]);
-                            const bool ann = (P == Qt) && (ii != jj) && sP != 0.0;  // the annihilated pair
-                            Am[XM[ii] * LD + YM[t][jj]] = ann ? 0.0 : (x1 + x4) + (x2 + x3);
-                            Um[XM[ii] * LD + Y[t][jj]] = u[t][ii][jj] * ci[ii] + u[t][1 - ii][jj] * si[ii];
-                        }
-                }
-                wave_lds_sync();
-#pragma unroll
-                for (int t = 0; t < QS; ++t)
-#pragma unroll
-                    for (int ii = 0; ii < 2; ++ii)
-#pragma unroll
-                        for (int jj = 0; jj < 2; ++jj) {
-                            a[t][ii][jj] = Am[X[ii] * LD + Y[t][jj]];
-                            u[t][ii][jj] = Um[X[ii] * LD + Y[t][jj]];
-                        }
-                wave_lds_sync();
-            }
-        }
         (void)An;
         (void)Un;
         (void)jn;
@@ -861,42 +746,7 @@ __global__ __launch_bounds__(kRedThreads) void k_sqrtm_b(const T *__restrict__ G
         lz_sqrtm_probe[1] = clock64() - t0;
     }
 #endif
-    // beta = V f(L) V^T with V[i][k] = U[k][i]; f(L) tabulated once
-    if (tid < B) {
-        const double sq = sqrt(fabs(Am[tid * LD + tid]));
-        cc[tid] = sq;
-        ss[tid] = 1.0 / sq;
-    }
-    wave_lds_sync();
-#pragma unroll 1
-    for (int k = 0; k < NE; ++k) {
-        const int i = r0 + RS * k;
-        double s1 = 0.0, s2 = 0.0;
-#pragma unroll 4
-        for (int kk = 0; kk < B; ++kk) {
-            const double vv = Um[kk * LD + i] * Um[kk * LD + j];
-            s1 += vv * cc[kk];
-            s2 += vv * ss[kk];
-        }
-        if (beta) beta[i * B + j] = (T)s1;
-        if (binv) binv[i * B + j] = (T)s2;
-        if (L) g[i * B + j] = s1;  // g (the Gram) is dead: park beta for LB
-        if constexpr (B == 16)
-            if (wfa) wbi[i * B + j] = (double)(T)s2;
-    }
-    if (L) {  // LB = L * beta (the Q-free iteration's P1 = beta_{j-1}^-1 beta_j)
-        wave_lds_sync();
-#pragma unroll 1
-        for (int k = 0; k < NE; ++k) {
-            const int i = r0 + RS * k;
-            double s = 0.0;
-#pragma unroll 4
-            for (int kk = 0; kk < B; ++kk) s = fma((double)L[i * B + kk], g[kk * B + j], s);
-            LB[i * B + j] = (T)s;
-            if constexpr (B == 16)
-                if (wfa) wp1[i * B + j] = (double)(T)s;
-        }
-    }
+    sqrtm_tail<T, B>(Am, Um, cc, ss, g, beta, binv, L, LB, wfa ? wbi : nullptr, wfa ? wp1 : nullptr, tid);
     if constexpr (B == 16) {
         if (wfa) {  // k_alpha_wf16's products, same order (one wave)
             wave_lds_sync();

@@ -1,0 +1,219 @@
+// lz_sqrtm.hpp -- the wave-level pieces of the b x b symmetric square root
+// (beta = sqrtm(G), beta^-1), shared by k_sqrtm_b (lz_dense.hip) and the
+// wavefront step's sqrtm block (lz_wf.hip) so both produce the same bits.
+// The reference's sqrtm: kernels/my_sqrtm_cusolver.hpp (syevj, then
+// V f(L) V^T).  One wave (lanes tid < 64) runs each function; Am, Um are
+// B x (B + 1) LDS matrices, cc / ss B-entry LDS vectors.
+#pragma once
+
+#include "lz_kernels.hpp"
+
+namespace lz {
+
+
+// Jacobi rotation for the pair (p, q): c, s with R[p][p] = R[q][q] = c,
+// R[p][q] = -s, R[q][p] = s annihilating a_pq -- Numerical Recipes' angle
+// (t = tan(theta) = sgn(d) a2 / (|d| + r), d = a_qq - a_pp, a2 = 2 a_pq,
+// r = hypot(d, a2)) through the half-angle forms, which need no division and
+// no square root: with cos(2 theta) = |d| / r, c^2 = u = (1 + |d| / r) / 2
+// and s = sin(2 theta) / (2 c) = sgn(d) a2 / (2 r c).  Two reciprocal square
+// roots (v_rsq_f64 and one Newton step each) replace the division, the sqrt
+// and the rsq of the direct form: the round's dependent chain is ~40 % shorter
+// (the sqrtm sits on the step's critical path).
+__device__ __forceinline__ void jacobi_rot(double app, double aqq, double apq, double &c, double &s)
+{
+#pragma clang fp contract(off)
+    constexpr double kTol2 = 2.220446049250313e-16 * 2.220446049250313e-16;
+    c = 1.0;
+    s = 0.0;
+    if (apq != 0.0 && apq * apq > kTol2 * (fabs(app) * fabs(aqq))) {
+        const double d = aqq - app, a2 = 2.0 * apq;
+        const double r2 = d * d + a2 * a2;
+        double ir = __builtin_amdgcn_rsq(r2);
+        ir = ir * (1.5 - 0.5 * r2 * ir * ir);  // 1 / r
+        const double u = 0.5 + 0.5 * (fabs(d) * ir);
+        double iu = __builtin_amdgcn_rsq(u);
+        iu = iu * (1.5 - 0.5 * u * iu * iu);  // 1 / c
+        c = u * iu;
+        s = (0.5 * (d >= 0.0 ? a2 : -a2)) * (ir * iu);
+    }
+}
+
+// A = the symmetric G (from its lower triangle, as syevj with
+// CUBLAS_FILL_MODE_LOWER), U = I; lane t owns entries (t / B + (64 / B) k, t % B)
+template <int B>
+__device__ __forceinline__ void sqrtm_init(const double *g, double *Am, double *Um, int tid)
+{
+    constexpr int LD = B + 1, NE = B * B / 64, RS = 64 / B;
+    const int j = tid % B, r0 = tid / B;
+#pragma unroll
+    for (int k = 0; k < NE; ++k) {
+        const int i = r0 + RS * k;
+        Am[i * LD + j] = (i < j) ? g[j * B + i] : g[i * B + j];
+        Um[i * LD + j] = (i == j) ? 1.0 : 0.0;
+    }
+    wave_lds_sync();
+}
+
+// The round-robin (circle method) parallel cyclic Jacobi of k_sqrtm_b (see
+// there), register-resident form for B = 16, 32: on return Am's diagonal
+// holds the eigenvalues and Um = V^T (LDS copies in index order).  Returns
+// the sweeps run.
+template <int B>
+__device__ int jacobi_rr(double *Am, double *Um, int tid)
+{
+#pragma clang fp contract(off)
+    static_assert(B == 16 || B == 32, "register-resident Jacobi: B in {16, 32}");
+    constexpr int LD = B + 1;
+    constexpr double kTol2 = 2.220446049250313e-16 * 2.220446049250313e-16;
+    int nsw = 0;
+    // Register-resident form.  The NPB = B/2 pairs (p, B-1-p) cut A into
+    // NPB x NPB 2x2 pair-blocks; lane L owns QS = NPB^2/64 of them: position
+    // rows {P, B-1-P} x columns {Q_t, B-1-Q_t}, t < QS (P = L / LPP,
+    // Q_t = (L % LPP) QS + t, LPP = NPB / QS lanes per row pair), and the
+    // same rows x index columns of U.  Per round: the lanes holding a
+    // diagonal block form that pair's rotation, every lane fetches its row
+    // and column rotations by lane shuffles and updates its blocks in
+    // registers (same products, same order as the LDS form, so A stays
+    // bit-symmetric); the circle move is one scatter to the LDS copy (moved
+    // positions) and one gather back -- no LDS round trip for the rotation
+    // parameters and about half the LDS accesses of the LDS form.
+    constexpr int NPB = B / 2, QS = NPB * NPB / 64, LPP = NPB / QS;
+    const int P = tid / LPP, Q0 = (tid % LPP) * QS;
+    auto owner = [](int p) { return p * LPP + p / QS; };  // lane holding pair p's diagonal block
+    auto mv = [](int x) { return x == 0 ? 0 : (x == 1 ? B - 1 : x - 1); };
+    const int X[2] = {P, B - 1 - P}, XM[2] = {mv(X[0]), mv(X[1])};
+    int Y[QS][2], YM[QS][2];
+#pragma unroll
+    for (int t = 0; t < QS; ++t) {
+        Y[t][0] = Q0 + t;
+        Y[t][1] = B - 1 - (Q0 + t);
+        YM[t][0] = mv(Y[t][0]);
+        YM[t][1] = mv(Y[t][1]);
+    }
+    const bool has_diag = (tid % LPP) == P / QS;  // slot P % QS holds block (P, P)
+    double a[QS][2][2], u[QS][2][2];
+#pragma unroll
+    for (int t = 0; t < QS; ++t)
+#pragma unroll
+        for (int ii = 0; ii < 2; ++ii)
+#pragma unroll
+            for (int jj = 0; jj < 2; ++jj) {
+                a[t][ii][jj] = Am[X[ii] * LD + Y[t][jj]];
+                u[t][ii][jj] = Um[X[ii] * LD + Y[t][jj]];
+            }
+    for (int sweep = 0; sweep < 60; ++sweep) {
+        nsw = sweep;
+        bool need = false;  // the LDS copy holds this sweep's matrix in index order
+#pragma unroll
+        for (int t = 0; t < QS; ++t)
+#pragma unroll
+            for (int ii = 0; ii < 2; ++ii)
+#pragma unroll
+                for (int jj = 0; jj < 2; ++jj) {
+                    const int x = X[ii], y = Y[t][jj];
+                    const double aij = a[t][ii][jj];
+                    if (x != y && aij != 0.0 &&
+                        aij * aij > kTol2 * (fabs(Am[x * LD + x]) * fabs(Am[y * LD + y])))
+                        need = true;
+                }
+        if (__ballot(need) == 0) break;  // wave-uniform
+#pragma unroll 1
+        for (int rnd = 0; rnd < B - 1; ++rnd) {
+            double c = 1.0, sn = 0.0;
+            if (has_diag) {
+                double d00 = a[0][0][0], d11 = a[0][1][1], d01 = a[0][0][1];
+#pragma unroll
+                for (int t = 1; t < QS; ++t)
+                    if (P % QS == t) {
+                        d00 = a[t][0][0];
+                        d11 = a[t][1][1];
+                        d01 = a[t][0][1];
+                    }
+                jacobi_rot(d00, d11, d01, c, sn);
+            }
+            const double cP = __shfl(c, owner(P), 64), sP = __shfl(sn, owner(P), 64);
+            // R[x0][x0] = R[x1][x1] = c, R[x0][x1] = -s, R[x1][x0] = s
+            const double ci[2] = {cP, cP}, si[2] = {-sP, sP};
+#pragma unroll
+            for (int t = 0; t < QS; ++t) {
+                const int Qt = Q0 + t;
+                const double cQ = __shfl(c, owner(Qt), 64), sQ = __shfl(sn, owner(Qt), 64);
+                const double cj[2] = {cQ, cQ}, sj[2] = {-sQ, sQ};
+#pragma unroll
+                for (int ii = 0; ii < 2; ++ii)
+#pragma unroll
+                    for (int jj = 0; jj < 2; ++jj) {
+                        const double x1 = a[t][ii][jj] * (ci[ii] * cj[jj]);
+                        const double x2 = a[t][ii][1 - jj] * (ci[ii] * sj[jj]);
+                        const double x3 = a[t][1 - ii][jj] * (si[ii] * cj[jj]);
+                        const double x4 = a[t][1 - ii][1 - jj] * (si[ii] * sj[jj]);
+                        const bool ann = (P == Qt) && (ii != jj) && sP != 0.0;  // the annihilated pair
+                        Am[XM[ii] * LD + YM[t][jj]] = ann ? 0.0 : (x1 + x4) + (x2 + x3);
+                        Um[XM[ii] * LD + Y[t][jj]] = u[t][ii][jj] * ci[ii] + u[t][1 - ii][jj] * si[ii];
+                    }
+            }
+            wave_lds_sync();
+#pragma unroll
+            for (int t = 0; t < QS; ++t)
+#pragma unroll
+                for (int ii = 0; ii < 2; ++ii)
+#pragma unroll
+                    for (int jj = 0; jj < 2; ++jj) {
+                        a[t][ii][jj] = Am[X[ii] * LD + Y[t][jj]];
+                        u[t][ii][jj] = Um[X[ii] * LD + Y[t][jj]];
+                    }
+            wave_lds_sync();
+        }
+    }
+    return nsw;
+}
+
+// beta = V f(L) V^T (f = sqrt |.|) and beta^-1 (f = 1 / sqrt |.|) from the
+// Jacobi result, V[i][k] = U[k][i], f(L) tabulated once in cc / ss; L != null:
+// LB = L * beta (g, the Gram, is dead and parks beta).  wbi / wp1 (optional,
+// LDS): beta^-1 and LB as the stored type rounds them.
+template <typename T, int B>
+__device__ void sqrtm_tail(const double *Am, const double *Um, double *cc, double *ss, double *g, T *beta, T *binv,
+                           const T *L, T *LB, double *wbi, double *wp1, int tid)
+{
+#pragma clang fp contract(off)
+    constexpr int LD = B + 1, NE = B * B / 64, RS = 64 / B;
+    const int j = tid % B, r0 = tid / B;
+    // beta = V f(L) V^T with V[i][k] = U[k][i]; f(L) tabulated once
+    if (tid < B) {
+        const double sq = sqrt(fabs(Am[tid * LD + tid]));
+        cc[tid] = sq;
+        ss[tid] = 1.0 / sq;
+    }
+    wave_lds_sync();
+#pragma unroll 1
+    for (int k = 0; k < NE; ++k) {
+        const int i = r0 + RS * k;
+        double s1 = 0.0, s2 = 0.0;
+#pragma unroll 4
+        for (int kk = 0; kk < B; ++kk) {
+            const double vv = Um[kk * LD + i] * Um[kk * LD + j];
+            s1 += vv * cc[kk];
+            s2 += vv * ss[kk];
+        }
+        if (beta) beta[i * B + j] = (T)s1;
+        if (binv) binv[i * B + j] = (T)s2;
+        if (L) g[i * B + j] = s1;  // g (the Gram) is dead: park beta for LB
+        if (wbi) wbi[i * B + j] = (double)(T)s2;
+    }
+    if (L) {  // LB = L * beta (the Q-free iteration's P1 = beta_{j-1}^-1 beta_j)
+        wave_lds_sync();
+#pragma unroll 1
+        for (int k = 0; k < NE; ++k) {
+            const int i = r0 + RS * k;
+            double s = 0.0;
+#pragma unroll 4
+            for (int kk = 0; kk < B; ++kk) s = fma((double)L[i * B + kk], g[kk * B + j], s);
+            LB[i * B + j] = (T)s;
+            if (wp1) wp1[i * B + j] = (double)(T)s;
+        }
+    }
+}
+
+}  // namespace lz
