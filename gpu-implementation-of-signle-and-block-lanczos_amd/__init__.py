@@ -93,7 +93,6 @@ HIP_SYMBOLS = [
     ("lz_comm_init_local", _c_int, [_c_vp, _c_vp, _c_int]),
     ("lz_comm_abort", _c_int, [_c_vp]),
     ("lz_debug_last_split", _c_int, [_c_vp, _c_vp]),
-    ("lz_debug_wf_stamps", _c_int, [_c_vp, _c_vp]),
     ("lz_block_lanczos_dist", _c_int, [_c_vp, _c_i64, _c_i64, _c_i64, _c_i64, _c_vp, _c_vp, _c_vp,
                                        _c_int, _c_int, _c_int, _c_i64, _c_int, _c_vp, _c_vp, _c_vp,
                                        _c_vp, _c_vp, _c_vp, _c_vp, _c_vp]),
@@ -596,17 +595,6 @@ class Handle:
         v = (_c_i64 * 2)()
         _check(self.L.lz_debug_last_split(self._h, v), "lz_debug_last_split")
         return None if v[0] < 0 else (int(v[0]), int(v[1]))
-
-    def wf_stamps(self):
-        """The sqrtm block's timing stamps of the last wavefront step launch
-        (LZ_WF_DBG bit 7; lz_debug_wf_stamps), in microseconds after the launch's
-        start: wait done, fold done, sqrtm done, last wavefront block's end, last
-        G slab stored.  None when no stamps were taken."""
-        v = (ctypes.c_int * 6)()
-        _check(self.L.lz_debug_wf_stamps(self._h, v), "lz_debug_wf_stamps")
-        if v[0] == 0:
-            return None
-        return [((v[i] - v[0]) & 0x7FFFFFFF) / 100.0 for i in range(1, 6)]
 
     def comm_abort(self):
         _check(self.L.lz_comm_abort(self._h), "lz_comm_abort")

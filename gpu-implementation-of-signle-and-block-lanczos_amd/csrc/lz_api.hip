@@ -185,38 +185,15 @@ static int block_lanczos_wf16(lz_handle *h, int64_t n, int64_t nnz, const int64_
     LZ_TRY(gram_partials<double>(h, n, 16, B, B, 16, &P));
     LZ_TRY(sqrtm_pair<double>(h, 16, nullptr, P, beta, binv[0], nullptr));
     LZ_TRY(wf_reset16(h, n, wp));
-    // The sqrtm block (default; LZ_WF_EARLY=0: the sqrtm after the launch,
-    // A/B; read per call): the step launch runs the wavefront on n_cu - 1
-    // blocks and the sqrtm of G_{j+1} (beta_{j+1}, its inverse, P1) in one
-    // more, as soon as every block's G slab is stored -- beside the launch's
-    // pass-1 tail, which trails the updaters by `lead` tiles.  After the
-    // launch only S1 and S2 are folded and the alpha kernel runs.  Same sums
-    // in the same order: the bits of the serial form on the same grid.
-    const char *ee = getenv("LZ_WF_EARLY");
-    const bool early = !(ee && ee[0] == '0') && h->grid_cap <= 0 && h->n_cu > 8;
-    WfSq sq;
-    sq.gdone = h->wf_flags + ceil_div(n, (int64_t)wp.tr) + 8;  // zeroed by wf_reset16
-    // Y_0 = A B, S1_0 = B^T Y_0 (on the wavefront grid of the steps that follow)
+    // Y_0 = A B, S1_0 = B^T Y_0
     LZ_TRY(wf_step16(h, n, rp, col, pl.col16, val, pl.pairs, wp, nullptr, nullptr, nullptr, nullptr, nullptr,
-                     nullptr, nullptr, B, Q0, 0, &P, -1, 0, -1, nullptr, early ? &sq : nullptr));
+                     nullptr, nullptr, B, Q0, 0, &P));
     LZ_TRY(alpha_wf16(h, h->partials2, P, binv[0], nullptr, alpha, P2, B, lc, n, q));
     const double *Vm1 = nullptr, *V0 = B;
     for (int j = 0; j + 1 < m; ++j) {
         double *Vn = j == 0 ? W : j == 1 ? Q1 : const_cast<double *>(Vm1);
-        sq.beta = beta + (j + 1) * bb;
-        sq.binv = binv[(j + 1) & 1];
-        sq.L = binv[j & 1];
-        sq.LB = P1;  // (the updaters read P1_j at their start; the sqrtm block writes P1_{j+1} after the last)
         LZ_TRY(wf_step16(h, n, rp, col, pl.col16, val, pl.pairs, wp, Q0, Vm1, V0, Vn, binv[j & 1], j ? P1 : nullptr,
-                         P2, Vn, Q0, j + 1, &P, -1, 0, -1, nullptr, early ? &sq : nullptr));
-        if (early) {
-            LZ_TRY(wf_fold16(h, h->partials2, P, nullptr, 0, nullptr, 0, slab, 2));
-            LZ_TRY(alpha_wf16(h, slab, 1, binv[(j + 1) & 1], P1, alpha + (j + 1) * bb, P2, Vn, lc, n,
-                              q + (j + 1) * 16));
-            Vm1 = V0;
-            V0 = Vn;
-            continue;
-        }
+                         P2, Vn, Q0, j + 1, &P));
         // the block slabs folded by 12 workgroups (one workgroup reading all
         // 1.5 MB took ~20 us), then beta_{j+1}, its inverse and P1 = beta_j^-1
         // beta_{j+1} from G, and (same launch) alpha_{j+1}, P2 and the row probe
@@ -1296,16 +1273,6 @@ int lz_comm_init(lz_handle *h, int nranks, int rank, const unsigned char id[128]
     Comm *c = nullptr;
     LZ_TRY(make_rccl_comm(nranks, rank, id, &c));
     return attach_comm(h, c);
-}
-
-int lz_debug_wf_stamps(lz_handle *h, int out[6])
-{
-    LZ_ARG_CHECK(h && out, "NULL argument");
-    for (int i = 0; i < 6; ++i) out[i] = 0;
-    if (!h->wf_flags || h->wf_T <= 0) return LZ_OK;
-    LZ_HIP_TRY(hipStreamSynchronize(h->stream));
-    LZ_HIP_TRY(hipMemcpy(out, h->wf_flags + h->wf_T + 12, sizeof(int) * 6, hipMemcpyDeviceToHost));
-    return LZ_OK;
 }
 
 int lz_debug_last_split(lz_handle *h, int64_t out[2])

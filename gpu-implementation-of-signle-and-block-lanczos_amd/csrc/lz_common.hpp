@@ -94,7 +94,6 @@ struct lz_handle {
     void *wf_deps = nullptr;
     int *wf_flags = nullptr;
     size_t wf_cap = 0;
-    int64_t wf_T = 0;             // tiles of the last wf_reset16 (the sqrtm block's counter sits past them)
     void *ybuf = nullptr;         // distributed generic-b iteration: the local SpMM result
     size_t ybuf_cap = 0;          // bytes
     void *halo = nullptr;         // lz::HaloPlan when lz_halo_init was called

@@ -40,16 +40,6 @@ struct WfAlpha {
     int64_t lc = -1;
     double *qrow = nullptr;
 };
-// The wavefront step's sqrtm block (wf_step16 with sq != null): one more
-// block than the wavefront's, which waits until every block has stored its G
-// slab (each adds 1 to *gdone, zeroed per solve; target epoch x blocks), folds
-// G like k_wf_fold and runs the sqrtm of lz_sqrtm.hpp while the launch's
-// pass-1 tail still runs: beta, binv = beta^-1, LB = L beta.
-struct WfSq {
-    int *gdone = nullptr;
-    double *beta = nullptr, *binv = nullptr, *LB = nullptr;
-    const double *L = nullptr;
-};
 // symmetric square root pair of G (device double b x b) or, when nparts > 0,
 // of the sum of the nparts slabs in h->partials.  L != null (b in {8,16,32}):
 // also LB = L * beta.  wa (b = 16): also the wavefront alpha products with
@@ -123,16 +113,12 @@ int wf_step16(lz_handle *h, int64_t n, const int64_t *rp, const int32_t *col, co
               const double *val, const uint64_t *pairs, const WfPlan &pl, const double *Yj, const double *Vprev,
               const double *Vj, double *Vout, const double *binv, const double *P1, const double *P2,
               const double *Vg, double *Yo, int epoch, int *nparts, int64_t nx = -1, int64_t p1a = 0,
-              int64_t p1b = -1, double *part = nullptr, const WfSq *sq = nullptr);
+              int64_t p1b = -1, double *part = nullptr);
 // (nx: rows of Vg, default n; pass 1 over tiles [p1a, p1b), default all; slabs
-// at part, default h->partials2; sq != null: the wavefront runs on n_cu - 1
-// blocks and, with pass 2, one more block runs the sqrtm of G beside the
-// launch's tail (WfSq); *nparts = the wavefront's blocks)
+// at part, default h->partials2)
 // the distributed step's sums: out[0..768) = [S1 (step launch G slabs + G1 + G2
 // boundary slabs) | S2 | G]
-int wf_fold16(lz_handle *h, const double *kp, int G, const double *b1, int G1, const double *b2, int G2, double *out,
-              int nmat = 3);  // nmat = 2: S1 and S2 only
-
+int wf_fold16(lz_handle *h, const double *kp, int G, const double *b1, int G1, const double *b2, int G2, double *out);
 // alpha = sym(binv (S1 binv - S2 P1)) (P1 == nullptr: no S2 term), P2 = binv alpha,
 // q = V[lc] binv; S1, S2 = the sums of the P slabs at part, part + 256 P
 int alpha_wf16(lz_handle *h, const double *part, int P, const double *binv, const double *P1, double *alpha,

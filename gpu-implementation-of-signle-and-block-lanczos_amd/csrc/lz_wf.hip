@@ -38,7 +38,6 @@
 
 #include "lz_internal.hpp"
 #include "lz_kernels.hpp"
-#include "lz_sqrtm.hpp"
 
 namespace lz {
 
@@ -152,32 +151,6 @@ __device__ __forceinline__ double dpp_swap1(double x)
     return r;
 }
 
-// entry i of slabs q, q + 16, q + 32, ... (of P) with four independent
-// accumulators; LD loads one double (plain, or sc1 inside a launch)
-template <typename LD>
-__device__ __forceinline__ double wf_fold_part(const double *p, int P, int q, int i, LD ld)
-{
-    double a0 = 0.0, a1 = 0.0, a2 = 0.0, a3 = 0.0;
-    int g = q;
-    for (; g + 48 < P; g += 64) {
-        a0 += ld(p + (int64_t)g * 256 + i);
-        a1 += ld(p + (int64_t)(g + 16) * 256 + i);
-        a2 += ld(p + (int64_t)(g + 32) * 256 + i);
-        a3 += ld(p + (int64_t)(g + 48) * 256 + i);
-    }
-    for (; g < P; g += 16) a0 += ld(p + (int64_t)g * 256 + i);
-    return (a0 + a1) + (a2 + a3);
-}
-
-// the 16 partial sums of one entry added in a fixed tree (lane l of wave 0)
-__device__ __forceinline__ double wf_fold_tree(const double (*ps)[64], int l)
-{
-    double t[4];
-#pragma unroll
-    for (int k = 0; k < 4; ++k) t[k] = (ps[4 * k][l] + ps[4 * k + 1][l]) + (ps[4 * k + 2][l] + ps[4 * k + 3][l]);
-    return (t[0] + t[1]) + (t[2] + t[3]);
-}
-
 // The step kernel.  P2 == nullptr: the first launch of a solve (pass 1 only,
 // on Vg = B; no flags).  P1 == nullptr: no V_{j-1} term (step 0).  Vprev and
 // Vout may alias (V_{j+1} over V_{j-1}: each strip is read, then written, by
@@ -190,7 +163,7 @@ __global__ __launch_bounds__(64 * (NC + NL + NU)) void k_wf16(
     const double *__restrict__ Vj, double *Vout, const double *__restrict__ binv, const double *__restrict__ P1,
     const double *__restrict__ P2, const double *Vg, double *Yo, const int2 *__restrict__ deps, int *flags, int epoch,
     int64_t hback, int lead, double *__restrict__ part, int *__restrict__ err, int dbg, int64_t nx, int64_t p1a,
-    int64_t p1b, int64_t Th, int cpol, WfSq sq)
+    int64_t p1b, int64_t Th, int cpol)
 {
     using CT = typename std::conditional<C16, int16_t, int32_t>::type;
     using C = FwCfg<NC, CAP, true, true, CT>;
@@ -221,80 +194,7 @@ __global__ __launch_bounds__(64 * (NC + NL + NU)) void k_wf16(
         if (threadIdx.x == 0) *err = 7;
         return;
     }
-    int *const gdone = sq.gdone;
-    // G wavefront blocks; with sq, block G runs the sqrtm
-    const int64_t G = gdone ? gridDim.x - 1 : gridDim.x, bid = blockIdx.x;
-    // timing diagnostics (LZ_WF_DBG bit 7): s_memrealtime stamps past the counter
-    int *const stamp = (gdone && (dbg & 128)) ? gdone + 4 : nullptr;
-    auto now = []() { return (int)(__builtin_amdgcn_s_memrealtime() & 0x7fffffff); };
-    if (stamp && bid == 0 && threadIdx.x == 0) __hip_atomic_store(stamp, now(), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    if (gdone && bid == G) {
-        // ------------------------------------------------------- sqrtm block
-        // Wait until every wavefront block has stored its G slab (sc1, drained,
-        // then one add each: MI355X_MICROARCH.md "Valid forms", first row; the
-        // count runs over the solve's steps), fold G with sc1 loads in
-        // k_wf_fold's sums and order, then one wave: the Jacobi and beta,
-        // beta^-1, LB = L beta of lz_sqrtm.hpp (k_sqrtm_b's bits).  The
-        // wavefront's updaters finish `lead` tiles ahead of its pass 1, so this
-        // runs beside the launch's tail.  The CSR stages are LDS scratch here.
-        static_assert(sizeof(st) >= sizeof(double) * (256 + 64 * 64 + 2 * 16 * 17 + 32), "sqrtm scratch");
-        double *wg = reinterpret_cast<double *>(&st[0]);
-        double(*ps)[64] = reinterpret_cast<double(*)[64]>(wg + 256);  // [4 x 16][64]
-        double *Am = wg + 256 + 64 * 64, *Um = Am + 16 * 17, *cc = Um + 16 * 17, *ss = cc + 16;
-        if (threadIdx.x == 0) {
-            const int target = epoch * (int)G;
-            long spin = 0;
-            while (__hip_atomic_load(gdone, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < target &&
-                   ++spin < (1L << 24))
-                __builtin_amdgcn_s_sleep(8);
-            ready[0] = spin < (1L << 24);
-            if (!ready[0]) *err = 8;
-        }
-        __syncthreads();
-        if (!ready[0]) return;
-        if (stamp && threadIdx.x == 0) __hip_atomic_store(stamp + 1, now(), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        auto ld = [](const double *a) {
-            const uint64_t u = __hip_atomic_load(reinterpret_cast<const uint64_t *>(a), __ATOMIC_RELAXED,
-                                                 __HIP_MEMORY_SCOPE_AGENT);
-            double d;
-            __builtin_memcpy(&d, &u, 8);
-            return d;
-        };
-        // wave q sums slabs q, q + 16, ... of all 256 entries at once (its four
-        // entries' sixteen accumulators in flight together), then wave 0 adds
-        // the 16 partial sums of each entry in the fixed tree
-        constexpr int NW = NC + NL + NU;
-        const double *gp = part + 2 * G * 256;
-        for (int q = w; q < 16; q += NW) {
-            double a[4][4];
-#pragma unroll
-            for (int r = 0; r < 4; ++r)
-#pragma unroll
-                for (int k = 0; k < 4; ++k) a[r][k] = 0.0;
-            int g = q;
-            for (; g + 48 < (int)G; g += 64)
-#pragma unroll
-                for (int r = 0; r < 4; ++r)
-#pragma unroll
-                    for (int k = 0; k < 4; ++k) a[r][k] += ld(gp + (int64_t)(g + 16 * k) * 256 + r * 64 + lane);
-            for (; g < (int)G; g += 16)
-#pragma unroll
-                for (int r = 0; r < 4; ++r) a[r][0] += ld(gp + (int64_t)g * 256 + r * 64 + lane);
-#pragma unroll
-            for (int r = 0; r < 4; ++r) ps[r * 16 + q][lane] = (a[r][0] + a[r][1]) + (a[r][2] + a[r][3]);
-        }
-        __syncthreads();
-        if (w < 4) wg[w * 64 + lane] = wf_fold_tree(ps + w * 16, lane);
-        __syncthreads();
-        if (stamp && threadIdx.x == 0) __hip_atomic_store(stamp + 2, now(), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        if (w == 0) {
-            sqrtm_init<16>(wg, Am, Um, lane);
-            (void)jacobi_rr<16>(Am, Um, lane);
-            sqrtm_tail<double, 16>(Am, Um, cc, ss, wg, sq.beta, sq.binv, sq.L, sq.LB, nullptr, nullptr, lane);
-            if (stamp && lane == 0) __hip_atomic_store(stamp + 3, now(), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        }
-        return;
-    }
+    const int64_t G = gridDim.x, bid = blockIdx.x;
     // regions: pass-1 tiles [begin, end) of region x go to the blocks b = x
     // (mod 8), interleaved; the region's pass-2 tiles are [pbeg, pend), the
     // same range moved hback tiles down, so the pass-2 wavefront leads
@@ -305,16 +205,11 @@ __global__ __launch_bounds__(64 * (NC + NL + NU)) void k_wf16(
     if (G < 8) {
         begin = p1a; end = p1b; kb = bid; KB = G; pbeg = 0; pend = T;
     } else {
-        // (a region's share of the tiles is its share of the blocks: with
-        // G % 8 != 0, e.g. one CU left to the early sqrtm, the regions differ
-        // by a block; for G % 8 == 0 this is NP1 x / 8)
         const int64_t x = bid & 7;
-        int64_t cum = 0;
-        for (int64_t y = 0; y < x; ++y) cum += (G - y + 7) >> 3;
-        KB = (G - x + 7) >> 3;
-        begin = p1a + NP1 * cum / G;
-        end = p1a + NP1 * (cum + KB) / G;
+        begin = p1a + NP1 * x / 8;
+        end = p1a + NP1 * (x + 1) / 8;
         kb = bid >> 3;
+        KB = (G - x + 7) >> 3;
         pbeg = x == 0 ? 0 : (begin - hback > 0 ? begin - hback : 0);
         pend = x == 7 ? T : (end - hback > 0 ? end - hback : 0);
     }
@@ -444,14 +339,9 @@ __global__ __launch_bounds__(64 * (NC + NL + NU)) void k_wf16(
                 if (s >= ns || s / NC <= paced) return;
                 paced = s / NC;
                 const uint32_t pa = ws_lds_addr(&p1pub);
-                // (never more than the block's pass-1 tiles less lead: a
-                // distributed rank's pass 1 here covers only the interior, and
-                // the tiles past the region's last pass-1 tile -- the last
-                // region's final hback tiles -- start lead tiles before the
-                // launch's end, so the G slabs (the sqrtm block) are complete
-                // that early)
-                const int64_t cap_t = nt - lead > 0 ? nt - lead : 0;
-                const int target = (int)(m - lead < cap_t ? m - lead : cap_t);
+                // (never more than the block's pass-1 tiles: a distributed rank's
+                // pass 1 here covers only the interior)
+                const int target = (int)(m - lead < nt ? m - lead : nt);
                 long spin = 0;
                 while (ws_lds_read(pa) < target && ++spin < kWsSpin) __builtin_amdgcn_s_sleep(2);
                 if (spin >= kWsSpin) *err = 6;
@@ -568,23 +458,7 @@ __global__ __launch_bounds__(64 * (NC + NL + NU)) void k_wf16(
                 double a = 0.0;
                 for (int u = 0; u < NU; ++u) a += ust[u][0][0][e];
                 // e < 256: G slab (at 2G), else S2 (at G)
-                double *dst = &part[(e < 256 ? 2 * G : G) * 256 + bid * 256 + (e & 255)];
-                if (gdone) {  // read inside this launch by the early sqrtm: write-through
-                    uint64_t u;
-                    __builtin_memcpy(&u, &a, 8);
-                    __hip_atomic_store(reinterpret_cast<uint64_t *>(dst), u, __ATOMIC_RELAXED,
-                                       __HIP_MEMORY_SCOPE_AGENT);
-                } else {
-                    *dst = a;
-                }
-            }
-            if (gdone) {
-                // this wave stored every byte of the block's G and S2 slabs (sc1):
-                // drained, then one add per block (MI355X_MICROARCH.md, "Valid
-                // forms", first row; k_wf_fold_wait polls the counter)
-                asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-                if (lane == 0) __hip_atomic_fetch_add(gdone, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-                if (stamp && lane == 0) __hip_atomic_fetch_max(stamp + 5, now(), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                part[(e < 256 ? 2 * G : G) * 256 + bid * 256 + (e & 255)] = a;
             }
         }
         return;
@@ -749,7 +623,6 @@ __global__ __launch_bounds__(64 * (NC + NL + NU)) void k_wf16(
             for (; sl < NC; ++sl) a[0] += scr[sl][e];
             slab[e] = (a[0] + a[1]) + (a[2] + a[3]);
         }
-        if (stamp && lane == 0) __hip_atomic_fetch_max(stamp + 4, now(), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     }
 }
 
@@ -819,7 +692,7 @@ int wf_step16(lz_handle *h, int64_t n, const int64_t *rp, const int32_t *col, co
               const double *val, const uint64_t *pairs, const WfPlan &pl, const double *Yj, const double *Vprev,
               const double *Vj, double *Vout, const double *binv, const double *P1, const double *P2,
               const double *Vg, double *Yo, int epoch, int *nparts, int64_t nx, int64_t p1a, int64_t p1b,
-              double *part, const WfSq *sq)
+              double *part)
 {
     const int64_t T = ceil_div(n, (int64_t)pl.tr);
     if (nx < 0) nx = n;
@@ -829,8 +702,6 @@ int wf_step16(lz_handle *h, int64_t n, const int64_t *rp, const int32_t *col, co
     LZ_ARG_CHECK(pl.ok && n < (1 << 24), "wavefront step: wf_plan16 first");
     LZ_ARG_CHECK(pairs != nullptr, "strip row orders (strip_pairs) missing");
     LZ_ARG_CHECK(P2 == nullptr || (Yj && Vj && Vout && binv && Vg == Vout), "wavefront step buffers");
-    LZ_ARG_CHECK(!sq || (h->grid_cap <= 0 && sq->gdone && (!P2 || (sq->beta && sq->binv && sq->L && sq->LB))),
-                 "wavefront step: sqrtm block arguments");
     static_assert(12 <= kPairPad, "row orders must cover the last tile's strips");
     // pass 2 covers every tile when it runs; a pass-1-only launch its range
     const int64_t work = P2 ? T : p1b - p1a;
@@ -839,12 +710,7 @@ int wf_step16(lz_handle *h, int64_t n, const int64_t *rp, const int32_t *col, co
         return LZ_OK;
     }
     // (virtual ranks sharing the device: each rank's share, so every grid is resident)
-    // (with the sqrtm block: n_cu - 1 wavefront blocks; LZ_WF_GRID caps the
-    // wavefront's blocks for A/B and the bitwise sqrtm-block test, read per call)
-    int cap = h->grid_cap > 0 ? h->grid_cap : (sq ? h->n_cu - 1 : h->n_cu);
-    const char *gc = getenv("LZ_WF_GRID");
-    if (gc && atoi(gc) > 0) cap = std::min(cap, atoi(gc));
-    const int grid = (int)std::max<int64_t>(1, std::min<int64_t>(work, cap));
+    const int grid = (int)std::max<int64_t>(1, std::min<int64_t>(work, h->grid_cap > 0 ? h->grid_cap : h->n_cu));
     // LZ_WF_DBG (timing diagnostics only; results are wrong): bit 0 skips the
     // loaders' flag polls, bit 1 the updaters' work, bit 2 the pass-1 tiles;
     // bit 3 / bit 6 run the updaters at issue priority 0 / 3 (default 2)
@@ -866,12 +732,11 @@ int wf_step16(lz_handle *h, int64_t n, const int64_t *rp, const int32_t *col, co
     const int cpol = cp ? atoi(cp) : 7;
     const int ev = prof_begin(h, PROF_SPMM_PASS);
     // (the block is 64 (NC + NL + NU) threads: the kernel refuses any other size)
-    const WfSq sqk = (sq && P2) ? *sq : WfSq{};  // the sqrtm block runs beside pass 2 only
     auto go = [&](auto kern, int waves) {
-        hipLaunchKernelGGL(kern, dim3(grid + (sqk.gdone ? 1 : 0)), dim3(64 * waves), 0, h->stream, n, rp, col, col16, val,
+        hipLaunchKernelGGL(kern, dim3(grid), dim3(64 * waves), 0, h->stream, n, rp, col, col16, val,
                            pairs, Yj, Vprev, Vj, Vout, binv, P1, P2, Vg, Yo,
                            static_cast<const int2 *>(h->wf_deps), h->wf_flags, epoch, (int64_t)pl.hback, lead,
-                           part, h->err_flag, dbg, nx, p1a, p1b, T, cpol, sqk);
+                           part, h->err_flag, dbg, nx, p1a, p1b, T, cpol);
     };
     // LDS (<= 160 KB): strip slots per updater DU + 1, fewer with 32-bit columns
     constexpr int cap12 = 12 * 16 * kWfCapPerRow, cap11 = 11 * 16 * kWfCapPerRow, cap10 = 10 * 16 * kWfCapPerRow;
@@ -908,22 +773,38 @@ __global__ __launch_bounds__(1024) void k_wf_fold(const double *__restrict__ kp,
 {
     __shared__ double ps[16][64];
     const int m = blockIdx.x >> 2, q = threadIdx.x >> 6, i = (blockIdx.x & 3) * 64 + (threadIdx.x & 63);
-    auto ld = [](const double *a) { return *a; };
-    double s = wf_fold_part(kp + (int64_t)m * G * 256, G, q, i, ld);
+    auto sum = [&](const double *p, int P) {
+        double a0 = 0.0, a1 = 0.0, a2 = 0.0, a3 = 0.0;
+        int g = q;
+        for (; g + 48 < P; g += 64) {
+            a0 += p[(int64_t)g * 256 + i];
+            a1 += p[(int64_t)(g + 16) * 256 + i];
+            a2 += p[(int64_t)(g + 32) * 256 + i];
+            a3 += p[(int64_t)(g + 48) * 256 + i];
+        }
+        for (; g < P; g += 16) a0 += p[(int64_t)g * 256 + i];
+        return (a0 + a1) + (a2 + a3);
+    };
+    double s = sum(kp + (int64_t)m * G * 256, G);
     if (m == 0) {
-        s += wf_fold_part(b1, G1, q, i, ld);
-        s += wf_fold_part(b2, G2, q, i, ld);
+        s += sum(b1, G1);
+        s += sum(b2, G2);
     }
     ps[q][threadIdx.x & 63] = s;
     __syncthreads();
-    if (q == 0) out[m * 256 + i] = wf_fold_tree(ps, threadIdx.x & 63);
+    if (q == 0) {
+        const int l = threadIdx.x & 63;
+        double t[4];
+#pragma unroll
+        for (int k = 0; k < 4; ++k) t[k] = (ps[4 * k][l] + ps[4 * k + 1][l]) + (ps[4 * k + 2][l] + ps[4 * k + 3][l]);
+        out[m * 256 + i] = (t[0] + t[1]) + (t[2] + t[3]);
+    }
 }
 
-int wf_fold16(lz_handle *h, const double *kp, int G, const double *b1, int G1, const double *b2, int G2, double *out,
-              int nmat)
+int wf_fold16(lz_handle *h, const double *kp, int G, const double *b1, int G1, const double *b2, int G2, double *out)
 {
     const int ev = prof_begin(h, PROF_SMALL);
-    hipLaunchKernelGGL(k_wf_fold, dim3(4 * nmat), dim3(1024), 0, h->stream, kp, G, b1, G1, b2, G2, out);
+    hipLaunchKernelGGL(k_wf_fold, dim3(12), dim3(1024), 0, h->stream, kp, G, b1, G1, b2, G2, out);
     prof_end(h, ev);
     LZ_LAUNCH_CHECK();
     return LZ_OK;
@@ -933,9 +814,7 @@ int wf_reset16(lz_handle *h, int64_t n, const WfPlan &pl)
 {
     const int64_t T = ceil_div(n, (int64_t)pl.tr);
     LZ_ARG_CHECK((size_t)T <= h->wf_cap, "wf_plan16 first");
-    // (the tile flags and, after them, the early sqrtm's block counter)
-    LZ_HIP_TRY(hipMemsetAsync(h->wf_flags, 0, sizeof(int) * (size_t)(T + 64), h->stream));
-    h->wf_T = T;
+    LZ_HIP_TRY(hipMemsetAsync(h->wf_flags, 0, sizeof(int) * (size_t)T, h->stream));
     return LZ_OK;
 }
 

@@ -210,12 +210,6 @@ int lz_comm_abort(lz_handle *h);
  * beside the exchange in the handle's last distributed solve ({-1, -1}: the
  * solve ran unsplit). */
 int lz_debug_last_split(lz_handle *h, int64_t out[2]);
-/* Timing diagnostics of the wavefront step's sqrtm block (LZ_WF_DBG bit 7,
- * single-GPU solves): s_memrealtime stamps (100 MHz, low 31 bits) of the last
- * step launch -- [0] launch start (block 0), [1] the sqrtm block's wait done,
- * [2] its G fold done, [3] its sqrtm done, [4] the last wavefront block's end,
- * [5] the last G slab stored; zeros when none were taken. */
-int lz_debug_wf_stamps(lz_handle *h, int out[6]);
 
 /* Distributed block Lanczos, all-gather form (the north star's exchange).
  * Every rank's slab is padded to n_pad rows (n_pad >= max rows per rank) and

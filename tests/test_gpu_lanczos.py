@@ -158,29 +158,6 @@ def test_block_b16_wavefront_bitwise(lz, handle, torch_cuda, monkeypatch):
         assert np.array_equal(x, y)
 
 
-@pytest.mark.parametrize("n", [400_009, 2_000_003])
-def test_block_b16_wavefront_early_sqrtm(lz, orc, handle, torch_cuda, monkeypatch, n):
-    """The sqrtm block (one more block of the step launch folds G and runs the
-    sqrtm beside the launch's pass-1 tail) gives the bits of the serial form
-    (fold, then the sqrtm kernel) on the same wavefront grid, and matches the
-    oracle."""
-    monkeypatch.setenv("LZ_PASS_WF", "1")
-    A = lz.gen_banded(n, 10.0, 4096, seed=5)
-    B = lz.uniform_B(A.n, 16, seed=5)
-    m, lc = 10, 84
-    grid = torch_cuda.cuda.get_device_properties(0).multi_processor_count - 1
-    monkeypatch.setenv("LZ_WF_EARLY", "1")
-    r1 = gpu_block(lz, handle, torch_cuda, A, B, m, lc)
-    assert handle.device_error() == 0
-    monkeypatch.setenv("LZ_WF_EARLY", "0")
-    monkeypatch.setenv("LZ_WF_GRID", str(grid))
-    r2 = gpu_block(lz, handle, torch_cuda, A, B, m, lc)
-    for x, y in zip(r1, r2):
-        assert np.array_equal(x, y)
-    monkeypatch.delenv("LZ_WF_GRID")
-    assert_close_run(lz, m, 16, r1, orc.block_lanczos(A, B, m, lc))
-
-
 def test_block_b16_tail_rows(lz, orc, handle, torch_cuda):
     """n not a multiple of the 16-row tiles, lc in the last partial tile."""
     A = lz.gen_banded(1000 * 16 + 11, 7.0, 64, seed=2)
