@@ -93,7 +93,6 @@ HIP_SYMBOLS = [
     ("lz_comm_init_local", _c_int, [_c_vp, _c_vp, _c_int]),
     ("lz_comm_abort", _c_int, [_c_vp]),
     ("lz_debug_last_split", _c_int, [_c_vp, _c_vp]),
-    ("lz_debug_wf_times", _c_int, [_c_vp, _c_int, _c_vp]),
     ("lz_block_lanczos_dist", _c_int, [_c_vp, _c_i64, _c_i64, _c_i64, _c_i64, _c_vp, _c_vp, _c_vp,
                                        _c_int, _c_int, _c_int, _c_i64, _c_int, _c_vp, _c_vp, _c_vp,
                                        _c_vp, _c_vp, _c_vp, _c_vp, _c_vp]),
@@ -596,15 +595,6 @@ class Handle:
         v = (_c_i64 * 2)()
         _check(self.L.lz_debug_last_split(self._h, v), "lz_debug_last_split")
         return None if v[0] < 0 else (int(v[0]), int(v[1]))
-
-    def wf_times(self, G):
-        """Per-block times of the last wavefront step launch (LZ_WF_DBG bit 7):
-        (start, consumers' end, updaters' end), each an array of G values in
-        microseconds after the earliest start."""
-        v = np.zeros(3 * G, np.float64)
-        _check(self.L.lz_debug_wf_times(self._h, G, v.ctypes.data), "lz_debug_wf_times")
-        v = (v - v[:G].min()) / 100.0
-        return v[:G], v[G:2 * G], v[2 * G:]
 
     def comm_abort(self):
         _check(self.L.lz_comm_abort(self._h), "lz_comm_abort")

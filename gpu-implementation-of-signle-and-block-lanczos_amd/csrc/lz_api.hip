@@ -1275,14 +1275,6 @@ int lz_comm_init(lz_handle *h, int nranks, int rank, const unsigned char id[128]
     return attach_comm(h, c);
 }
 
-int lz_debug_wf_times(lz_handle *h, int G, double *out)
-{
-    LZ_ARG_CHECK(h && out && G > 0 && G <= 1024, "lz_debug_wf_times arguments");
-    LZ_HIP_TRY(hipStreamSynchronize(h->stream));
-    LZ_HIP_TRY(hipMemcpy(out, h->partials2 + (int64_t)3 * G * 256, sizeof(double) * 3 * G, hipMemcpyDeviceToHost));
-    return LZ_OK;
-}
-
 int lz_debug_last_split(lz_handle *h, int64_t out[2])
 {
     LZ_ARG_CHECK(h && out, "NULL argument");

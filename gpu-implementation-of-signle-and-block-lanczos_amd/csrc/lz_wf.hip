@@ -195,11 +195,6 @@ __global__ __launch_bounds__(64 * (NC + NL + NU)) void k_wf16(
         return;
     }
     const int64_t G = gridDim.x, bid = blockIdx.x;
-    // timing diagnostics (LZ_WF_DBG bit 7; lz_debug_wf_times): s_memrealtime of
-    // each block's start, its consumers' and its updaters' end, past the slabs
-    double *const tstamp = (dbg & 128) ? part + 3 * G * 256 : nullptr;
-    auto now = []() { return (double)__builtin_amdgcn_s_memrealtime(); };
-    if (tstamp && threadIdx.x == 0) tstamp[bid] = now();
     // regions: pass-1 tiles [begin, end) of region x go to the blocks b = x
     // (mod 8), interleaved; the region's pass-2 tiles are [pbeg, pend), the
     // same range moved hback tiles down, so the pass-2 wavefront leads
@@ -465,7 +460,6 @@ __global__ __launch_bounds__(64 * (NC + NL + NU)) void k_wf16(
                 // e < 256: G slab (at 2G), else S2 (at G)
                 part[(e < 256 ? 2 * G : G) * 256 + bid * 256 + (e & 255)] = a;
             }
-            if (tstamp && lane == 0) tstamp[2 * G + bid] = now();
         }
         return;
     }
@@ -629,7 +623,6 @@ __global__ __launch_bounds__(64 * (NC + NL + NU)) void k_wf16(
             for (; sl < NC; ++sl) a[0] += scr[sl][e];
             slab[e] = (a[0] + a[1]) + (a[2] + a[3]);
         }
-        if (tstamp && lane == 0) tstamp[G + bid] = now();
     }
 }
 
@@ -720,8 +713,7 @@ int wf_step16(lz_handle *h, int64_t n, const int64_t *rp, const int32_t *col, co
     const int grid = (int)std::max<int64_t>(1, std::min<int64_t>(work, h->grid_cap > 0 ? h->grid_cap : h->n_cu));
     // LZ_WF_DBG (timing diagnostics only; results are wrong): bit 0 skips the
     // loaders' flag polls, bit 1 the updaters' work, bit 2 the pass-1 tiles;
-    // bit 3 / bit 6 run the updaters at issue priority 0 / 3 (default 2); bit 7
-    // takes per-block time stamps (results unchanged; lz_debug_wf_times)
+    // bit 3 / bit 6 run the updaters at issue priority 0 / 3 (default 2)
     const char *dg = getenv("LZ_WF_DBG");
     const int dbg = dg ? atoi(dg) : 0;
     // the updaters' pace (tiles ahead of the block's pass 1): at least the

@@ -210,10 +210,6 @@ int lz_comm_abort(lz_handle *h);
  * beside the exchange in the handle's last distributed solve ({-1, -1}: the
  * solve ran unsplit). */
 int lz_debug_last_split(lz_handle *h, int64_t out[2]);
-/* Timing diagnostics of the last wavefront step launch of G blocks, taken when
- * LZ_WF_DBG has bit 7 (128) set: out[0, G) each block's start, out[G, 2G) its
- * consumers' end, out[2G, 3G) its updaters' end, s_memrealtime ticks (100 MHz). */
-int lz_debug_wf_times(lz_handle *h, int G, double *out);
 
 /* Distributed block Lanczos, all-gather form (the north star's exchange).
  * Every rank's slab is padded to n_pad rows (n_pad >= max rows per rank) and
