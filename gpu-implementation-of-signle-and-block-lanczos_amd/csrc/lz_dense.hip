@@ -657,14 +657,7 @@ __global__ __launch_bounds__(kRedThreads) void k_sqrtm_b(const T *__restrict__ G
     const int jq = B - 1 - j;                      // partner position of j
     const int jn = j == 0 ? 0 : (j == 1 ? B - 1 : j - 1);  // moved position of j
     double *Am = Abuf[0], *An = Abuf[1], *Um = Ubuf[0], *Un = Ubuf[1];
-#pragma unroll UN
-    for (int k = 0; k < NE; ++k) {
-        const int i = r0 + RS * k;
-        // symmetrise from the lower triangle (syevj with CUBLAS_FILL_MODE_LOWER)
-        Am[i * LD + j] = (i < j) ? g[j * B + i] : g[i * B + j];
-        Um[i * LD + j] = (i == j) ? 1.0 : 0.0;
-    }
-    wave_lds_sync();
+    sqrtm_init<B>(g, Am, Um, tid);  // symmetrised from the lower triangle, U = I
 #ifdef LZ_SQRTM_PROBE
     const long long t0 = clock64();
     int nsw = 0;

@@ -1,15 +1,14 @@
 // lz_sqrtm.hpp -- the wave-level pieces of the b x b symmetric square root
-// (beta = sqrtm(G), beta^-1), shared by k_sqrtm_b (lz_dense.hip) and the
-// wavefront step's sqrtm block (lz_wf.hip) so both produce the same bits.
-// The reference's sqrtm: kernels/my_sqrtm_cusolver.hpp (syevj, then
-// V f(L) V^T).  One wave (lanes tid < 64) runs each function; Am, Um are
-// B x (B + 1) LDS matrices, cc / ss B-entry LDS vectors.
+// (beta = sqrtm(G), beta^-1) that k_sqrtm_b (lz_dense.hip) runs after its slab
+// reduction: any kernel that includes them gets k_sqrtm_b's bits.  The
+// reference's sqrtm: kernels/my_sqrtm_cusolver.hpp (syevj, then V f(L) V^T).
+// One wave (lanes tid < 64) runs each function; Am, Um are B x (B + 1) LDS
+// matrices, cc / ss B-entry LDS vectors.
 #pragma once
 
 #include "lz_kernels.hpp"
 
 namespace lz {
-
 
 // Jacobi rotation for the pair (p, q): c, s with R[p][p] = R[q][q] = c,
 // R[p][q] = -s, R[q][p] = s annihilating a_pq -- Numerical Recipes' angle
@@ -18,8 +17,8 @@ namespace lz {
 // no square root: with cos(2 theta) = |d| / r, c^2 = u = (1 + |d| / r) / 2
 // and s = sin(2 theta) / (2 c) = sgn(d) a2 / (2 r c).  Two reciprocal square
 // roots (v_rsq_f64 and one Newton step each) replace the division, the sqrt
-// and the rsq of the direct form: the round's dependent chain is ~40 % shorter
-// (the sqrtm sits on the step's critical path).
+// and the rsq of the direct form, which head every round's dependent chain
+// (C3: the sqrtm kernel 56.8 -> 51.4 us per step).
 __device__ __forceinline__ void jacobi_rot(double app, double aqq, double apq, double &c, double &s)
 {
 #pragma clang fp contract(off)
