@@ -54,6 +54,7 @@ HIP_SYMBOLS = [
     ("lz_init", _c_int, [_c_int, ctypes.POINTER(_c_vp)]),
     ("lz_finalize", _c_int, [_c_vp]),
     ("lz_set_stream", _c_int, [_c_vp, _c_vp]),
+    ("lz_set_final_state", _c_int, [_c_vp, _c_int]),
     ("lz_last_error", ctypes.c_char_p, []),
     ("lz_version", ctypes.c_char_p, []),
     ("lz_device_ok", _c_int, [_c_int]),
@@ -65,6 +66,7 @@ HIP_SYMBOLS = [
     ("lz_csr_spmm", _c_int, [_c_vp, _c_i64, _c_i64, _c_i64, _c_vp, _c_vp, _c_vp, _c_int, _c_int,
                              _c_vp, _c_i64, _c_int, _c_vp, _c_i64]),
     ("lz_to_row_major", _c_int, [_c_vp, _c_i64, _c_int, _c_int, _c_vp, _c_i64, _c_vp]),
+    ("lz_to_col_major", _c_int, [_c_vp, _c_i64, _c_int, _c_int, _c_vp, _c_vp, _c_i64]),
     ("lz_csr_spmv", _c_int, [_c_vp, _c_i64, _c_i64, _c_i64, _c_vp, _c_vp, _c_vp, _c_int, _c_vp, _c_vp]),
     ("lz_gram", _c_int, [_c_vp, _c_i64, _c_int, _c_int, _c_vp, _c_i64, _c_vp]),
     ("lz_sym_cross_gram", _c_int, [_c_vp, _c_i64, _c_int, _c_int, _c_vp, _c_vp, _c_i64, _c_vp]),
@@ -532,6 +534,11 @@ class Handle:
         _check(fn(self.ptr, n, A.nnz, _ptr(A.row_ptr), _ptr(A.col), _ptr(A.val), A.dtype, b, m, lc,
                   _ptr(B), _ptr(q), _ptr(alpha), _ptr(beta), _ptr(Q0), _ptr(Q1), _ptr(W)),
                "lz_block_lanczos")
+
+    def set_final_state(self, on: bool) -> None:
+        """True (default): block_lanczos_blas leaves Q0 = Q1 = Q_{m-1} and W = the
+        last residual, as the reference does; False: they are scratch on return."""
+        _check(self.L.lz_set_final_state(self.ptr, 1 if on else 0), "lz_set_final_state")
 
     def vector_lanczos(self, A: CsrDevice, bvec, m: int, lc: int, q, alpha, beta, q0, q1, w):
         """vector_lanczos (methods/vector_lanczos.hpp:8-67); alpha/beta are device tensors.

@@ -50,6 +50,23 @@ void set_error(const char *fmt, ...)
     va_end(ap);
 }
 
+// The wavefront step and the persistent pass 1 end a wait they would
+// otherwise never leave by setting the device error word (lz_device_error);
+// their results are then wrong.  The solve entry points that launch them read
+// the word once at the end (one host synchronisation per solve) and fail.
+static int solve_status(lz_handle *h)
+{
+    int e = 0;
+    LZ_HIP_TRY(hipMemcpyAsync(&e, h->err_flag, sizeof(int), hipMemcpyDeviceToHost, h->stream));
+    LZ_HIP_TRY(hipStreamSynchronize(h->stream));
+    if (e != 0) {
+        set_error("device error word %d: a persistent kernel abandoned a bounded wait; the results are invalid "
+                  "(lz_device_error reads and clears the word)", e);
+        return LZ_E_DEVICE;
+    }
+    return LZ_OK;
+}
+
 static int check_csr(int64_t n, int64_t nnz, const int64_t *rp, const int32_t *col,
                      const void *val)
 {
@@ -129,6 +146,10 @@ static int block_lanczos_unfused(lz_handle *h, int64_t n, int64_t nnz, const int
         std::swap(Q0, Q1);                                           // Q0 = Q1 (:162), no copy
         LZ_TRY(copy_row<T>(h, b, Q0, b, 0, lc, q + j * b));          // (:165)
     }
+    // the pointer swaps leave Q_{m-1} in one buffer and Q_{m-2} in the other:
+    // one copy gives the reference's Q0 = Q1 = Q_{m-1} on return
+    if (m >= 2 && h->final_state)
+        LZ_HIP_TRY(hipMemcpyAsync(Q1, Q0, sizeof(T) * (size_t)n * b, hipMemcpyDeviceToDevice, h->stream));
     return LZ_OK;
 }
 
@@ -213,6 +234,12 @@ static int block_lanczos_wf16(lz_handle *h, int64_t n, int64_t nnz, const int64_
     }
     LZ_HIP_TRY(hipMemcpyAsync(beta + m * bb, binv[(m - 1) & 1], sizeof(double) * bb, hipMemcpyDeviceToDevice,
                               h->stream));
+    // the reference's post-call state: W_m = Y_{m-1} beta^-1 - V_{m-2} P1 -
+    // V_{m-1} P2 (the pass 2 a further step would run), Q0 = Q1 = V_{m-1} beta^-1
+    // (Q1 untouched at m = 1, as the reference's)
+    if (h->final_state)
+        LZ_TRY(final_state<double>(h, n, 16, Q0, Vm1, V0, nullptr, binv[(m - 1) & 1], Vm1 ? P1 : nullptr, P2, W, Q0,
+                                   m >= 2 ? Q1 : nullptr));
     return LZ_OK;
 }
 
@@ -254,6 +281,9 @@ static int block_lanczos_fused16(lz_handle *h, int64_t n, int64_t nnz, const int
     }
     LZ_HIP_TRY(hipMemcpyAsync(beta + m * bb, qb.binv[(m - 1) & 1], sizeof(double) * bb, hipMemcpyDeviceToDevice,
                               h->stream));
+    if (h->final_state)  // W = W_m (in), Q0 = Q1 = W_{m-1} beta^-1 (prev)
+        LZ_TRY(final_state<double>(h, n, 16, nullptr, nullptr, prev, in, qb.binv[(m - 1) & 1], nullptr, nullptr, W,
+                                   Q0, m >= 2 ? Q1 : nullptr));
     return LZ_OK;
 }
 
@@ -311,6 +341,9 @@ static int block_lanczos_b2_32(lz_handle *h, int64_t n, int64_t nnz, const int64
         in = out;
     }
     LZ_HIP_TRY(hipMemcpyAsync(beta + m * bb, binv[(m - 1) & 1], sizeof(float) * bb, hipMemcpyDeviceToDevice, h->stream));
+    if (h->final_state)  // W = W_m (in), Q0 = Q1 = W_{m-1} beta^-1 (prev)
+        LZ_TRY(final_state<float>(h, n, b, nullptr, nullptr, prev, in, binv[(m - 1) & 1], nullptr, nullptr, W, Q0,
+                                  m >= 2 ? Q1 : nullptr));
     return LZ_OK;
 }
 
@@ -358,6 +391,9 @@ static int block_lanczos_sep(lz_handle *h, int64_t n, int64_t nnz, const int64_t
         in = out;
     }
     LZ_HIP_TRY(hipMemcpyAsync(beta + m * bb, binv[(m - 1) & 1], sizeof(T) * bb, hipMemcpyDeviceToDevice, h->stream));
+    if (h->final_state)  // W = W_m (in), Q0 = Q1 = W_{m-1} beta^-1 (prev)
+        LZ_TRY(final_state<T>(h, n, b, nullptr, nullptr, prev, in, binv[(m - 1) & 1], nullptr, nullptr, W, Q0,
+                              m >= 2 ? Q1 : nullptr));
     return LZ_OK;
 }
 
@@ -453,12 +489,27 @@ static int fdtd_block(lz_handle *h, int64_t n, int64_t nnz, const int64_t *rp, c
 
 int attach_comm(lz_handle *h, Comm *c)
 {
-    h->comm = c;
+    // the exchange stream and its events first; the communicator is attached
+    // last, so a failure leaves the handle detached (and c deleted)
+    hipStream_t xs = nullptr;
+    hipEvent_t e1 = nullptr, e2 = nullptr;
+    hipError_t e = hipStreamCreateWithFlags(&xs, hipStreamNonBlocking);
+    if (e == hipSuccess) e = hipEventCreateWithFlags(&e1, hipEventDisableTiming);
+    if (e == hipSuccess) e = hipEventCreateWithFlags(&e2, hipEventDisableTiming);
+    if (e != hipSuccess) {
+        if (e2) (void)hipEventDestroy(e2);
+        if (e1) (void)hipEventDestroy(e1);
+        if (xs) (void)hipStreamDestroy(xs);
+        delete c;
+        set_error("attach_comm: exchange stream / events -> %s", hipGetErrorString(e));
+        return LZ_E_HIP;
+    }
+    h->xstream = xs;
+    h->ev_cx = e1;
+    h->ev_xd = e2;
     h->nranks = c->nranks;
     h->rank = c->rank;
-    LZ_HIP_TRY(hipStreamCreateWithFlags(&h->xstream, hipStreamNonBlocking));
-    LZ_HIP_TRY(hipEventCreateWithFlags(&h->ev_cx, hipEventDisableTiming));
-    LZ_HIP_TRY(hipEventCreateWithFlags(&h->ev_xd, hipEventDisableTiming));
+    h->comm = c;
     return LZ_OK;
 }
 
@@ -895,8 +946,11 @@ static int dist_solve(lz_handle *h, int form, HaloPlan *hp, int64_t n, int64_t n
                       const int32_t *col, const T *val, int b, int m, int64_t lc, const T *B, T *q, T *alpha, T *beta,
                       T *X0, T *X1)
 {
-    const int rc = dist_solve_impl<T>(h, form, hp, n, n_pad, nnz, rp, col, val, b, m, lc, B, q, alpha, beta, X0, X1);
+    int rc = dist_solve_impl<T>(h, form, hp, n, n_pad, nnz, rp, col, val, b, m, lc, B, q, alpha, beta, X0, X1);
     if (rc != LZ_OK && h->comm) h->comm->abort();
+    // (after the closing fence: every rank has finished its collectives, so a
+    // rank failing here leaves no peer waiting)
+    if (rc == LZ_OK) rc = solve_status(h);
     return rc;
 }
 
@@ -1067,6 +1121,13 @@ int lz_prof_read(lz_handle *h, int cls, double *ms_total, int *count)
     return LZ_OK;
 }
 
+int lz_set_final_state(lz_handle *h, int on)
+{
+    LZ_HANDLE_CHECK(h);
+    h->final_state = on ? 1 : 0;
+    return LZ_OK;
+}
+
 int lz_set_stream(lz_handle *h, void *stream)
 {
     LZ_HANDLE_CHECK(h);
@@ -1104,6 +1165,14 @@ int lz_to_row_major(lz_handle *h, int64_t rows, int b, lz_dtype dtype, const voi
     LZ_ARG_CHECK(X && Y && X != Y, "to_row_major: X, Y distinct, not NULL");
     if (dtype == LZ_F64) return to_row_major<double>(h, rows, b, (const double *)X, ldx, (double *)Y);
     return to_row_major<float>(h, rows, b, (const float *)X, ldx, (float *)Y);
+}
+
+int lz_to_col_major(lz_handle *h, int64_t rows, int b, lz_dtype dtype, const void *X, void *Y, int64_t ldy)
+{
+    LZ_HANDLE_CHECK(h);
+    LZ_ARG_CHECK(X && Y && X != Y, "to_col_major: X, Y distinct, not NULL");
+    if (dtype == LZ_F64) return to_col_major<double>(h, rows, b, (const double *)X, ldy, (double *)Y);
+    return to_col_major<float>(h, rows, b, (const float *)X, ldy, (float *)Y);
 }
 
 int lz_csr_spmv(lz_handle *h, int64_t n_rows, int64_t n_cols, int64_t nnz, const int64_t *rp,
@@ -1220,10 +1289,11 @@ int lz_block_lanczos(lz_handle *h, int64_t n, int64_t nnz, const int64_t *rp, co
 {
     LZ_HANDLE_CHECK(h);
     LZ_TRY(block_args(n, nnz, rp, col, val, b, m, lc, B, q, alpha, beta, Q0, Q1, W));
-    if (dtype == LZ_F64 && b == 16)
-        return block_lanczos_fused16(h, n, nnz, rp, col, (const double *)val, m, lc,
-                                     (const double *)B, (double *)q, (double *)alpha,
-                                     (double *)beta, (double *)Q0, (double *)Q1, (double *)W);
+    if (dtype == LZ_F64 && b == 16) {
+        LZ_TRY(block_lanczos_fused16(h, n, nnz, rp, col, (const double *)val, m, lc, (const double *)B, (double *)q,
+                                     (double *)alpha, (double *)beta, (double *)Q0, (double *)Q1, (double *)W));
+        return solve_status(h);
+    }
     if (dtype == LZ_F64)
         return block_lanczos_sep<double>(h, n, nnz, rp, col, (const double *)val, b, m, lc, (const double *)B,
                                          (double *)q, (double *)alpha, (double *)beta, (double *)Q0, (double *)Q1,
@@ -1464,7 +1534,11 @@ int lz_halo_exchange(lz_handle *h, lz_dtype dtype, int b, void *X)
     HaloPlan &hp = *static_cast<HaloPlan *>(h->halo);
     const size_t rowb = (size_t)b * (dtype == LZ_F64 ? 8 : 4);
     if (h->comm && h->nranks > 1) LZ_TRY(grow_ws(h, &hp.sendbuf, &hp.send_cap, (size_t)std::max<int64_t>(hp.n_send, 1) * rowb));
-    return halo_exchange(h, hp, X, rowb, h->stream);
+    LZ_TRY(halo_exchange(h, hp, X, rowb, h->stream));
+    // after the fence no peer still reads this rank's send buffer: the next
+    // call may repack (or, at a larger b, reallocate) it.  (Inside the solves
+    // the step's all-reduces order the exchanges; they fence once at the end.)
+    return h->comm ? h->comm->fence(h->stream) : LZ_OK;
 }
 
 static int lz_block_lanczos_halo_impl(lz_handle *h, int64_t n_local, int64_t nnz_local, const int64_t *rp,

@@ -33,15 +33,35 @@ public:
     {
         if (c) ncclCommDestroy(c);
     }
+    bool aborted = false;
     const char *kind() const override { return "rccl"; }
+    // a failing rank aborts its communicator: RCCL operations in flight on it
+    // (a peer's included, once the peers see the failed connection) return
+    // instead of waiting, and every later call here fails
+    void abort() override
+    {
+        if (c && !aborted) (void)ncclCommAbort(c);
+        if (c) c = nullptr;
+        aborted = true;
+    }
+    int usable() const
+    {
+        if (!c || aborted) {
+            set_error("RCCL communicator aborted");
+            return LZ_E_COMM;
+        }
+        return LZ_OK;
+    }
     int allreduce_sum(double *buf, size_t count, hipStream_t s) override
     {
+        LZ_TRY(usable());
         LZ_NCCL_CHECK(ncclAllReduce(buf, buf, count, ncclDouble, ncclSum, c, s));
         return LZ_OK;
     }
     int allgather(const void *send, void *X, size_t slot_bytes, hipStream_t s) override
     {
         // in place when send is this rank's slot (RCCL then copies nothing locally)
+        LZ_TRY(usable());
         if (slot_bytes % 8 == 0)
             LZ_NCCL_CHECK(ncclAllGather(send, X, slot_bytes / 8, ncclDouble, c, s));
         else
@@ -50,6 +70,7 @@ public:
     }
     int exchange(const P2POp *ops, int nops, hipStream_t s) override
     {
+        LZ_TRY(usable());
         LZ_NCCL_CHECK(ncclGroupStart());
         ncclResult_t r = ncclSuccess;
         for (int i = 0; i < nops && r == ncclSuccess; ++i) {

@@ -82,6 +82,9 @@ struct lz_handle {
     hipStream_t xstream = nullptr;
     hipEvent_t ev_cx = nullptr, ev_xd = nullptr;
     int64_t last_split[2] = {-1, -1};  // lz_debug_last_split
+    // lz_block_lanczos leaves Q0 = Q1 = Q_{m-1}, W = W_m as the reference does
+    // (one row-local pass per solve); lz_set_final_state(h, 0) skips that pass
+    int final_state = 1;
     // fixed-nnz SpMM format (experiment, lz_spmm.hip fnz_prepare): the operator's
     // columns with row-end flags and each tile's first row, keyed by the operator
     void *c16buf = nullptr;       // pass 1's 16-bit columns (col16_plan), nnz int16

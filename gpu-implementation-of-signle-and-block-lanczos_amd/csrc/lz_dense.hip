@@ -1008,6 +1008,108 @@ int tsmm(lz_handle *h, int64_t n, int b, T sw, T sq, const T *Q, const T *S, T *
     return LZ_OK;
 }
 
+// ============================================================ final state
+// The state block_lanczos_blas leaves behind (methods/block_lanczos.hpp:145,
+// 159, 162): Q0 = Q1 = Q_{m-1} and W = the last residual W_m.  The Q-free steps
+// never store Q, so one row-local pass after the last step makes them:
+//   Q = Vq binv                              into Q0 and (Q1 != null) Q1;
+//   W = Y binv - Vp P1 - Vq P2  (Y != null; the wavefront form, Vp may be null)
+//     or W = Wm (copied unless Wm == Wout).
+// Inputs and outputs may alias (every buffer is row-local: a tile's rows are
+// staged in LDS before any of them is written).  b <= 32.
+template <typename T>
+__global__ __launch_bounds__(256) void k_final_state(int64_t n, int b, const T *Y, const T *Vp, const T *Vq,
+                                                     const T *Wm, const T *__restrict__ binv,
+                                                     const T *__restrict__ P1, const T *__restrict__ P2, T *Wout,
+                                                     T *Q0, T *Q1)
+{
+    constexpr int TR = 16, MB = 32;
+    __shared__ T mb[3][MB * MB];
+    __shared__ T rs[3][TR * MB];  // the tile's Vq, then Y / Vp (or Wm) rows
+    const int tid = threadIdx.x, bb = b * b;
+    for (int e = tid; e < bb; e += 256) {
+        mb[0][e] = binv[e];
+        mb[1][e] = P1 ? P1[e] : T(0);
+        mb[2][e] = P2 ? P2[e] : T(0);
+    }
+    XcdSched s(ceil_div(n, TR));
+    for (int64_t u = s.begin; u < s.end; u += s.step) {
+        const int64_t r0 = u * TR;
+        const int nr = (int)(n - r0 < TR ? n - r0 : TR), ne = nr * b;
+        __syncthreads();  // the previous tile's rows are no longer read
+        for (int e = tid; e < ne; e += 256) {
+            const int64_t g = r0 * b + e;
+            rs[0][e] = Vq[g];
+            rs[1][e] = Y ? Y[g] : Wm[g];
+            rs[2][e] = Vp ? Vp[g] : T(0);
+        }
+        __syncthreads();  // every row of the tile read before any is written
+        for (int e = tid; e < ne; e += 256) {
+            const int r = e / b, j = e % b;
+            const T *vq = &rs[0][r * b], *y = &rs[1][r * b], *vp = &rs[2][r * b];
+            T q = T(0), a = T(0), c = T(0), d = T(0);
+            for (int i = 0; i < b; ++i) {
+                q = fma(vq[i], mb[0][i * b + j], q);
+                a = fma(y[i], mb[0][i * b + j], a);
+                c = fma(vp[i], mb[1][i * b + j], c);
+                d = fma(vq[i], mb[2][i * b + j], d);
+            }
+            const int64_t g = r0 * b + e;
+            if (Y) Wout[g] = (a - c) - d;
+            else if (Wm != Wout) Wout[g] = y[j];
+            Q0[g] = q;
+            if (Q1) Q1[g] = q;
+        }
+    }
+}
+
+template <typename T>
+int final_state(lz_handle *h, int64_t n, int b, const T *Y, const T *Vp, const T *Vq, const T *Wm, const T *binv,
+                const T *P1, const T *P2, T *Wout, T *Q0, T *Q1)
+{
+    LZ_ARG_CHECK(b >= 1 && b <= 32 && Vq && binv && Wout && Q0 && (Y ? P2 != nullptr : Wm != nullptr),
+                 "final state (internal)");
+    if (n <= 0) return LZ_OK;
+    const int grid = (int)std::max<int64_t>(1, std::min<int64_t>(ceil_div(n, 16), (int64_t)h->n_cu * 4));
+    hipLaunchKernelGGL((k_final_state<T>), dim3(grid), dim3(256), 0, h->stream, n, b, Y, Vp, Vq, Wm, binv, P1, P2,
+                       Wout, Q0, Q1);
+    LZ_LAUNCH_CHECK();
+    return LZ_OK;
+}
+
+// row-major rows x b (ld b) -> column-major (leading dimension ld >= rows), a
+// 64-row tile through LDS: coalesced reads, one column piece of 64 per store
+template <typename T>
+__global__ __launch_bounds__(256) void k_rm_to_cm(int64_t rows, int b, const T *__restrict__ src, int64_t ld,
+                                                  T *__restrict__ dst)
+{
+    constexpr int TR = 64;
+    __shared__ T t[TR * kMaxB];
+    const int tid = threadIdx.x;
+    for (int64_t u = blockIdx.x; u * TR < rows; u += gridDim.x) {
+        const int64_t r0 = u * TR;
+        const int nr = (int)(rows - r0 < TR ? rows - r0 : TR);
+        __syncthreads();
+        for (int e = tid; e < nr * b; e += 256) t[e] = src[r0 * b + e];
+        __syncthreads();
+        for (int e = tid; e < nr * b; e += 256) {
+            const int c = e / nr, r = e % nr;
+            dst[(int64_t)c * ld + r0 + r] = t[r * b + c];
+        }
+    }
+}
+
+template <typename T>
+int to_col_major(lz_handle *h, int64_t rows, int b, const T *src, int64_t ld, T *dst)
+{
+    LZ_ARG_CHECK(b >= 1 && b <= kMaxB && ld >= rows && src != dst, "to_col_major shape");
+    if (rows <= 0) return LZ_OK;
+    const int grid = (int)std::max<int64_t>(1, std::min<int64_t>(ceil_div(rows, 64), (int64_t)h->n_cu * 4));
+    hipLaunchKernelGGL((k_rm_to_cm<T>), dim3(grid), dim3(256), 0, h->stream, rows, b, src, ld, dst);
+    LZ_LAUNCH_CHECK();
+    return LZ_OK;
+}
+
 // ================================================================ row probe
 template <typename T>
 __global__ void k_copy_row(int b, const T *__restrict__ Q, int64_t ld, int col_major, int64_t lc,
@@ -1033,7 +1135,10 @@ int copy_row(lz_handle *h, int b, const T *Q, int64_t ld, int col_major, int64_t
     template int sqrtm_pair<T>(lz_handle *, int, const T *, int, T *, T *, T *, const double *, const T *, T *,  \
                                const WfAlpha *);\
     template int tsmm<T>(lz_handle *, int64_t, int, T, T, const T *, const T *, T *, int64_t); \
-    template int copy_row<T>(lz_handle *, int, const T *, int64_t, int, int64_t, T *);
+    template int copy_row<T>(lz_handle *, int, const T *, int64_t, int, int64_t, T *);             \
+    template int final_state<T>(lz_handle *, int64_t, int, const T *, const T *, const T *, const T *, const T *, \
+                                const T *, const T *, T *, T *, T *);                             \
+    template int to_col_major<T>(lz_handle *, int64_t, int, const T *, int64_t, T *);
 LZ_DENSE_INST(double)
 LZ_DENSE_INST(float)
 

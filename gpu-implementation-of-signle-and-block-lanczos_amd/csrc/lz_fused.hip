@@ -1547,6 +1547,11 @@ int vector_lanczos_dev(lz_handle *h, int64_t n, int64_t nnz, const int64_t *rp, 
         wcur = wnext;
         wi ^= 1;
     }
+    // the reference's post-call state (vector_lanczos.hpp:60,62): q0 = q1 =
+    // q_{m-1} (q0 already holds it; q1 untouched at m = 1) and w = the last
+    // residual, which alternated between w and q1
+    if (wcur != w) LZ_HIP_TRY(hipMemcpyAsync(w, wcur, sizeof(T) * (size_t)n, hipMemcpyDeviceToDevice, h->stream));
+    if (m >= 2) LZ_HIP_TRY(hipMemcpyAsync(q1, q0, sizeof(T) * (size_t)n, hipMemcpyDeviceToDevice, h->stream));
     return LZ_OK;
 }
 

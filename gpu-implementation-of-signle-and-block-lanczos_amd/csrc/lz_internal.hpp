@@ -53,6 +53,15 @@ template <typename T>
 int tsmm(lz_handle *h, int64_t n, int b, T sw, T sq, const T *Q, const T *S, T *W, int64_t ld);
 template <typename T>
 int copy_row(lz_handle *h, int b, const T *Q, int64_t ld, int col_major, int64_t lc, T *q);
+// the reference's post-call state (block_lanczos.hpp:145,159,162): Q0 (and Q1
+// when non-null) = Vq binv; W = Y binv - Vp P1 - Vq P2 (Y != null; Vp may be
+// null) or W = Wm.  Row-local: inputs may alias outputs.  b <= 32.
+template <typename T>
+int final_state(lz_handle *h, int64_t n, int b, const T *Y, const T *Vp, const T *Vq, const T *Wm, const T *binv,
+                const T *P1, const T *P2, T *Wout, T *Q0, T *Q1);
+// row-major rows x b (ld b) -> column-major with leading dimension ld >= rows
+template <typename T>
+int to_col_major(lz_handle *h, int64_t rows, int b, const T *src, int64_t ld, T *dst);
 
 // ---- fused block-Lanczos passes, b = 16 fp64 (lz_fused.hip)
 // Q-free form: Q_j = W_j beta_j^-1 is formed in registers wherever it is used

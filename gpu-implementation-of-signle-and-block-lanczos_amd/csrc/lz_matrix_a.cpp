@@ -3,7 +3,8 @@
 // helpers of matrix_a/build_ell_utils.hpp and Ell_matrix::mult_diagonal,
 // objects/ell_matrix.hpp:340-361), reproducing the reference's floating-point
 // operation order so the values are bit-identical (checked against the
-// reference's own host code in tests/test_matrix_a.py).
+// reference's own host code compiled in place: tests/test_host.py and
+// tests/test_oracle.py against oracle/_ref).
 //
 // Storage: "ELL, column-major slots" like the reference before change_order:
 // slot s of row r at r + s*n_rows, uint32 column index, explicit zeros kept.

@@ -333,9 +333,17 @@ __global__ __launch_bounds__(64 * (NC + NL + NU)) void k_wf16(
             // they are written (in L2 / the MALL), not a region later.  lead
             // exceeds the tiles a pass-1 tile reaches ahead, so the pass-1
             // tiles the wait is for never wait on this wave (no cycle).
+            // A region whose pass-1 range starts more than hback tiles after its
+            // pass-2 range (region 0 of a distributed rank's interior launch, whose
+            // pass 1 starts at p1a while its pass 2 starts at tile 0) counts its
+            // pace from the pass-1 start: the host's lead covers an offset of
+            // hback between the two ranges, and the first pass-1 tile needs the
+            // pass-2 tiles at block positions up to (p1a + hfwd) / KB.
+            const int64_t gap = begin - pbeg - hback;
+            const int64_t poff = gap > 0 ? (gap + KB - 1) / KB : 0;
             int64_t paced = -1;  // last tile cleared
             auto pace = [&](int64_t s) {
-                const int64_t m = uw + (s / NC) * NU;
+                const int64_t m = uw + (s / NC) * NU - poff;
                 if (s >= ns || s / NC <= paced) return;
                 paced = s / NC;
                 const uint32_t pa = ws_lds_addr(&p1pub);
@@ -730,13 +738,53 @@ int wf_step16(lz_handle *h, int64_t n, const int64_t *rp, const int32_t *col, co
     // (C3: 1.74-1.81 -> 1.69-1.70 ms; 8, nt on V_{j+1}, 1.84)
     const char *cp = getenv("LZ_WF_CPOL");
     const int cpol = cp ? atoi(cp) : 7;
+    // Liveness needs every block resident at once (their waits on each other's
+    // flags).  The launch is checked: the occupancy of the instantiation at its
+    // block size must admit the grid, and by default it goes out as a
+    // cooperative launch, which the runtime refuses (instead of running part of
+    // the grid later) when the grid cannot be resident.  LZ_WF_COOP=0: an
+    // ordinary launch after the same occupancy check (A/B).
+    const char *co = getenv("LZ_WF_COOP");
+    const bool coop = !(co && co[0] == '0');
+    int rc = LZ_OK;
     const int ev = prof_begin(h, PROF_SPMM_PASS);
     // (the block is 64 (NC + NL + NU) threads: the kernel refuses any other size)
     auto go = [&](auto kern, int waves) {
-        hipLaunchKernelGGL(kern, dim3(grid), dim3(64 * waves), 0, h->stream, n, rp, col, col16, val,
-                           pairs, Yj, Vprev, Vj, Vout, binv, P1, P2, Vg, Yo,
-                           static_cast<const int2 *>(h->wf_deps), h->wf_flags, epoch, (int64_t)pl.hback, lead,
-                           part, h->err_flag, dbg, nx, p1a, p1b, T, cpol);
+        static int occ = -1;  // blocks per CU of this instantiation (per process: one device model)
+        if (occ < 0 && hipOccupancyMaxActiveBlocksPerMultiprocessor(&occ, kern, 64 * waves, 0) != hipSuccess)
+            occ = 0;
+        if ((int64_t)grid > (int64_t)occ * h->n_cu) {
+            set_error("wavefront step: %d blocks of %d threads cannot all be resident (%d per CU x %d CUs)", grid,
+                      64 * waves, occ, h->n_cu);
+            rc = LZ_E_HIP;
+            return;
+        }
+        const int2 *deps = static_cast<const int2 *>(h->wf_deps);
+        int *flags = h->wf_flags, *err = h->err_flag;
+        int64_t a_n = n, a_hb = pl.hback, a_nx = nx, a_p1a = p1a, a_p1b = p1b, a_T = T;
+        int a_ep = epoch, a_lead = lead, a_dbg = dbg, a_cp = cpol;
+        const int64_t *a_rp = rp;
+        const int32_t *a_col = col;
+        const int16_t *a_c16 = col16;
+        const double *a_val = val, *a_Yj = Yj, *a_Vp = Vprev, *a_Vj = Vj, *a_bi = binv, *a_P1 = P1, *a_P2 = P2,
+                     *a_Vg = Vg;
+        const uint64_t *a_pr = pairs;
+        double *a_Vo = Vout, *a_Yo = Yo, *a_part = part;
+        if (coop) {
+            void *args[] = {&a_n,  &a_rp, &a_col, &a_c16, &a_val, &a_pr,    &a_Yj, &a_Vp,  &a_Vj, &a_Vo,
+                            &a_bi, &a_P1, &a_P2,  &a_Vg,  &a_Yo,  &deps,    &flags, &a_ep, &a_hb, &a_lead,
+                            &a_part, &err, &a_dbg, &a_nx, &a_p1a, &a_p1b, &a_T,   &a_cp};
+            const hipError_t e = hipLaunchCooperativeKernel(reinterpret_cast<const void *>(kern), dim3(grid),
+                                                            dim3(64 * waves), args, 0, h->stream);
+            if (e != hipSuccess) {
+                set_error("wavefront step: cooperative launch of %d blocks -> %s", grid, hipGetErrorString(e));
+                rc = LZ_E_HIP;
+            }
+            return;
+        }
+        hipLaunchKernelGGL(kern, dim3(grid), dim3(64 * waves), 0, h->stream, a_n, a_rp, a_col, a_c16, a_val, a_pr,
+                           a_Yj, a_Vp, a_Vj, a_Vo, a_bi, a_P1, a_P2, a_Vg, a_Yo, deps, flags, a_ep, a_hb, a_lead,
+                           a_part, err, a_dbg, a_nx, a_p1a, a_p1b, a_T, a_cp);
     };
     // LDS (<= 160 KB): strip slots per updater DU + 1, fewer with 32-bit columns
     constexpr int cap12 = 12 * 16 * kWfCapPerRow, cap11 = 11 * 16 * kWfCapPerRow, cap10 = 10 * 16 * kWfCapPerRow;
@@ -755,6 +803,7 @@ int wf_step16(lz_handle *h, int64_t n, const int64_t *rp, const int32_t *col, co
         else go(k_wf16<10, cap10, kWfK, kWfNL, 4, 1, false>, 10 + kWfNL + 4);
     }
     prof_end(h, ev);
+    LZ_TRY(rc);
     LZ_LAUNCH_CHECK();
     *nparts = grid;
     return LZ_OK;

@@ -36,7 +36,9 @@ enum {
     LZ_E_ARG = -1,      /* invalid argument (shape, null pointer, unsupported b/dtype) */
     LZ_E_HIP = -2,      /* HIP runtime error (includes "no device") */
     LZ_E_COMM = -3,     /* RCCL error */
-    LZ_E_STATE = -4     /* handle not initialised / wrong call order */
+    LZ_E_STATE = -4,    /* handle not initialised / wrong call order */
+    LZ_E_DEVICE = -5    /* a persistent kernel abandoned a bounded wait (lz_device_error
+                           gives its code); the call's results are invalid */
 };
 
 typedef struct lz_handle lz_handle;  /* opaque */
@@ -48,6 +50,9 @@ typedef struct lz_handle lz_handle;  /* opaque */
 int lz_init(int device, lz_handle **h);
 int lz_finalize(lz_handle *h);
 int lz_set_stream(lz_handle *h, void *hip_stream);
+/* 1 (default): lz_block_lanczos / lz_block_lanczos_unfused leave Q0, Q1, W as
+ * the reference does (see lz_block_lanczos); 0: they are scratch on return. */
+int lz_set_final_state(lz_handle *h, int on);
 const char *lz_last_error(void);
 const char *lz_version(void);
 /* 1 when a gfx950 device is visible and the code object loads on it. */
@@ -96,6 +101,11 @@ int lz_csr_spmm(lz_handle *h, int64_t n_rows, int64_t n_cols, int64_t nnz,
  * start block into the row-major iteration once. */
 int lz_to_row_major(lz_handle *h, int64_t rows, int b, lz_dtype dtype, const void *X, int64_t ldx, void *Y);
 
+/* The inverse: Y (rows x b, COLUMN-major, leading dimension ldy >= rows) = X
+ * (rows x b, row-major, ld = b).  lz_methods.hpp uses it to hand the final
+ * Q0 / Q1 / W blocks back in the caller's column-major layout. */
+int lz_to_col_major(lz_handle *h, int64_t rows, int b, lz_dtype dtype, const void *X, void *Y, int64_t ldy);
+
 /* y = A*x  (spmv, kernels/spmv_spmm.hpp:209-260) */
 int lz_csr_spmv(lz_handle *h, int64_t n_rows, int64_t n_cols, int64_t nnz,
                 const int64_t *row_ptr, const int32_t *col, const void *val, lz_dtype dtype,
@@ -140,10 +150,22 @@ int lz_copy_row(lz_handle *h, int b, lz_dtype dtype, const void *Q, int64_t ld, 
  *   q[m*b]          row lc of Q_0..Q_{m-1}
  *   alpha[m*b*b]    alpha_j
  *   beta[(m+1)*b*b] beta_0 = sqrtm(B^T B), beta_j (j=1..m-1), beta_m = last inverse sqrt
- * B, Q0, Q1, W: n x b row-major (ld = b), device.  B is read only; Q0/Q1/W are
- * workspace (the reference passes them pre-set to B; their input content is
- * ignored here).  Fused device-resident iteration: no host synchronisation
- * inside; every output stays on the device. */
+ * B, Q0, Q1, W: n x b row-major (ld = b), device.  B is read only.  Q0/Q1/W
+ * are workspace during the call (the reference passes them pre-set to B; their
+ * input content is ignored here) and on return hold what the reference leaves
+ * in them (block_lanczos.hpp:145,159,162): Q0 = Q1 = Q_{m-1} (the last
+ * normalised Krylov block; Q1 is not written when m = 1) and W = the last
+ * residual A Q_{m-1} - Q_{m-2} beta_{m-1} - Q_{m-1} alpha_{m-1} (unnormalised).
+ * That costs one row-local pass per call; lz_set_final_state(h, 0) skips it
+ * for callers that never read the three blocks (they are then scratch).
+ * Fused device-resident iteration: no host synchronisation inside the steps;
+ * every output stays on the device.  At b = 16 fp64 the call ends with one
+ * host synchronisation, to read the device error word of the step kernels
+ * (LZ_E_DEVICE when one of them abandoned a bounded wait).
+ * The b = 16 fp64 step kernels keep one workgroup on every CU and their
+ * workgroups wait on each other's progress: the launch is checked for
+ * co-residency, and no kernel that itself waits on the solve's results may
+ * run beside it on the device. */
 int lz_block_lanczos(lz_handle *h, int64_t n, int64_t nnz, const int64_t *row_ptr,
                      const int32_t *col, const void *val, lz_dtype dtype, int b, int m,
                      int64_t lc, const void *B, void *q, void *alpha, void *beta, void *Q0,

@@ -285,12 +285,54 @@ const T *row_major_block(const Dense_matrix<T> &B, int64_t n, DeviceArray<T> &tm
 }
 
 // workspace blocks may come in either layout (the reference allocates Q0, Q1, W
-// like B): only their capacity matters, their content is overwritten
+// like B): their input content is ignored; on return they hold what the
+// reference leaves in them (Q0 = Q1 = Q_{m-1}, W = the last residual), in
+// their own layout
 template <typename T>
 void check_workspace(const Dense_matrix<T> &X, int64_t n, int b, const char *who)
 {
-    const int64_t cap = X.layout() == LZ_ROW_MAJOR ? X.n_rows() * X.ld() : (int64_t)X.n_cols() * X.ld();
-    if (cap < n * b) throw std::runtime_error(std::string(who) + ": workspace block smaller than n x b");
+    if (X.n_cols() != b || X.n_rows() < n || X.ld() < (X.layout() == LZ_ROW_MAJOR ? (int64_t)b : X.n_rows()))
+        throw std::runtime_error(std::string(who) + ": workspace block is not n x b");
+}
+
+// the iteration writes row-major n x b blocks (ld = b): a caller block in that
+// exact layout is used in place, any other gets a row-major temporary
+template <typename T>
+bool row_major_dense(const Dense_matrix<T> &X)
+{
+    return X.layout() == LZ_ROW_MAJOR && X.ld() == X.n_cols();
+}
+
+// the final n x b row-major block `src` into the caller's block X
+template <typename T>
+void store_block(Dense_matrix<T> &X, const T *src, int64_t n, int b, Context &ctx, const char *who)
+{
+    if (X.layout() == LZ_COL_MAJOR) {
+        check(lz_to_col_major(ctx.get(), n, b, dtype_of<T>(), src, X.data(), X.ld()), who);
+        return;
+    }
+    hip_check(hipMemcpy2DAsync(X.data(), sizeof(T) * X.ld(), src, sizeof(T) * b, sizeof(T) * b, n,
+                               hipMemcpyDeviceToDevice, ctx.stream()),
+              who);
+}
+
+// run `call(Q0, Q1, W)` on row-major n x b blocks and leave its final blocks in
+// the caller's (m == 1: the reference does not write Q1)
+template <typename T, typename F>
+void with_final_blocks(Dense_matrix<T> &Q0, Dense_matrix<T> &Q1, Dense_matrix<T> &W, int64_t n, int b, unsigned m,
+                       Context &ctx, const char *who, F call)
+{
+    for (Dense_matrix<T> *X : {&Q0, &Q1, &W}) check_workspace(*X, n, b, who);
+    if (row_major_dense(Q0) && row_major_dense(Q1) && row_major_dense(W)) {
+        call(Q0.data(), Q1.data(), W.data());
+        return;
+    }
+    DeviceArray<T> t0((size_t)n * b), t1((size_t)n * b), t2((size_t)n * b);
+    call(t0.data(), t1.data(), t2.data());
+    store_block(Q0, t0.data(), n, b, ctx, who);
+    if (m >= 2) store_block(Q1, t1.data(), n, b, ctx, who);
+    store_block(W, t2.data(), n, b, ctx, who);
+    ctx.synchronize();  // t0..t2 are released on return
 }
 
 // block_lanczos_blas (methods/block_lanczos.hpp:88-167).  alpha: array of m
@@ -312,11 +354,12 @@ void block_lanczos_blas(const Csr_matrix<T> &A, const Dense_matrix<T> &B, unsign
     if (q.size() < (int64_t)m * b) throw std::runtime_error("block_lanczos_blas: q needs m*b entries");
     DeviceArray<T> Bt;
     const T *Bp = row_major_block(B, n, Bt, ctx, "block_lanczos_blas");
-    for (Dense_matrix<T> *X : {&Q0, &Q1, &W}) check_workspace(*X, n, b, "block_lanczos_blas");
     DeviceArray<T> al((size_t)m * bb), be((size_t)(m + 1) * bb);
-    check(lz_block_lanczos(ctx.get(), n, A.nnz(), A.row_ptr(), A.col(), A.val(), dtype_of<T>(), b, (int)m, lc,
-                           Bp, q.data(), al.data(), be.data(), Q0.data(), Q1.data(), W.data()),
-          "block_lanczos_blas");
+    with_final_blocks(Q0, Q1, W, n, b, m, ctx, "block_lanczos_blas", [&](T *q0, T *q1, T *w) {
+        check(lz_block_lanczos(ctx.get(), n, A.nnz(), A.row_ptr(), A.col(), A.val(), dtype_of<T>(), b, (int)m, lc,
+                               Bp, q.data(), al.data(), be.data(), q0, q1, w),
+              "block_lanczos_blas");
+    });
     // scatter into the caller's per-step matrices (device to device, on the stream)
     for (unsigned j = 0; j < m; ++j)
         hip_check(hipMemcpyAsync(alpha[j].data(), al.data() + j * bb, sizeof(T) * bb, hipMemcpyDeviceToDevice,
@@ -339,11 +382,12 @@ void block_lanczos_blas_reference_order(const Csr_matrix<T> &A, const Dense_matr
     const int64_t n = A.n_rows(), bb = (int64_t)b * b;
     DeviceArray<T> Bt;
     const T *Bp = row_major_block(B, n, Bt, ctx, "block_lanczos_blas_reference_order");
-    for (Dense_matrix<T> *X : {&Q0, &Q1, &W}) check_workspace(*X, n, b, "block_lanczos_blas_reference_order");
     DeviceArray<T> al((size_t)m * bb), be((size_t)(m + 1) * bb);
-    check(lz_block_lanczos_unfused(ctx.get(), n, A.nnz(), A.row_ptr(), A.col(), A.val(), dtype_of<T>(), b, (int)m,
-                                   lc, Bp, q.data(), al.data(), be.data(), Q0.data(), Q1.data(), W.data()),
-          "block_lanczos_blas_reference_order");
+    with_final_blocks(Q0, Q1, W, n, b, m, ctx, "block_lanczos_blas_reference_order", [&](T *q0, T *q1, T *w) {
+        check(lz_block_lanczos_unfused(ctx.get(), n, A.nnz(), A.row_ptr(), A.col(), A.val(), dtype_of<T>(), b,
+                                       (int)m, lc, Bp, q.data(), al.data(), be.data(), q0, q1, w),
+              "block_lanczos_blas_reference_order");
+    });
     for (unsigned j = 0; j < m; ++j)
         hip_check(hipMemcpyAsync(alpha[j].data(), al.data() + j * bb, sizeof(T) * bb, hipMemcpyDeviceToDevice,
                                  ctx.stream()), "alpha copy");

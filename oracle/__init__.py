@@ -41,6 +41,10 @@ def lib():
             "lzo_sqrtm_pair": (_c_int, [_c_int, _c_vp, _c_vp, _c_vp]),
             "lzo_block_lanczos": (_c_int, [_c_i64, _c_vp, _c_vp, _c_vp, _c_int, _c_int, _c_i64, _c_vp, _c_vp, _c_vp, _c_vp]),
             "lzo_block_lanczos_f32": (_c_int, [_c_i64, _c_vp, _c_vp, _c_vp, _c_int, _c_int, _c_i64, _c_vp, _c_vp, _c_vp, _c_vp]),
+            "lzo_block_lanczos_final": (_c_int, [_c_i64, _c_vp, _c_vp, _c_vp, _c_int, _c_int, _c_i64, _c_vp, _c_vp,
+                                                 _c_vp, _c_vp, _c_vp, _c_vp]),
+            "lzo_block_lanczos_final_f32": (_c_int, [_c_i64, _c_vp, _c_vp, _c_vp, _c_int, _c_int, _c_i64, _c_vp,
+                                                     _c_vp, _c_vp, _c_vp, _c_vp, _c_vp]),
             "lzo_vector_lanczos": (_c_int, [_c_i64, _c_vp, _c_vp, _c_vp, _c_int, _c_i64, _c_vp, _c_vp, _c_vp, _c_vp]),
             "lzo_vector_lanczos_f32": (_c_int, [_c_i64, _c_vp, _c_vp, _c_vp, _c_int, _c_i64, _c_vp, _c_vp, _c_vp,
                                                 _c_vp]),
@@ -120,6 +124,29 @@ def block_lanczos(A, B: np.ndarray, m: int, lc: int):
     if rc:
         raise RuntimeError(f"lzo_block_lanczos rc={rc}")
     return q, alpha, beta
+
+
+def block_lanczos_final(A, B: np.ndarray, m: int, lc: int):
+    """block_lanczos plus the final Q0 (= Q1 = Q_{m-1}) and W (last residual)
+    the reference leaves in its arguments: (q, alpha, beta, Qf, Wf)."""
+    rp, col, val = _csr(A)
+    B = np.ascontiguousarray(B)
+    n, b = B.shape
+    dt = B.dtype
+    q = np.zeros(m * b, dt)
+    alpha = np.zeros((m, b, b), dt)
+    beta = np.zeros((m + 1, b, b), dt)
+    Qf = np.zeros((n, b), dt)
+    Wf = np.zeros((n, b), dt)
+    if dt == np.float32:
+        rc = lib().lzo_block_lanczos_final_f32(n, _p(rp), _p(col), _p(val.astype(np.float32)), b, m, lc, _p(B),
+                                               _p(q), _p(alpha), _p(beta), _p(Qf), _p(Wf))
+    else:
+        rc = lib().lzo_block_lanczos_final(n, _p(rp), _p(col), _p(val.astype(np.float64)), b, m, lc, _p(B),
+                                           _p(q), _p(alpha), _p(beta), _p(Qf), _p(Wf))
+    if rc:
+        raise RuntimeError(f"lzo_block_lanczos_final rc={rc}")
+    return q, alpha, beta, Qf, Wf
 
 
 def vector_lanczos(A, bvec: np.ndarray, m: int, lc: int):

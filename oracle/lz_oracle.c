@@ -183,21 +183,36 @@ int lzo_sqrtm_pair(int b, const double *G, double *beta, double *beta_inv)
 int lzo_block_lanczos(int64_t n, const int64_t *rp, const int32_t *col, const double *val, int b,
                       int m, int64_t lc, const double *B, double *q, double *alpha, double *beta)
 {
-    return block_lanczos_impl_f64(n, rp, col, val, b, m, lc, B, q, alpha, beta, NULL);
+    return block_lanczos_impl_f64(n, rp, col, val, b, m, lc, B, q, alpha, beta, NULL, NULL, NULL);
 }
 
 int lzo_block_lanczos_f32(int64_t n, const int64_t *rp, const int32_t *col, const float *val,
                           int b, int m, int64_t lc, const float *B, float *q, float *alpha,
                           float *beta)
 {
-    return block_lanczos_impl_f32(n, rp, col, val, b, m, lc, B, q, alpha, beta, NULL);
+    return block_lanczos_impl_f32(n, rp, col, val, b, m, lc, B, q, alpha, beta, NULL, NULL, NULL);
+}
+
+/* the same, plus the final Q0 (= Q1) and W blocks the reference leaves behind */
+int lzo_block_lanczos_final(int64_t n, const int64_t *rp, const int32_t *col, const double *val, int b,
+                            int m, int64_t lc, const double *B, double *q, double *alpha, double *beta,
+                            double *Qf, double *Wf)
+{
+    return block_lanczos_impl_f64(n, rp, col, val, b, m, lc, B, q, alpha, beta, NULL, Qf, Wf);
+}
+
+int lzo_block_lanczos_final_f32(int64_t n, const int64_t *rp, const int32_t *col, const float *val, int b,
+                                int m, int64_t lc, const float *B, float *q, float *alpha, float *beta,
+                                float *Qf, float *Wf)
+{
+    return block_lanczos_impl_f32(n, rp, col, val, b, m, lc, B, q, alpha, beta, NULL, Qf, Wf);
 }
 
 int lzo_block_lanczos_timed(int64_t n, const int64_t *rp, const int32_t *col, const double *val, int b,
                             int m, int64_t lc, const double *B, double *q, double *alpha, double *beta,
                             double *t_each)
 {
-    return block_lanczos_impl_f64(n, rp, col, val, b, m, lc, B, q, alpha, beta, t_each);
+    return block_lanczos_impl_f64(n, rp, col, val, b, m, lc, B, q, alpha, beta, t_each, NULL, NULL);
 }
 
 /* ------------------------------------------------- single-vector Lanczos
@@ -278,7 +293,7 @@ int lzo_vector_lanczos_timed(int64_t n, const int64_t *rp, const int32_t *col, c
 int lzo_block_lanczos_f32_timed(int64_t n, const int64_t *rp, const int32_t *col, const float *val, int b, int m,
                                 int64_t lc, const float *B, float *q, float *alpha, float *beta, double *t_each)
 {
-    return block_lanczos_impl_f32(n, rp, col, val, b, m, lc, B, q, alpha, beta, t_each);
+    return block_lanczos_impl_f32(n, rp, col, val, b, m, lc, B, q, alpha, beta, t_each, NULL, NULL);
 }
 
 /* vector_lanczos<float> (methods/vector_lanczos.hpp:8-67 at T = float, as

@@ -56,6 +56,16 @@ int lzo_block_lanczos_f32(int64_t n, const int64_t *row_ptr, const int32_t *col,
                           const float *val, int b, int m, int64_t lc, const float *B,
                           float *q, float *alpha, float *beta);
 
+/* lzo_block_lanczos plus the blocks the reference leaves in its arguments on
+ * return (block_lanczos.hpp:159,162): Qf = Q0 = Q1 = Q_{m-1}, Wf = W (the last
+ * residual, unnormalised); n x b row-major each.  fp64 and fp32. */
+int lzo_block_lanczos_final(int64_t n, const int64_t *row_ptr, const int32_t *col, const double *val,
+                            int b, int m, int64_t lc, const double *B, double *q, double *alpha,
+                            double *beta, double *Qf, double *Wf);
+int lzo_block_lanczos_final_f32(int64_t n, const int64_t *row_ptr, const int32_t *col, const float *val,
+                                int b, int m, int64_t lc, const float *B, float *q, float *alpha,
+                                float *beta, float *Qf, float *Wf);
+
 /* vector_lanczos (methods/vector_lanczos.hpp:8-67, the correct variant).
  * q[m], alpha[m], beta[m] (beta[0] = ||b||). */
 int lzo_vector_lanczos(int64_t n, const int64_t *row_ptr, const int32_t *col, const double *val,

@@ -78,9 +78,12 @@ static void FN(tsmm_rm)(int64_t n, int b, REAL s_w, REAL s_q, const REAL *Q, con
 }
 
 /* block_lanczos_blas, methods/block_lanczos.hpp:104-166, op for op. */
+/* Qf, Wf (optional, n x b): the state the reference leaves in Q0 (= Q1) and W
+ * on return (:159, :162): Q_{m-1} and the last residual W_m. */
 static int FN(block_lanczos_impl)(int64_t n, const int64_t *rp, const int32_t *col,
                                   const REAL *val, int b, int m, int64_t lc, const REAL *B,
-                                  REAL *q, REAL *alpha, REAL *beta, double *t_each)
+                                  REAL *q, REAL *alpha, REAL *beta, double *t_each, REAL *Qf,
+                                  REAL *Wf)
 {
     if (b < 1 || b > 64 || m < 1 || n < 1) return -1;
     const size_t nb = (size_t)n * b, bb = (size_t)b * b;
@@ -127,6 +130,8 @@ static int FN(block_lanczos_impl)(int64_t n, const int64_t *rp, const int32_t *c
         if (t_each) t_each[j - 1] = lzo_wtime() - t0;
     }
     if (beta) for (size_t k = 0; k < bb; ++k) beta[(size_t)m * bb + k] = (REAL)Si[k];
+    if (Qf) memcpy(Qf, Q0, nb * sizeof(REAL));
+    if (Wf) memcpy(Wf, W, nb * sizeof(REAL));
     free(Q0); free(Q1); free(W);
     return 0;
 }

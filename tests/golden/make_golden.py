@@ -36,8 +36,9 @@ def ell_to_csr(n, d, ix, row_major_stride4=False):
     return Csr(n, A.indptr.astype(np.int64), A.indices.astype(np.int32), A.data.astype(np.float64))
 
 
-def numpy_block_lanczos(A, B, m, lc):
-    """Independent restatement (dense numpy) of methods/block_lanczos.hpp:104-166."""
+def numpy_block_lanczos(A, B, m, lc, final=False):
+    """Independent restatement (dense numpy) of methods/block_lanczos.hpp:104-166.
+    final: also return the Q0 (= Q1) and W blocks the reference leaves behind."""
     Ad = sp.csr_matrix((A.val, A.col, A.row_ptr), shape=(A.n, A.n))
 
     def sq(G):
@@ -58,6 +59,8 @@ def numpy_block_lanczos(A, B, m, lc):
         W = W - Q1 @ a
         Q0 = Q1
         al.append(a); be.append(bj); q.append(Q0[lc])
+    if final:
+        return np.concatenate(q), np.array(al), np.array(be), Q0, W
     return np.concatenate(q), np.array(al), np.array(be)
 
 

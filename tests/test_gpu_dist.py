@@ -1,5 +1,6 @@
-"""GPU coverage of the distributed entry points on one device (the driver's
-multi-GPU bench is the only place more ranks run).
+"""GPU coverage of the distributed entry points on one device, at one rank
+(N-rank decompositions on one GPU are in test_gpu_vranks.py, virtual ranks;
+RCCL with more than one peer runs only in the driver's multi-GPU bench).
 
 * lz_block_lanczos_halo / lz_halo_init with no communicator and with a
   one-rank RCCL communicator: the per-step halo exchange, the b x b

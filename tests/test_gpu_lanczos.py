@@ -546,3 +546,86 @@ def test_prof_class_mask(lz, handle, torch_cuda, monkeypatch, wf):
         outs.append((q.cpu().numpy(), al.cpu().numpy(), be.cpu().numpy()))
     assert all(np.array_equal(x, y) for x, y in zip(outs[0], outs[1]))
     assert handle.device_error() == 0
+
+
+@pytest.mark.parametrize("m", [1, 2, 5])
+@pytest.mark.parametrize("path", ["wavefront", "twopass", "unfused", "sep_b4", "b2_f32_b32"])
+def test_block_final_state(lz, orc, handle, torch_cuda, monkeypatch, path, m):
+    """On return Q0 = Q1 = Q_{m-1} and W = the last residual, as the reference
+    leaves them (methods/block_lanczos.hpp:145,159,162; Q1 is not written at
+    m = 1): every step form against the oracle's final blocks."""
+    torch = torch_cuda
+    b, dt = (4, np.float64) if path == "sep_b4" else (32, np.float32) if path == "b2_f32_b32" else (16, np.float64)
+    if path == "twopass":
+        monkeypatch.setenv("LZ_PASS_WF", "0")
+    A = lz.gen_banded(30_011, 10.0, 700, seed=70 + m, dtype=dt)
+    B = lz.uniform_B(A.n, b, seed=71, dtype=dt)
+    lc = 29_000
+    Ad = lz.CsrDevice.from_host(A)
+    kw = dict(dtype=torch.float64 if dt == np.float64 else torch.float32, device="cuda")
+    q, al, be = torch.zeros(m * b, **kw), torch.zeros(m, b, b, **kw), torch.zeros(m + 1, b, b, **kw)
+    Q0, Q1, W = (torch.full((A.n, b), float("nan"), **kw) for _ in range(3))
+    handle.block_lanczos_blas(Ad, torch.from_numpy(B).cuda(), m, lc, q, al, be, Q0, Q1, W,
+                              fused=path != "unfused")
+    torch.cuda.synchronize()
+    assert handle.device_error() == 0
+    qo, ao, bo, Qf, Wf = orc.block_lanczos_final(A, B, m, lc)
+    tol = 1e-8 if dt == np.float64 else 2e-3
+    Qg, Wg = Q0.cpu().numpy(), W.cpu().numpy()
+    assert np.max(np.abs(Qg - Qf)) <= tol * np.abs(Qf).max()
+    assert np.max(np.abs(Wg - Wf)) <= tol * np.abs(Wf).max()
+    if m >= 2:
+        assert np.array_equal(Q1.cpu().numpy(), Qg)
+    else:
+        assert bool(torch.isnan(Q1).all())  # untouched, as the reference's
+    assert np.allclose(al.cpu().numpy(), ao, rtol=tol, atol=tol * np.abs(ao).max())
+
+
+def test_block_final_state_off(lz, orc, handle, torch_cuda):
+    """lz_set_final_state(h, 0): the same alpha / beta / q bits, the blocks are scratch."""
+    torch = torch_cuda
+    A = lz.gen_banded(20_011, 10.0, 500, seed=75)
+    B = lz.uniform_B(A.n, 16, seed=76)
+    m, lc = 4, 77
+    runs = []
+    for on in (True, False):
+        handle.set_final_state(on)
+        try:
+            runs.append(gpu_block(lz, handle, torch, A, B, m, lc))
+        finally:
+            handle.set_final_state(True)
+    for x, y in zip(*runs):
+        assert np.array_equal(x, y)
+
+
+@pytest.mark.parametrize("m", [1, 3, 6])
+def test_vector_final_state(lz, handle, torch_cuda, m):
+    """vector_lanczos leaves q0 = q1 = q_{m-1} and w = the last residual
+    (methods/vector_lanczos.hpp:60,62; q1 untouched at m = 1)."""
+    import scipy.sparse as sp
+    torch = torch_cuda
+    A = lz.gen_banded(20_011, 10.0, 400, seed=80 + m)
+    bv = lz.uniform_B(A.n, 1, seed=81)[:, 0].copy()
+    M = sp.csr_matrix((A.val, A.col, A.row_ptr), shape=(A.n, A.n))
+    b0 = np.linalg.norm(bv)
+    q0 = bv / b0
+    w = M @ q0
+    w = w - (w @ q0) * q0
+    for _ in range(1, m):
+        q1 = w / np.linalg.norm(w)
+        w = M @ q1 - np.linalg.norm(w) * q0
+        w = w - (w @ q1) * q1
+        q0 = q1
+    Ad = lz.CsrDevice.from_host(A)
+    kw = dict(dtype=torch.float64, device="cuda")
+    q, al, be = torch.zeros(m, **kw), torch.zeros(m, **kw), torch.zeros(m, **kw)
+    g0 = torch.zeros(A.n, **kw)
+    g1, gw = (torch.full((A.n,), float("nan"), **kw) for _ in range(2))
+    handle.vector_lanczos(Ad, torch.from_numpy(bv).cuda(), m, 5, q, al, be, g0, g1, gw)
+    torch.cuda.synchronize()
+    assert np.allclose(g0.cpu().numpy(), q0, rtol=1e-9, atol=1e-12 * np.abs(q0).max())
+    assert np.allclose(gw.cpu().numpy(), w, rtol=1e-8, atol=1e-10 * np.abs(w).max())
+    if m >= 2:
+        assert np.array_equal(g1.cpu().numpy(), g0.cpu().numpy())
+    else:
+        assert bool(torch.isnan(g1).all())

@@ -285,3 +285,67 @@ def test_vranks_argument_error_aborts_group(lz, torch_cuda):
     lz.run_virtual_ranks(2, rank_fn)
     assert time.time() - t0 < 60
     assert codes[1] == -1 and codes[0] == -3, codes  # LZ_E_ARG on rank 1, LZ_E_COMM on rank 0
+
+
+def _with_far_entries(lz, A, pairs, v=1e-3):
+    """A plus the symmetric entries (r, c), (c, r) of `pairs`, value v."""
+    import scipy.sparse as sp
+    M = sp.csr_matrix((A.val, A.col, A.row_ptr), shape=(A.n, A.n))
+    r = np.array([p[0] for p in pairs] + [p[1] for p in pairs])
+    c = np.array([p[1] for p in pairs] + [p[0] for p in pairs])
+    M = (M + sp.csr_matrix((np.full(r.size, v), (r, c)), shape=(A.n, A.n))).tocsr()
+    M.sort_indices()
+    return lz.CsrHost(A.n, M.indptr.astype(np.int64), M.indices.astype(np.int32), M.data.astype(np.float64))
+
+
+@pytest.mark.parametrize("nranks", [2, 4])
+def test_vranks_b16_far_head_rows(lz, orc, torch_cuda, nranks):
+    """A banded operator plus a few rows well inside each rank's first half
+    that reference distant rows of the previous rank: the interior starts
+    hundreds of tiles into the rank (the wavefront step's region 0 runs pass 2
+    from tile 0 but pass 1 from there), so its updaters must pace from the
+    pass-1 start, or the interior launch's waits form a cycle (device error 6)."""
+    n = 160_000
+    A = lz.gen_banded(n, 10.0, 500, seed=90 + nranks)
+    bounds = np.array([n * g // nranks for g in range(nranks + 1)], np.int64)
+    pairs = []
+    for g in range(1, nranks):
+        r0, r1 = int(bounds[g]), int(bounds[g + 1])
+        for k, frac in enumerate((0.30, 0.36, 0.41)):  # first half of the rank's rows
+            pairs.append((r0 + int(frac * (r1 - r0)) + k, int(bounds[g - 1]) + 100 + 37 * k))
+    A = _with_far_entries(lz, A, pairs)
+    B = lz.uniform_B(A.n, 16, seed=91)
+    m, lc = 6, n - 1000
+    got, splits = run_dist(lz, torch_cuda, A, B, m, lc, nranks, "halo", bounds=bounds)
+    for g in range(1, nranks):  # the far rows moved the interior start deep into the rank
+        assert splits[g] is not None and splits[g][0] > 0.25 * (bounds[g + 1] - bounds[g]), splits
+    assert_close_run(lz, m, 16, got, orc.block_lanczos(A, B, m, lc))
+
+
+def test_vranks_halo_exchange_back_to_back(lz, torch_cuda):
+    """Two lz_halo_exchange calls in a row, the second at a larger b (its send
+    buffer is reallocated): each fills every halo row with its owner's row of
+    that call's block (no peer reads a repacked or freed send buffer)."""
+    torch = torch_cuda
+    A = lz.gen_banded(9_001, 6.0, 2000, seed=52)
+    bounds = np.array([0, 3000, 6000, 9001], np.int64)
+    Gs = {b: np.arange(A.n * b, dtype=np.float64).reshape(A.n, b) / (3.0 + b) for b in (4, 16)}
+
+    def rank_fn(r, h):
+        r0, r1 = int(bounds[r]), int(bounds[r + 1])
+        _, col, _ = _slab(A, r0, r1)
+        _, cnt, rows = lz.halo_plan(col, bounds, r)
+        h.halo_init(r0, r1 - r0, cnt, rows)
+        out = {}
+        for b in (4, 16):
+            X = torch.zeros(r1 - r0 + rows.size, b, dtype=torch.float64, device="cuda")
+            X[: r1 - r0] = torch.from_numpy(Gs[b][r0:r1]).cuda()
+            h.halo_exchange(X)
+            X[: r1 - r0] = -1.0  # overwritten at once: a late peer copy would see it
+            out[b] = X
+        return {b: X.cpu().numpy() for b, X in out.items()}, rows
+
+    for r, (Xs, rows) in enumerate(lz.run_virtual_ranks(3, rank_fn)):
+        nl = int(bounds[r + 1] - bounds[r])
+        for b, X in Xs.items():
+            assert np.array_equal(X[nl:], Gs[b][rows.astype(np.int64)]), (r, b)

@@ -40,6 +40,19 @@ def test_oracle_vs_numpy_restatement(lz, orc, b):
     assert np.allclose(q, qn, rtol=1e-9, atol=1e-12)
 
 
+@pytest.mark.parametrize("m", [1, 2, 5])
+def test_oracle_final_state_vs_numpy(lz, orc, m):
+    """The blocks the reference leaves in Q0 (= Q1) and W on return
+    (block_lanczos.hpp:159,162): oracle against the numpy restatement."""
+    A = lz.gen_banded(2001, 8.0, 120, seed=30 + m)
+    B = lz.uniform_B(A.n, 4, seed=3)
+    q, al, be, Qf, Wf = orc.block_lanczos_final(A, B, m, 5)
+    qn, aln, ben, Qn, Wn = numpy_block_lanczos(A, B, m, 5, final=True)
+    assert np.allclose(al, aln, rtol=1e-9, atol=1e-12)
+    assert np.allclose(Qf, Qn, rtol=1e-9, atol=1e-12 * np.abs(Qn).max())
+    assert np.allclose(Wf, Wn, rtol=1e-8, atol=1e-10 * np.abs(Wn).max())
+
+
 def test_oracle_spmm_vs_reference_ell_spmm(lz, orc, golden):
     """CSR SpMM restatement == the reference's host Ell_matrix::spmm (ell_matrix.hpp:287-300)."""
     if not orc.ref_available(4):
