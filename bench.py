@@ -127,7 +127,7 @@ def spmm_kernel(nnz, n):
 
 # the source file of each profiled kernel: a committed counter file is used only
 # while that file is byte-identical to the one profiled (profiles record its sha256)
-KERNEL_SRC = {"k_wf16": "lz_wf.hip", "k_fused_pp16": "lz_fused.hip", "k_fused_update16": "lz_fused.hip", "k_spmm_seg": "lz_spmm.hip",
+KERNEL_SRC = {"k_wf16": "lz_wf.hip", "k_vl_spmv_win": "lz_fused.hip", "k_fused_pp16": "lz_fused.hip", "k_fused_update16": "lz_fused.hip", "k_spmm_seg": "lz_spmm.hip",
               "k_fused_el32": "lz_fused32.hip", "k_fused_ub32": "lz_fused32.hip", "k_gram16_f64": "lz_dense.hip",
               "k_gram32_f32": "lz_dense.hip"}
 CSRC = os.path.join(ROOT, "gpu-implementation-of-signle-and-block-lanczos_amd", "csrc")
@@ -221,7 +221,9 @@ def parse_args():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=20)
     ap.add_argument("--warmup", type=int, default=3)
-    ap.add_argument("--config", choices=["c3", "c4"], default="c3")
+    ap.add_argument("--config", choices=["c3", "c4", "c4rank"], default="c3",
+                    help="c4rank: one rank's share of C4 on one GPU (n = 5M of 40M, 25 nnz/row, half "
+                         "width 2^16): the per-GPU step of the 8-GPU north-star configuration")
     ap.add_argument("--n", type=int, default=None, help="c3: rows per GPU (1e7); c4: rows in total (4e7)")
     ap.add_argument("--nnz-per-row", type=float, default=None)
     ap.add_argument("--halfwidth", type=int, default=None)
@@ -246,11 +248,13 @@ def parse_args():
     ap.add_argument("--dist", action="store_true",
                     help="run the distributed entry point even at N = 1 (rehearsal of the N > 1 path)")
     args = ap.parse_args()
-    c4 = args.config == "c4"
+    c4 = args.config in ("c4", "c4rank")
     for k, v3, v4 in (("n", 10_000_000, 40_000_000), ("nnz_per_row", 10.0, 25.0), ("halfwidth", 4096, 1 << 16),
                       ("c2_steps", 200, 0), ("c5_steps", 10, 0), ("rand_steps", 10, 0), ("cpu_iters", 6, 2)):
         if getattr(args, k) is None:
             setattr(args, k, v4 if c4 else v3)
+    if args.config == "c4rank" and args.n == 40_000_000:
+        args.n = 5_000_000
     return args
 
 
@@ -277,6 +281,9 @@ def main():
     lz = ge.load_package()
     h = lz.Handle(local)
     c4 = args.config == "c4"
+    c4rank = args.config == "c4rank"
+    if c4rank and world != 1:
+        raise SystemExit("--config c4rank runs one rank's share on ONE GPU (the 8-GPU run is --config c4)")
     b = args.b
     seed = 20261015
     # the global operator and this rank's rows [r0, r1)
@@ -523,8 +530,34 @@ def main():
         dt2 = time.perf_counter() - t0c
         c2 = {"workload": f"C2 single-vector Lanczos fp64, banded-random n={n2} nnz={A2.nnz}",
               "iters_per_s": round(k2 / dt2, 1), "us_per_iter": round(dt2 / k2 * 1e6, 2),
-              "iteration_GBs": round((A2.nnz * 12 + (n2 + 1) * 8 + 5 * n2 * 8) / (dt2 / k2) / 1e9, 1),
-              "note": "A + 5 n s bytes per step (A, w read, q_{j-1} read, q_j written, w' written)"}
+              "iteration_GBs": round((A2.nnz * 12 + (n2 + 1) * 8 + 7 * n2 * 8) / (dt2 / k2) / 1e9, 1),
+              "note": "A + 7 n s bytes per step: SpMV pass A + 4 n s (w_j gathered, q_{j-1} read, q_j and w' "
+                      "written), update pass 3 n s (w', q_j read, w' written)"}
+        # the dominant kernel (the SpMV pass) against the HBM roofline: HIP events of a separate
+        # solve with the two vector classes recorded
+        k2p = min(k2, 50)
+        h.prof_enable(True)
+        h.vector_lanczos(A2d, b2, k2p, 84, q2, al2, be2, v0, v1, v2)
+        torch.cuda.synchronize()
+        sv_ms, sv_cnt = h.prof_read(h.PROF_SPMM_PASS)
+        up_ms, up_cnt = h.prof_read(h.PROF_UPDATE_PASS)
+        h.prof_enable(False)
+        if sv_cnt and up_cnt:
+            spmv_b = A2.nnz * 12 + (n2 + 1) * 8 + 4 * n2 * 8
+            t_sv, t_up = sv_ms / sv_cnt * 1e-3, up_ms / up_cnt * 1e-3
+            kn2 = "k_vl_spmv_win<double,8,512,9216>"
+            tr2, src2 = pmc_traffic("k_vl_spmv_win", n2, A2.nnz, 4096, kn2)
+            c2["roofline"] = {"bound": "hbm", "kernel": kn2, "bytes_per_launch": spmv_b,
+                              "avg_ms": round(t_sv * 1e3, 5), "achieved": round(spmv_b / t_sv / 1e9, 1),
+                              "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                              "frac": round(spmv_b / t_sv / 1e9 / HBM_PEAK_GBS, 4),
+                              "traffic": tr2, "traffic_source": src2,
+                              "update_pass": {"kernel": "k_vl_update<double>", "bytes_per_launch": 3 * n2 * 8,
+                                              "avg_ms": round(t_up * 1e3, 5),
+                                              "frac": round(3 * n2 * 8 / t_up / 1e9 / HBM_PEAK_GBS, 4)},
+                              "note": "HIP events around each launch of a separate solve; a launch moves "
+                                      f"{spmv_b / 1e6:.0f} MB in ~{t_sv * 1e6:.0f} us, so launch ramp-up and "
+                                      "tail are a visible share of it"}
         if not args.no_cpu_baseline:
             orc = ge.load_oracle()
             m2 = min(k2, 12)
@@ -567,6 +600,40 @@ def main():
                           f"nnz={A5.nnz}, max row {int(np.diff(A5.row_ptr).max())}",
               "iters_per_s": round(k5 / dt5, 2), "ms_per_iter": round(dt5 / k5 * 1e3, 3),
               "finite": bool(torch.isfinite(al5).all())}
+        # rooflines: the SpMM (the dominant kernel: U = A W_j - W_{j-1} M_j, tile pass + long-tile
+        # pass) and the whole iteration (beta^2 form: A + 8 n b s), HIP events of a separate solve
+        k5p = min(k5, 5)
+        h.prof_enable(True)
+        h.block_lanczos_blas(A5d, B5, k5p, 84, q5, al5, be5, *P5)
+        torch.cuda.synchronize()
+        sp5_ms, sp5_cnt = h.prof_read(h.PROF_SPMM)
+        el5_ms, el5_cnt = h.prof_read(h.PROF_SPMM_PASS)
+        ub5_ms, ub5_cnt = h.prof_read(h.PROF_UPDATE_PASS)
+        h.prof_enable(False)
+        a5 = A5.nnz * 8 + (n5 + 1) * 8  # fp32 values + int32 columns + row pointers
+        nbs5 = n5 * 32 * 4
+        if sp5_cnt == k5p:
+            # step 0 has no W_{j-1} term: A + 2 nbs, later steps A + 3 nbs
+            sp5_b = k5p * (a5 + 2 * nbs5) + (k5p - 1) * nbs5
+            t5 = sp5_ms * 1e-3
+            kn5 = "k_spmm_seg<float,32,48,768,false,0,false,true>"
+            tr5, src5 = pmc_traffic("k_spmm_seg_c5", n5, A5.nnz, 0, kn5)
+            c5["roofline"] = {"bound": "hbm", "kernel": kn5 + " (+ its long-tile pass, MODE 1)",
+                              "bytes_per_launch": round(sp5_b / k5p), "avg_ms": round(t5 / k5p * 1e3, 4),
+                              "achieved": round(sp5_b / t5 / 1e9, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                              "frac": round(sp5_b / t5 / 1e9 / HBM_PEAK_GBS, 4),
+                              "traffic": tr5, "traffic_source": src5,
+                              "bytes_note": "A (4-B values, 4-B columns) + W_j gathered once + W_{j-1} read + U "
+                                            "written = A + 3 n b s (step 0: A + 2 n b s); the reference's SpMM "
+                                            "model A + 2 n b s is spmm_model_bytes",
+                              "spmm_model_bytes": a5 + 2 * nbs5}
+            if el5_cnt and ub5_cnt:
+                c5["iteration_roofline"] = {
+                    "bytes_per_step": a5 + 8 * nbs5, "ms_per_step": round(dt5 / k5 * 1e3, 3),
+                    "frac": round((a5 + 8 * nbs5) / (dt5 / k5) / 1e9 / HBM_PEAK_GBS, 4),
+                    "kernels_ms_per_step": {"spmm": round(sp5_ms / k5p, 4), "pass_el": round(el5_ms / el5_cnt, 4),
+                                            "pass_ub": round(ub5_ms / ub5_cnt, 4)},
+                    "note": "beta^2 form: SpMM A + 3 nbs, pass EL 2 nbs, pass UB 3 nbs"}
         if not args.no_cpu_baseline:  # fp32: 1e-4 relative
             orc = ge.load_oracle()
             m5 = min(k5, 4)
@@ -728,6 +795,10 @@ def main():
             workload = (f"C4 block Lanczos b=16 fp64, banded-random symmetric CSR n={n_total} total "
                         f"({world} rank(s), {n} rows on rank 0), nnz~{args.nnz_per_row:g}/row, "
                         f"halfwidth {args.halfwidth}")
+        elif c4rank:
+            workload = (f"C4 per-rank share on one GPU: block Lanczos b=16 fp64, banded-random symmetric CSR "
+                        f"n={args.n} (one of 8 ranks of the 40M-row operator), nnz~{args.nnz_per_row:g}/row, "
+                        f"halfwidth {args.halfwidth} (columns clipped to the share: no halo rows)")
         else:
             workload = ("C3 block Lanczos b=16 fp64, banded-random symmetric CSR "
                         f"n={args.n} per GPU, nnz~{args.nnz_per_row:g}/row, halfwidth {args.halfwidth}")
@@ -764,13 +835,19 @@ def main():
                                        "gram": round(gram_ms / K_bd, 4),
                                        "note": f"fused_spmm_pass: HIP events in the timed region; the others: "
                                                f"a separate {K_bd}-step run with every class recorded"},
-                "iteration_frac_of_roofline": round((a_bytes + 8 * n * b * 8) / it_s / 1e9 / HBM_PEAK_GBS, 4),
-                "iteration_min_bytes": a_bytes + 8 * n * b * 8,
+                # the achieved fraction of the iteration: the bytes the implemented step moves
                 "iteration_frac_qfree_bytes": round((a_bytes + step_nbs * n * b * 8) / it_s / 1e9 / HBM_PEAK_GBS, 4),
                 "iteration_qfree_bytes": a_bytes + step_nbs * n * b * 8,
-                "iteration_bytes_note": "min_bytes: SURVEY.md 8(d) convention A + 8nbs (fixed); qfree_bytes: "
-                                        f"A + {step_nbs}nbs, what the implemented Q-free "
-                                        f"{'wavefront' if wf else 'two-pass'} step moves",
+                # NOT an achieved fraction: the SURVEY.md 8(d) model's A + 8nbs (more bytes than the
+                # implemented step moves) per measured step time, kept for comparison with that convention
+                "iteration_rate_vs_survey_model_A8nbs": round((a_bytes + 8 * n * b * 8) / it_s / 1e9 / HBM_PEAK_GBS, 4),
+                "survey_model_bytes": a_bytes + 8 * n * b * 8,
+                "iteration_bytes_note": f"qfree_bytes: A + {step_nbs}nbs, what the implemented Q-free "
+                                        f"{'wavefront' if wf else 'two-pass'} step moves (A with 12-B entries; "
+                                        "the roofline kernel streams 2-B columns); survey_model_bytes: SURVEY.md "
+                                        "8(d)'s fixed A + 8nbs convention, not bytes this step moves; the per-solve "
+                                        "final-state pass (Q0 = Q1 = Q_{m-1}, W = W_m: 6 nbs once) is inside the "
+                                        "timed solve",
                 "step_form": "wavefront (lz_wf.hip)" if wf else ("two-pass (lz_fused.hip)" if fused else "unfused"),
                 # the gather-bound pass's natural unit: nonzeros (one 128-B X row gathered each) per second,
                 # comparable across C3 (10 nnz/row) and C4 (25 nnz/row)

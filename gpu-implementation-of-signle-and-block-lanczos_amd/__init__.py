@@ -95,6 +95,7 @@ HIP_SYMBOLS = [
     ("lz_comm_init_local", _c_int, [_c_vp, _c_vp, _c_int]),
     ("lz_comm_abort", _c_int, [_c_vp]),
     ("lz_debug_last_split", _c_int, [_c_vp, _c_vp]),
+    ("lz_debug_last_wf", _c_int, [_c_vp, ctypes.POINTER(_c_int)]),
     ("lz_block_lanczos_dist", _c_int, [_c_vp, _c_i64, _c_i64, _c_i64, _c_i64, _c_vp, _c_vp, _c_vp,
                                        _c_int, _c_int, _c_int, _c_i64, _c_int, _c_vp, _c_vp, _c_vp,
                                        _c_vp, _c_vp, _c_vp, _c_vp, _c_vp]),
@@ -595,6 +596,12 @@ class Handle:
         """Attach this handle as virtual rank `rank` of an in-process group (one device)."""
         _check(self.L.lz_comm_init_local(self.ptr, group.ptr, rank), "lz_comm_init_local")
         group._keep.append(self)
+
+    def last_wf(self):
+        """(wavefront step, pass-2-first overlap) flags of the last distributed solve."""
+        v = (_c_int * 2)()
+        _check(self.L.lz_debug_last_wf(self._h, v), "lz_debug_last_wf")
+        return bool(v[0]), bool(v[1])
 
     def last_split(self):
         """(i0, i1) of the last distributed solve's interior rows (pass 1 beside the

@@ -218,7 +218,9 @@ static int block_lanczos_wf16(lz_handle *h, int64_t n, int64_t nnz, const int64_
         // the block slabs folded by 12 workgroups (one workgroup reading all
         // 1.5 MB took ~20 us), then beta_{j+1}, its inverse and P1 = beta_j^-1
         // beta_{j+1} from G, and (same launch) alpha_{j+1}, P2 and the row probe
-        LZ_TRY(wf_fold16(h, h->partials2, P, nullptr, 0, nullptr, 0, slab));
+        WfSlabs sl;
+        sl.add(h->partials2, P);
+        LZ_TRY(wf_fold16(h, sl, slab));
         WfAlpha wa;
         wa.part = slab;
         wa.P = 1;
@@ -517,6 +519,10 @@ int attach_comm(lz_handle *h, Comm *c)
 // of the receiver's halo (ascending global row, so grouped by owner).
 struct HaloPlan {
     int64_t n_local = 0, n_halo = 0, n_send = 0;
+    // the rows peers request lie in [0, send_head) and [send_tail, n_local)
+    // (the first / second half's extremes): the wavefront step's pass 2 of
+    // their tiles runs first, so the exchange can overlap the rest of the step
+    int64_t send_head = 0, send_tail = 0;
     std::vector<int64_t> soff, roff;  // nranks + 1 row offsets per peer
     int32_t *send_idx = nullptr;      // device: local rows to pack, grouped by peer
     void *sendbuf = nullptr;          // device: n_send packed rows
@@ -677,9 +683,10 @@ static int split_plan(lz_handle *h, int64_t n, const int64_t *rp, const int32_t 
 
 enum { kFormHalo = 0, kFormAllgather = 1 };
 
-static int dist_solve_wf16(lz_handle *h, HaloPlan *hp, int64_t n, int64_t nnz, const int64_t *rp, const int32_t *col,
-                           const double *val, int m, int64_t lc, const double *B, double *q, double *alpha,
-                           double *beta, double *X0, double *X1, const WfPlan &wp, const SplitPlan &sp);
+static int dist_solve_wf16(lz_handle *h, int form, HaloPlan *hp, int64_t n, int64_t n_pad, int64_t nnz,
+                           const int64_t *rp, const int32_t *col, const double *val, int m, int64_t lc,
+                           const double *B, double *q, double *alpha, double *beta, double *X0, double *X1,
+                           const WfPlan &wp, const SplitPlan &sp);
 
 // The distributed iteration, both exchange forms, any b <= 32, fp64 / fp32.
 //   b = 16 fp64: the fused Q-free passes of block_lanczos_fused16 (pass 1 =
@@ -724,9 +731,18 @@ static int dist_solve_impl(lz_handle *h, int form, HaloPlan *hp, int64_t n, int6
     if (!ag && hp && cm && h->nranks > 1)
         LZ_TRY(grow_ws(h, &hp->sendbuf, &hp->send_cap, (size_t)std::max<int64_t>(hp->n_send, 1) * rowb));
     if constexpr (std::is_same<T, double>::value) {
-        if (f16 && !ag) {  // the wavefront step when it applies (LZ_PASS_WF=0: the two passes)
+        // the wavefront step when it applies (LZ_PASS_WF=0: the two passes).  The
+        // all-gather form takes it at one rank, where its exchange moves nothing:
+        // at N > 1 the all-gather (the whole block from every peer; ~4.2 ms at C4
+        // on 8 GPUs) outlasts the step's compute, and the two-pass
+        // step hides the interior rows' pass 1 under it where the wavefront step,
+        // which needs the exchange between its pass 2 and the boundary tiles'
+        // pass 1, could hide nothing.  LZ_AG_WF=1 / 0 forces it on / off (tests).
+        const char *agw = getenv("LZ_AG_WF");
+        const bool ag_wf = agw ? agw[0] == '1' : h->nranks == 1;
+        if (f16 && (!ag || ag_wf)) {
             WfPlan wp;
-            LZ_TRY(wf_plan16(h, n, nnz, rp, col, &wp, nx));
+            LZ_TRY(wf_plan16(h, n, nnz, rp, col, &wp, nx, own_off));
             if (cm && h->nranks > 1) {  // every rank takes the same form (their collectives must match)
                 double v = wp.ok ? 1.0 : 0.0;
                 LZ_HIP_TRY(hipMemcpyAsync(slab, &v, sizeof(double), hipMemcpyHostToDevice, h->stream));
@@ -735,15 +751,19 @@ static int dist_solve_impl(lz_handle *h, int form, HaloPlan *hp, int64_t n, int6
                 LZ_HIP_TRY(hipStreamSynchronize(h->stream));
                 wp.ok = v == (double)h->nranks;
             }
+            h->last_wf = wp.ok ? 1 : 0;
+            h->last_wf_pre = 0;
             if (wp.ok) {
                 SplitPlan sp;
-                LZ_TRY(split_plan(h, n, rp, col, 0, n, &sp));
+                LZ_TRY(split_plan(h, n, rp, col, own_off, own_off + n, &sp));
                 h->last_split[0] = sp.on ? sp.i0 : -1;
                 h->last_split[1] = sp.on ? sp.i1 : -1;
-                return dist_solve_wf16(h, hp, n, nnz, rp, col, val, m, lc, B, q, alpha, beta, X0, X1, wp, sp);
+                return dist_solve_wf16(h, form, hp, n, n_pad, nnz, rp, col, val, m, lc, B, q, alpha, beta, X0, X1,
+                                       wp, sp);
             }
         }
     }
+    h->last_wf = h->last_wf_pre = 0;
     Pass1Plan pl;
     if (f16) LZ_TRY(pass1_plan(h, n, nnz, rp, col, nx, own_off, &pl));
     SplitPlan sp;
@@ -846,35 +866,51 @@ static int dist_solve_impl(lz_handle *h, int form, HaloPlan *hp, int64_t n, int6
     return LZ_OK;
 }
 
-// The wavefront step (lz_wf.hip) on a row-partitioned rank, halo form, b = 16
-// fp64.  Per step: one launch runs pass 2 over all own rows and pass 1 over the
-// interior tiles (their columns are own rows); the halo rows of V_{j+1} are
-// exchanged; pass 1 of the boundary tiles (head, tail) runs on the completed
-// gather source; the three sums [S1 | S2 | G] are folded and all-reduced in
-// one 768-double collective; one sqrtm launch makes beta, P1 and alpha, P2, q.
-// V_0 = B copied into X0 (with its halo); V_{j+1} over V_{j-1} in X1, X0, ...;
-// Y (own rows) in the handle's workspace.
-static int dist_solve_wf16(lz_handle *h, HaloPlan *hp, int64_t n, int64_t nnz, const int64_t *rp, const int32_t *col,
-                           const double *val, int m, int64_t lc, const double *B, double *q, double *alpha,
-                           double *beta, double *X0, double *X1, const WfPlan &wp, const SplitPlan &sp)
+// The wavefront step (lz_wf.hip) on a row-partitioned rank, b = 16 fp64.
+// Halo form, per step:
+//   1. pass 2 of the tiles holding rows peers request (the first and last
+//      ones of a banded slab): a pass-2-only launch;
+//   2. the halo exchange of V_{j+1} on the exchange stream, beside
+//   3. the step launch: pass 2 of the other tiles + pass 1 of the interior
+//      tiles (their columns are own rows);
+//   4. pass 1 of the boundary tiles (head, tail) once the halo has landed;
+// then the slab sets [S1 | S2 | G] of the launches are folded and summed over
+// the ranks in ONE 768-double all-reduce, and one sqrtm launch makes beta,
+// P1 and alpha, P2, q.  Without a split (or with the requested rows spread
+// over the slab) steps 1 and 2 are the step launch's pass 2 and a serial
+// exchange.  V_0 = B copied into X0 (with its halo); V_{j+1} over V_{j-1} in
+// X1, X0, ...; Y (own rows) in the handle's workspace.
+// All-gather form: X0 = X_full (n_pad * N rows), the rank's slot at rank *
+// n_pad holds V_j; X1 = W (n_pad rows) holds V_{j-1}: the step launch's pass 2
+// writes V_{j+1} into the slot and V_j into W (SW), then the in-place
+// all-gather, then the boundary tiles.
+static int dist_solve_wf16(lz_handle *h, int form, HaloPlan *hp, int64_t n, int64_t n_pad, int64_t nnz,
+                           const int64_t *rp, const int32_t *col, const double *val, int m, int64_t lc,
+                           const double *B, double *q, double *alpha, double *beta, double *X0, double *X1,
+                           const WfPlan &wp, const SplitPlan &sp)
 {
     Comm *cm = h->comm;
     constexpr int64_t bb = 256;
     const size_t rowb = 128;
-    const int64_t nx = n + (hp ? hp->n_halo : 0);
+    const bool ag = form == kFormAllgather;
+    const int64_t nx = ag ? n_pad * h->nranks : n + (hp ? hp->n_halo : 0);
+    const int64_t own_off = ag ? (int64_t)h->rank * n_pad : 0;
     const int64_t T = ceil_div(n, (int64_t)wp.tr);
     double *slab = h->scratch;  // [S1 | S2 | G], all-reduced in place
     double *sc = h->scratch + 4 * kMaxB * kMaxB;
     double *binv[2] = {sc, sc + bb}, *P1 = sc + 2 * bb, *P2 = sc + 3 * bb;
     (void)nnz;
+    LZ_ARG_CHECK(wp.xoff == own_off, "wavefront plan for another slot (internal)");
     LZ_TRY(grow_ws(h, &h->ybuf, &h->ybuf_cap, (size_t)std::max<int64_t>(n, 1) * rowb));
     double *Y = static_cast<double *>(h->ybuf);
     const uint64_t *pairs = nullptr;
     LZ_TRY(strip_pairs(h, n, rp, &pairs));
-    // interior pass-1 tiles: inside the split plan's interior rows (a single
-    // rank: every tile)
+    double *slot = X0 + own_off * 16;  // all-gather: this rank's rows of X_full
+    // interior pass-1 tiles: inside the split plan's interior rows (every tile
+    // when no column leaves the rank's rows)
+    const bool exch = h->nranks > 1 && (ag || (hp && hp->n_halo > 0));
     int64_t t0 = 0, t1 = T;
-    if (h->nranks > 1 && hp && hp->n_halo > 0) {
+    if (exch) {
         t0 = t1 = 0;
         if (sp.on) {
             t0 = ceil_div(sp.i0, (int64_t)wp.tr);
@@ -882,42 +918,88 @@ static int dist_solve_wf16(lz_handle *h, HaloPlan *hp, int64_t n, int64_t nnz, c
             if (t1 <= t0) t0 = t1 = 0;
         }
     }
+    // halo form: pass 2 of the requested rows' tiles first, the exchange
+    // beside the rest of the step (LZ_DIST_OVERLAP=0 turns the split off too)
+    int64_t sh = 0, st = T;
+    bool pre = false;
+    if (!ag && exch && sp.on && hp->n_send > 0) {
+        sh = ceil_div(hp->send_head, (int64_t)wp.tr);
+        st = std::max(sh, hp->send_tail / wp.tr);
+        pre = st - sh >= T / 4;
+    }
+    h->last_wf_pre = pre ? 1 : 0;
     const bool reduce = cm && h->nranks > 1;
     auto allreduce = [&](size_t cnt) -> int { return reduce ? cm->allreduce_sum(slab, cnt, h->stream) : LZ_OK; };
-    auto exchange = [&](double *X) -> int { return hp ? halo_exchange(h, *hp, X, rowb, h->stream) : LZ_OK; };
+    auto exchange = [&](double *X, hipStream_t s) -> int {
+        if (ag) return cm ? cm->allgather(slot, X0, (size_t)n_pad * rowb, s) : LZ_OK;
+        return hp ? halo_exchange(h, *hp, X, rowb, s) : LZ_OK;
+    };
     const int64_t lcl = (lc >= 0 && lc < n) ? lc : -1;
-    // ---- beta_0 from the global Gram of B; V_0 = B with its halo
+    // ---- beta_0 from the global Gram of B; V_0 = B with its halo / in every slot
     int np = 0;
     LZ_TRY(gram_partials<double>(h, n, 16, B, B, 16, &np));
     LZ_TRY(gram_finish<double>(h, 16, np, 0, slab));
     LZ_TRY(allreduce(bb));
     LZ_TRY(sqrtm_pair<double>(h, 16, nullptr, 1, beta, binv[0], nullptr, slab));
-    LZ_HIP_TRY(hipMemcpyAsync(X0, B, (size_t)n * rowb, hipMemcpyDeviceToDevice, h->stream));
-    LZ_TRY(exchange(X0));
+    if (ag) {
+        if (cm) LZ_TRY(cm->allgather(B, X0, (size_t)n_pad * rowb, h->stream));
+        else LZ_HIP_TRY(hipMemcpyAsync(slot, B, (size_t)n * rowb, hipMemcpyDeviceToDevice, h->stream));
+    } else {
+        LZ_HIP_TRY(hipMemcpyAsync(X0, B, (size_t)n * rowb, hipMemcpyDeviceToDevice, h->stream));
+        LZ_TRY(exchange(X0, h->stream));
+    }
     LZ_TRY(wf_reset16(h, n, wp));
     // ---- Y_0 = A V_0 (pass 1 only, every tile), alpha_0
     int G = 0;
     LZ_TRY(wf_step16(h, n, rp, col, wp.col16, val, pairs, wp, nullptr, nullptr, nullptr, nullptr, nullptr, nullptr,
                      nullptr, X0, Y, 0, &G, nx, 0, T, h->partials2));
-    LZ_TRY(wf_fold16(h, h->partials2, G, nullptr, 0, nullptr, 0, slab));
+    {
+        WfSlabs sl;
+        sl.add(h->partials2, G);
+        LZ_TRY(wf_fold16(h, sl, slab));
+    }
     LZ_TRY(allreduce(3 * bb));
-    LZ_TRY(alpha_wf16(h, slab, 1, binv[0], nullptr, alpha, P2, X0, lcl, n, q));
-    const double *Vm1 = nullptr, *V0 = X0;
+    LZ_TRY(alpha_wf16(h, slab, 1, binv[0], nullptr, alpha, P2, ag ? slot : X0, lcl, n, q));
+    const double *Vm1 = nullptr, *V0 = ag ? slot : X0;
     for (int j = 0; j + 1 < m; ++j) {
-        double *Vn = (j & 1) ? X0 : X1;
-        // pass 2 (every own tile) + pass 1 of the interior tiles
-        int Gk = 0, G1 = 0, G2 = 0;
-        LZ_TRY(wf_step16(h, n, rp, col, wp.col16, val, pairs, wp, Y, Vm1, V0, Vn, binv[j & 1], j ? P1 : nullptr, P2,
-                         Vn, Y, j + 1, &Gk, nx, t0, t1, h->partials2));
-        // V_{j+1}'s halo rows, then pass 1 of the boundary tiles
-        LZ_TRY(exchange(Vn));
-        double *p1 = h->partials2 + 3 * (int64_t)Gk * 256;
-        LZ_TRY(wf_step16(h, n, rp, col, wp.col16, val, pairs, wp, nullptr, nullptr, nullptr, nullptr, nullptr,
-                         nullptr, nullptr, Vn, Y, 0, &G1, nx, 0, t0, p1));
-        double *p2 = p1 + 3 * (int64_t)G1 * 256;
-        LZ_TRY(wf_step16(h, n, rp, col, wp.col16, val, pairs, wp, nullptr, nullptr, nullptr, nullptr, nullptr,
-                         nullptr, nullptr, Vn, Y, 0, &G2, nx, t1, T, p2));
-        LZ_TRY(wf_fold16(h, h->partials2, Gk, p1, G1, p2, G2, slab));
+        // (all-gather: V_{j+1} into the slot over V_j, V_j into X1 over V_{j-1})
+        double *Vn = ag ? slot : ((j & 1) ? X0 : X1);
+        double *Vg = ag ? X0 : Vn;
+        const double *Vprev = ag ? (j ? X1 : nullptr) : Vm1;
+        double *Vsave = ag ? X1 : nullptr;
+        WfSlabs sl;
+        double *part = h->partials2;
+        int Gp = 0, Gk = 0, G1 = 0, G2 = 0;
+        if (pre) {  // pass 2 of the requested rows' tiles, then their exchange beside the step launch
+            const int64_t qa[4] = {0, sh, st, T};
+            LZ_TRY(wf_step16(h, n, rp, col, wp.col16, val, pairs, wp, Y, Vprev, V0, Vn, binv[j & 1],
+                             j ? P1 : nullptr, P2, Vg, Y, j + 1, &Gp, nx, 0, 0, part, qa, Vsave));
+            sl.add(part, Gp);
+            part += 3 * (int64_t)Gp * 256;
+            LZ_HIP_TRY(hipEventRecord(h->ev_cx, h->stream));
+            LZ_HIP_TRY(hipStreamWaitEvent(h->xstream, h->ev_cx, 0));
+            LZ_TRY(exchange(Vn, h->xstream));
+            LZ_HIP_TRY(hipEventRecord(h->ev_xd, h->xstream));
+        }
+        // the step launch: pass 2 (the other tiles) + pass 1 of the interior tiles
+        const int64_t qk[4] = {pre ? sh : 0, pre ? st : T, T, T};
+        LZ_TRY(wf_step16(h, n, rp, col, wp.col16, val, pairs, wp, Y, Vprev, V0, Vn, binv[j & 1], j ? P1 : nullptr,
+                         P2, Vg, Y, j + 1, &Gk, nx, t0, t1, part, qk, Vsave));
+        sl.add(part, Gk);
+        part += 3 * (int64_t)Gk * 256;
+        if (exch) {
+            // V_{j+1}'s halo rows / peers' slots, then pass 1 of the boundary tiles
+            if (pre) LZ_HIP_TRY(hipStreamWaitEvent(h->stream, h->ev_xd, 0));
+            else LZ_TRY(exchange(Vn, h->stream));
+            LZ_TRY(wf_step16(h, n, rp, col, wp.col16, val, pairs, wp, nullptr, nullptr, nullptr, nullptr, nullptr,
+                             nullptr, nullptr, Vg, Y, 0, &G1, nx, 0, t0, part));
+            sl.add(part, G1);
+            part += 3 * (int64_t)G1 * 256;
+            LZ_TRY(wf_step16(h, n, rp, col, wp.col16, val, pairs, wp, nullptr, nullptr, nullptr, nullptr, nullptr,
+                             nullptr, nullptr, Vg, Y, 0, &G2, nx, t1, T, part));
+            sl.add(part, G2);
+        }
+        LZ_TRY(wf_fold16(h, sl, slab));
         LZ_TRY(allreduce(3 * bb));
         WfAlpha wa;
         wa.part = slab;
@@ -1353,6 +1435,14 @@ int lz_debug_last_split(lz_handle *h, int64_t out[2])
     return LZ_OK;
 }
 
+int lz_debug_last_wf(lz_handle *h, int out[2])
+{
+    LZ_ARG_CHECK(h && out, "NULL argument");
+    out[0] = h->last_wf;
+    out[1] = h->last_wf_pre;
+    return LZ_OK;
+}
+
 int lz_comm_destroy(lz_handle *h)
 {
     LZ_HANDLE_CHECK(h);
@@ -1495,10 +1585,14 @@ static int halo_init_impl(lz_handle *h, int64_t row0, int64_t n_local, const int
     (void)hipFree(dreq);
     if (rc != LZ_OK) return rc;
     // 3. global -> local row; every requested row must be ours
+    hp->send_head = 0;
+    hp->send_tail = n_local;
     for (int64_t i = 0; i < hp->n_send; ++i) {
         const int64_t g = (int64_t)sidx[i] - row0;
         LZ_ARG_CHECK(g >= 0 && g < n_local, "a peer requested a row this rank does not own");
         sidx[i] = (int32_t)g;
+        if (2 * g < n_local) hp->send_head = std::max(hp->send_head, g + 1);
+        else hp->send_tail = std::min(hp->send_tail, g);
     }
     if (hp->n_send)
         LZ_HIP_TRY(hipMemcpy(hp->send_idx, sidx.data(), sizeof(int32_t) * hp->n_send, hipMemcpyHostToDevice));

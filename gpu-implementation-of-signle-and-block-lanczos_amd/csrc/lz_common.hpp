@@ -82,6 +82,7 @@ struct lz_handle {
     hipStream_t xstream = nullptr;
     hipEvent_t ev_cx = nullptr, ev_xd = nullptr;
     int64_t last_split[2] = {-1, -1};  // lz_debug_last_split
+    int last_wf = 0, last_wf_pre = 0;  // lz_debug_last_wf: wavefront step, pass-2-first overlap
     // lz_block_lanczos leaves Q0 = Q1 = Q_{m-1}, W = W_m as the reference does
     // (one row-local pass per solve); lz_set_final_state(h, 0) skips that pass
     int final_state = 1;

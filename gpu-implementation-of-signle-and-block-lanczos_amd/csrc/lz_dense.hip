@@ -1063,6 +1063,67 @@ __global__ __launch_bounds__(256) void k_final_state(int64_t n, int b, const T *
     }
 }
 
+// b = 16 fp64: thread (column j = t & 15, row group t >> 4) keeps column j of
+// binv, P1, P2 in registers and walks 4 of the tile's 64 rows; a row's values
+// are LDS broadcasts (16-B reads).  Same products and order as k_final_state.
+__global__ __launch_bounds__(256) void k_final_state16(int64_t n, const double *Y, const double *Vp, const double *Vq,
+                                                      const double *Wm, const double *__restrict__ binv,
+                                                      const double *__restrict__ P1, const double *__restrict__ P2,
+                                                      double *Wout, double *Q0, double *Q1)
+{
+    constexpr int TR = 64;
+    __shared__ double2 rs[3][TR * 8];  // the tile's Vq, Y (or Wm), Vp rows
+    const int tid = threadIdx.x, j = tid & 15, rg = tid >> 4;
+    double mb[16], m1[16], m2[16];
+#pragma unroll
+    for (int i = 0; i < 16; ++i) {
+        mb[i] = binv[i * 16 + j];
+        m1[i] = P1 ? P1[i * 16 + j] : 0.0;
+        m2[i] = P2 ? P2[i * 16 + j] : 0.0;
+    }
+    const double2 *vq2 = reinterpret_cast<const double2 *>(Vq), *y2 = reinterpret_cast<const double2 *>(Y ? Y : Wm),
+                  *vp2 = reinterpret_cast<const double2 *>(Vp);
+    XcdSched s(ceil_div(n, TR));
+    for (int64_t u = s.begin; u < s.end; u += s.step) {
+        const int64_t r0 = u * TR;
+        const int nr = (int)(n - r0 < TR ? n - r0 : TR);
+        __syncthreads();  // the previous tile's rows are no longer read
+        for (int e = tid; e < nr * 8; e += 256) {
+            const int64_t g = r0 * 8 + e;
+            rs[0][e] = vq2[g];
+            rs[1][e] = y2[g];
+            rs[2][e] = Vp ? vp2[g] : make_double2(0.0, 0.0);
+        }
+        __syncthreads();  // every row of the tile read before any is written
+#pragma unroll
+        for (int k = 0; k < TR / 16; ++k) {
+            const int r = rg + 16 * k;
+            if (r >= nr) break;
+            double q = 0.0, a = 0.0, c = 0.0, d = 0.0;
+#pragma unroll
+            for (int i2 = 0; i2 < 8; ++i2) {
+                const double2 x = rs[0][r * 8 + i2], yv = rs[1][r * 8 + i2], pv = rs[2][r * 8 + i2];
+                q = fma(x.x, mb[2 * i2], q);
+                q = fma(x.y, mb[2 * i2 + 1], q);
+                a = fma(yv.x, mb[2 * i2], a);
+                a = fma(yv.y, mb[2 * i2 + 1], a);
+                c = fma(pv.x, m1[2 * i2], c);
+                c = fma(pv.y, m1[2 * i2 + 1], c);
+                d = fma(x.x, m2[2 * i2], d);
+                d = fma(x.y, m2[2 * i2 + 1], d);
+            }
+            const int64_t g = (r0 + r) * 16 + j;
+            if (Y) Wout[g] = (a - c) - d;
+            else if (Wm != Wout) {
+                const double2 yv = rs[1][r * 8 + (j >> 1)];
+                Wout[g] = (j & 1) ? yv.y : yv.x;
+            }
+            Q0[g] = q;
+            if (Q1) Q1[g] = q;
+        }
+    }
+}
+
 template <typename T>
 int final_state(lz_handle *h, int64_t n, int b, const T *Y, const T *Vp, const T *Vq, const T *Wm, const T *binv,
                 const T *P1, const T *P2, T *Wout, T *Q0, T *Q1)
@@ -1070,6 +1131,15 @@ int final_state(lz_handle *h, int64_t n, int b, const T *Y, const T *Vp, const T
     LZ_ARG_CHECK(b >= 1 && b <= 32 && Vq && binv && Wout && Q0 && (Y ? P2 != nullptr : Wm != nullptr),
                  "final state (internal)");
     if (n <= 0) return LZ_OK;
+    if constexpr (std::is_same<T, double>::value) {
+        if (b == 16) {
+            const int grid = (int)std::max<int64_t>(1, std::min<int64_t>(ceil_div(n, 64), (int64_t)h->n_cu * 4));
+            hipLaunchKernelGGL(k_final_state16, dim3(grid), dim3(256), 0, h->stream, n, Y, Vp, Vq, Wm, binv, P1, P2,
+                               Wout, Q0, Q1);
+            LZ_LAUNCH_CHECK();
+            return LZ_OK;
+        }
+    }
     const int grid = (int)std::max<int64_t>(1, std::min<int64_t>(ceil_div(n, 16), (int64_t)h->n_cu * 4));
     hipLaunchKernelGGL((k_final_state<T>), dim3(grid), dim3(256), 0, h->stream, n, b, Y, Vp, Vq, Wm, binv, P1, P2,
                        Wout, Q0, Q1);

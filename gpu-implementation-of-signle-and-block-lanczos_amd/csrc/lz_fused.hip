@@ -1502,6 +1502,7 @@ int vector_lanczos_dev(lz_handle *h, int64_t n, int64_t nnz, const int64_t *rp, 
     int wi = 0;
     for (int j = 0; j < m; ++j) {
         T *wnext = wbuf[wi];
+        const int ev_s = prof_begin(h, PROF_SPMM_PASS);  // the SpMV pass (bench: C2 roofline)
 #define LZ_VL_CASE(LV)                                                                          \
     case LV:                                                                                    \
         hipLaunchKernelGGL((k_vl_spmv<T, LV>), dim3(grid), dim3(kVlThreads), 0, h->stream, n, rp, \
@@ -1539,9 +1540,12 @@ int vector_lanczos_dev(lz_handle *h, int64_t n, int64_t nnz, const int64_t *rp, 
             }
         }
 #undef LZ_VL_CASE
+        prof_end(h, ev_s);
         LZ_LAUNCH_CHECK();
+        const int ev_u = prof_begin(h, PROF_UPDATE_PASS);
         hipLaunchKernelGGL(k_vl_update<T>, dim3(gridu), dim3(kVlThreads), 0, h->stream, n, wnext, q0,
                            pb, grid, alpha + j, pa);
+        prof_end(h, ev_u);
         LZ_LAUNCH_CHECK();
         P = gridu;
         wcur = wnext;

@@ -107,11 +107,15 @@ struct WfPlan {
     int nc = 12, tr = 192;    // consumers per block, rows per tile (16 nc)
     int var = 0;              // measurement shape (LZ_WF_SHAPE 104 / 111), 0: the standard ones
     const int16_t *col16 = nullptr;  // pass 1's 16-bit columns (made in the same pass), or null
+    int64_t xoff = 0;         // gather-source row of local row 0 (the all-gather form's slot)
 };
 // once per solve: per-tile dependency ranges and the 16-bit columns in one pass
 // over the CSR columns; synchronises the stream once
 int wf_plan16(lz_handle *h, int64_t n, int64_t nnz, const int64_t *rp, const int32_t *col, WfPlan *pl,
-              int64_t nx = -1);  // nx: rows of the gather source (a rank's own + halo rows), default n
+              int64_t nx = -1, int64_t xoff = 0);
+// (nx: rows of the gather source -- a rank's own + halo rows, or the all-gather
+// form's n_pad * N -- default n; xoff: its row of local row 0; 2^24+ rows are
+// read through per-strip windows, checked here)
 // zero the pass-2 flags (start of a solve; epochs 1, 2, ... follow)
 int wf_reset16(lz_handle *h, int64_t n, const WfPlan &pl);
 // P2 == nullptr: pass 1 only (Y = A Vg, S1 slabs).  Otherwise V_{j+1} = Yj binv
@@ -122,12 +126,27 @@ int wf_step16(lz_handle *h, int64_t n, const int64_t *rp, const int32_t *col, co
               const double *val, const uint64_t *pairs, const WfPlan &pl, const double *Yj, const double *Vprev,
               const double *Vj, double *Vout, const double *binv, const double *P1, const double *P2,
               const double *Vg, double *Yo, int epoch, int *nparts, int64_t nx = -1, int64_t p1a = 0,
-              int64_t p1b = -1, double *part = nullptr);
+              int64_t p1b = -1, double *part = nullptr, const int64_t *q = nullptr, double *Vsave = nullptr);
 // (nx: rows of Vg, default n; pass 1 over tiles [p1a, p1b), default all; slabs
-// at part, default h->partials2)
-// the distributed step's sums: out[0..768) = [S1 (step launch G slabs + G1 + G2
-// boundary slabs) | S2 | G]
-int wf_fold16(lz_handle *h, const double *kp, int G, const double *b1, int G1, const double *b2, int G2, double *out);
+// at part, default h->partials2; q: pass-2 tiles [q[0], q[1]) u [q[2], q[3]),
+// default all -- two ranges only without pass-1 tiles; Vout = Vg + 16 xoff;
+// Vsave: pass 2 also stores V_j's rows there (the all-gather form), 111 / wide
+// shapes only)
+// one step's slab sets (set t: [S1 | S2 | G] of g[t] block slabs at p[t]);
+// wf_fold16: out[0..768) = [S1 | S2 | G] summed over every set, in order
+struct WfSlabs {
+    static constexpr int kMax = 6;
+    const double *p[kMax] = {};
+    int g[kMax] = {};
+    int k = 0;
+    void add(const double *ptr, int nslab)
+    {
+        p[k] = ptr;
+        g[k] = nslab;
+        ++k;
+    }
+};
+int wf_fold16(lz_handle *h, const WfSlabs &sl, double *out);
 // alpha = sym(binv (S1 binv - S2 P1)) (P1 == nullptr: no S2 term), P2 = binv alpha,
 // q = V[lc] binv; S1, S2 = the sums of the P slabs at part, part + 256 P
 int alpha_wf16(lz_handle *h, const double *part, int P, const double *binv, const double *P1, double *alpha,

@@ -387,7 +387,8 @@ __global__ __launch_bounds__(256) void k_spmm_seg(int64_t n, const int64_t *__re
                                                   const T *__restrict__ val,
                                                   const T *__restrict__ X, int64_t ldx, int64_t nx,
                                                   T *__restrict__ Y, int64_t ldy, int *__restrict__ longq,
-                                                  int parity, const T *__restrict__ Wp, const T *__restrict__ Mm)
+                                                  int parity, const T *__restrict__ Wp, const T *__restrict__ Mm,
+                                                  int diag)
 {
     // MODE 0: tiles whose run exceeds the stage (or, WIN, whose columns exceed
     //         the window) are queued (longq[0] = count, longq[1..] = tile ids)
@@ -533,7 +534,16 @@ __global__ __launch_bounds__(256) void k_spmm_seg(int64_t n, const int64_t *__re
         }
         return;
     } else {
-    const int64_t r0 = xcd_remap(blockIdx.x, gridDim.x) * TR;
+    // diag > 0 (LZ_SPMM_DIAG, a measurement of the tile structure, results
+    // wrong): block b runs tile (its tile mod diag), so the row pointers, CSR
+    // runs, X window and Y rows of all blocks are those of `diag` tiles -- L2-
+    // resident -- with the same per-tile instruction mix
+    // (diag bit 30: the Y rows stored stay the block's own, so only the reads
+    // are L2-resident)
+    const int64_t tdx = xcd_remap(blockIdx.x, gridDim.x);
+    const int dmod = diag & 0x3fffffff;
+    const int64_t r0 = (dmod > 0 ? tdx % dmod : tdx) * TR;
+    const int64_t ry = (diag & (1 << 30)) ? tdx * TR : r0;  // the Y tile's first row
     const int nrows = (int)((n - r0) < TR ? (n - r0) : TR);
     const int64_t kA = rp[r0];
     if (tid <= nrows) rel[tid] = (int)(rp[r0 + tid] - kA);
@@ -710,7 +720,8 @@ __global__ __launch_bounds__(256) void k_spmm_seg(int64_t n, const int64_t *__re
         return;
     }
     for (int idx = tid; idx < nrows * LPR; idx += 256) {
-        T *dst = Y + (r0 + idx / LPR) * ldy + (idx % LPR) * VEC;
+        if (ry + idx / LPR >= n) break;  // (diag only: a Y tile shorter than the tile read)
+        T *dst = Y + (ry + idx / LPR) * ldy + (idx % LPR) * VEC;
         Vec<T, VEC> y = yt[idx / LPR][idx % LPR];
         if constexpr (EPI)
             if (epi) y = epi_piece<T, B, VEC>(y, Wp + (r0 + idx / LPR) * B, Ms, idx % LPR);
@@ -1136,11 +1147,16 @@ static int launch_seg(lz_handle *h, int64_t n, const int64_t *rp, const int32_t 
     }
     const int parity = h->longq_parity;
     h->longq_parity ^= 1;
+    // measurement only (results wrong), read per call: LZ_SPMM_DIAG = tiles mod
+    // this; LZ_SPMM_DIAG_Y=1: the Y tiles stay the blocks' own
+    const char *dg = getenv("LZ_SPMM_DIAG");
+    const char *dy = getenv("LZ_SPMM_DIAG_Y");
+    const int diag = (dg ? atoi(dg) : 0) | (dy && dy[0] == '1' ? 1 << 30 : 0);
     hipLaunchKernelGGL((k_spmm_seg<T, B, TR, CAP, WIN, 0, YCM, EPI>), dim3((unsigned)st), dim3(256), 0, h->stream, n, rp,
-                       col, val, X, ldx, nx, Y, ldy, h->longq, parity, Wp, Mm);
+                       col, val, X, ldx, nx, Y, ldy, h->longq, parity, Wp, Mm, diag);
     const int g2 = (int)std::max<int64_t>(1, std::min<int64_t>(st, (int64_t)h->n_cu * 4));
     hipLaunchKernelGGL((k_spmm_seg<T, B, TR, CAP, WIN, 1, YCM, EPI>), dim3(g2), dim3(256), 0, h->stream, n, rp, col, val,
-                       X, ldx, nx, Y, ldy, h->longq, parity, Wp, Mm);
+                       X, ldx, nx, Y, ldy, h->longq, parity, Wp, Mm, 0);
     return LZ_OK;
 }
 

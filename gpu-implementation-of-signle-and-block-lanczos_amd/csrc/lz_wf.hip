@@ -71,15 +71,20 @@ constexpr long kWfSpin = 1L << 21;  // flag polls per tile before the loader giv
 // spans[3] != 0 if one is out of int16 reach.  Columns >= ncol (a rank's halo
 // rows) are left out of the ranges.  A wave walks one strip's run
 // (coalesced); one atomic per block and quantity.
+// xoff: the gather-source row of local row 0 (the all-gather form's slot
+// offset; 0 otherwise); own rows are [xoff, xoff + n), the others are left out
+// of the ranges.  win: the gather source has 2^24+ rows, so every column must
+// lie within kWinRows / 2 of its strip's own row (spans[3] bit 1 otherwise).
 __global__ __launch_bounds__(256) void k_wf_deps(int64_t n, int TR, const int64_t *__restrict__ rp,
                                                  const int32_t *__restrict__ col, int2 *__restrict__ deps,
-                                                 int16_t *__restrict__ col16, int *__restrict__ spans, int64_t ncol)
+                                                 int16_t *__restrict__ col16, int *__restrict__ spans, int64_t xoff,
+                                                 int win)
 {
     __shared__ int smin[4], smax[4];
     const int64_t T = ceil_div(n, (int64_t)TR);
     const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
     const int ns = TR / 16;
-    int sb = 0, sf = 0, sw = 0, bad = 0;  // this block's span maxima (thread 0) and range flag
+    int sb = 0, sf = 0, sw = 0, bad = 0, far = 0;  // span maxima (thread 0), int16 / window range flags
     for (int64_t t = blockIdx.x; t < T; t += gridDim.x) {
         int mn = INT_MAX, mx = -1;
         for (int s = w; s < ns; s += 4) {
@@ -87,13 +92,14 @@ __global__ __launch_bounds__(256) void k_wf_deps(int64_t n, int TR, const int64_
             if (s0 >= n) break;
             const int64_t s1 = s0 + 16 < n ? s0 + 16 : n;
             for (int64_t k = rp[s0] + lane, e = rp[s1]; k < e; k += 64) {
-                const int c = col[k];
-                if (c < ncol) {  // (a distributed rank's halo columns: its boundary tiles, no flags)
-                    mn = c < mn ? c : mn;
-                    mx = c > mx ? c : mx;
+                const int64_t c = (int64_t)col[k] - xoff;  // local row (own rows: [0, n))
+                if (c >= 0 && c < n) {  // (other columns: a rank's halo / peers' slots, boundary tiles)
+                    mn = c < mn ? (int)c : mn;
+                    mx = c > mx ? (int)c : mx;
                 }
+                const int64_t d = c - s0;
+                if (win) far |= (d < -(kWinRows / 2) + 32) | (d > kWinRows / 2 - 32);
                 if (col16) {
-                    const int64_t d = (int64_t)c - s0;
                     bad |= (d < -32768) | (d > 32767);
                     col16[k] = (int16_t)d;
                 }
@@ -129,6 +135,7 @@ __global__ __launch_bounds__(256) void k_wf_deps(int64_t n, int TR, const int64_
         __syncthreads();
     }
     if (__ballot(bad) != 0 && lane == 0) atomicOr(&spans[3], 1);
+    if (__ballot(far) != 0 && lane == 0) atomicOr(&spans[3], 2);
     if (threadIdx.x == 0) {
         atomicMax(&spans[0], sb);
         atomicMax(&spans[1], sf);
@@ -151,19 +158,27 @@ __device__ __forceinline__ double dpp_swap1(double x)
     return r;
 }
 
-// The step kernel.  P2 == nullptr: the first launch of a solve (pass 1 only,
-// on Vg = B; no flags).  P1 == nullptr: no V_{j-1} term (step 0).  Vprev and
-// Vout may alias (V_{j+1} over V_{j-1}: each strip is read, then written, by
-// one wave); Vg == Vout when P2 != nullptr.  part: S1 slabs at [0, G), S2 at
-// [G, 2G), G at [2G, 3G) (256 doubles each, one per block).
-template <int NC, int CAP, int K, int NL, int NU, int DU, bool C16>
+// The step kernel.  P2 == nullptr: pass 1 only (the first launch of a solve,
+// on Vg = B, or a distributed rank's boundary tiles; no flags).  P1 ==
+// nullptr: no V_{j-1} term (step 0).  Vprev and Vout may alias (V_{j+1} over
+// V_{j-1}: each strip is read, then written, by one wave).  With P2, Vout is
+// the gather source's own rows: Vg + 16 xoff.  part: S1 slabs at [0, G), S2
+// at [G, 2G), G at [2G, 3G) (256 doubles each, one per block).
+// Distributed forms: pass 1 over tiles [p1a, p1b) and pass 2 over the tiles
+// [q0, q1) u [q2, q3) (a pass-2-only launch may take two ranges; with pass-1
+// tiles q2 == q3); xoff = the gather-source row of local row 0 (the
+// all-gather form's slot), a gather source of 2^24+ rows read through a
+// per-strip window of kWinRows rows (the plan proved every column inside);
+// SW: pass 2 also stores V_j's rows into Vsave (over V_{j-1}, read earlier by
+// the same wave), so V_{j+1} can take V_j's place in the all-gather slot.
+template <int NC, int CAP, int K, int NL, int NU, int DU, bool C16, bool SW = false>
 __global__ __launch_bounds__(64 * (NC + NL + NU)) void k_wf16(
     int64_t n, const int64_t *__restrict__ rp, const int32_t *__restrict__ col, const int16_t *__restrict__ col16,
     const double *__restrict__ val, const uint64_t *__restrict__ pairs, const double *Yj, const double *Vprev,
-    const double *__restrict__ Vj, double *Vout, const double *__restrict__ binv, const double *__restrict__ P1,
+    const double *Vj, double *Vout, const double *__restrict__ binv, const double *__restrict__ P1,
     const double *__restrict__ P2, const double *Vg, double *Yo, const int2 *__restrict__ deps, int *flags, int epoch,
     int64_t hback, int lead, double *__restrict__ part, int *__restrict__ err, int dbg, int64_t nx, int64_t p1a,
-    int64_t p1b, int64_t Th, int cpol)
+    int64_t p1b, int64_t Th, int cpol, int64_t xoff, int64_t q0, int64_t q1, int64_t q2, int64_t q3, double *Vsave)
 {
     using CT = typename std::conditional<C16, int16_t, int32_t>::type;
     using C = FwCfg<NC, CAP, true, true, CT>;
@@ -200,18 +215,27 @@ __global__ __launch_bounds__(64 * (NC + NL + NU)) void k_wf16(
     // same range moved hback tiles down, so the pass-2 wavefront leads
     // (pass-1 tiles: [p1a, p1b) -- all of them, or the interior ones of a
     // distributed rank; pass 2 covers every tile)
+    // (pass-2 tiles by a virtual index v in [0, NQ): v < nq1 -> tile q0 + v,
+    // else q2 + v - nq1; region bounds pbeg / pend are virtual)
     int64_t begin, end, kb, KB, pbeg, pend;
-    const int64_t NP1 = p1b - p1a;
+    const int64_t NP1 = p1b - p1a, nq1 = q1 - q0, NQ = nq1 + (q3 - q2);
+    auto ptile = [&](int64_t v) { return v < nq1 ? q0 + v : q2 + (v - nq1); };
+    auto clampq = [&](int64_t v) { return v < 0 ? (int64_t)0 : (v > NQ ? NQ : v); };
     if (G < 8) {
-        begin = p1a; end = p1b; kb = bid; KB = G; pbeg = 0; pend = T;
+        begin = p1a; end = p1b; kb = bid; KB = G; pbeg = 0; pend = NQ;
     } else {
         const int64_t x = bid & 7;
         begin = p1a + NP1 * x / 8;
         end = p1a + NP1 * (x + 1) / 8;
         kb = bid >> 3;
         KB = (G - x + 7) >> 3;
-        pbeg = x == 0 ? 0 : (begin - hback > 0 ? begin - hback : 0);
-        pend = x == 7 ? T : (end - hback > 0 ? end - hback : 0);
+        if (NP1 > 0) {  // (one pass-2 range)
+            pbeg = x == 0 ? 0 : clampq(begin - hback - q0);
+            pend = x == 7 ? NQ : clampq(end - hback - q0);
+        } else {  // pass 2 only: the (virtual) range split evenly
+            pbeg = NQ * x / 8;
+            pend = NQ * (x + 1) / 8;
+        }
     }
     int64_t nt = (end - begin - kb + KB - 1) / KB > 0 ? (end - begin - kb + KB - 1) / KB : 0;
     if (dbg & 4) nt = 0;  // timing diagnostics (LZ_WF_DBG): no pass-1 tiles
@@ -306,7 +330,7 @@ __global__ __launch_bounds__(64 * (NC + NL + NU)) void k_wf16(
                 bq[1][kc] = has_prev ? -P1[idx] : 0.0;
                 bq[2][kc] = -P2[idx];
             }
-            const int64_t ut0 = pbeg + kb + uw * KB, ustep = (int64_t)NU * KB;
+            const int64_t ut0 = pbeg + kb + uw * KB, ustep = (int64_t)NU * KB;  // (virtual indices)
             const int64_t ntl = ut0 < pend ? (pend - ut0 + ustep - 1) / ustep : 0;
             const int64_t ns = ntl * NC;  // strips of this wave's tiles, in order
             const int bytes = (int)(n * 128);
@@ -316,7 +340,8 @@ __global__ __launch_bounds__(64 * (NC + NL + NU)) void k_wf16(
                                                   has_prev ? bytes : 0, 0x00020000),
                 __builtin_amdgcn_make_buffer_rsrc(const_cast<double *>(Vj), (short)0, bytes, 0x00020000)};
             const auto Or = __builtin_amdgcn_make_buffer_rsrc(Vout, (short)0, bytes, 0x00020000);
-            auto strip_r0 = [&](int64_t s) { return (ut0 + (s / NC) * ustep) * TR + 16 * (s % NC); };
+            const auto Sr = __builtin_amdgcn_make_buffer_rsrc(SW ? Vsave : Vout, (short)0, SW ? bytes : 0, 0x00020000);
+            auto strip_r0 = [&](int64_t s) { return ptile(ut0 + (s / NC) * ustep) * TR + 16 * (s % NC); };
             // this lane's DMA pieces: LDS piece q = 64 k + lane holds row q >> 3,
             // global piece (q & 7) ^ swizzle
             uint32_t goff[2];
@@ -339,7 +364,7 @@ __global__ __launch_bounds__(64 * (NC + NL + NU)) void k_wf16(
             // pace from the pass-1 start: the host's lead covers an offset of
             // hback between the two ranges, and the first pass-1 tile needs the
             // pass-2 tiles at block positions up to (p1a + hfwd) / KB.
-            const int64_t gap = begin - pbeg - hback;
+            const int64_t gap = begin - (NQ > 0 ? ptile(pbeg < NQ ? pbeg : NQ - 1) : 0) - hback;
             const int64_t poff = gap > 0 ? (gap + KB - 1) / KB : 0;
             int64_t paced = -1;  // last tile cleared
             auto pace = [&](int64_t s) {
@@ -385,13 +410,15 @@ __global__ __launch_bounds__(64 * (NC + NL + NU)) void k_wf16(
             for (int64_t s = 0; s < ns; ++s) {
                 dma(s + DU);
                 // strip s landed: DU younger strips' six DMAs each, and from the
-                // steady state on also DU strips' two stores, were issued after it
+                // steady state on also DU strips' two (SW: four) stores, were
+                // issued after it
+                constexpr int ST = SW ? 4 : 2;
                 if (s < DU) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(6 * DU) : "memory");
-                else asm volatile("s_waitcnt vmcnt(%0)" ::"n"(8 * DU) : "memory");
+                else asm volatile("s_waitcnt vmcnt(%0)" ::"n"((6 + ST) * DU) : "memory");
                 if (s % NC == DU && s >= NC && lane == 0)
                     // tile s / NC - 1 ended with strip s - DU - 1, whose stores
                     // are older than strip s's DMA: drained
-                    __hip_atomic_store(flags + ut0 + (s / NC - 1) * ustep, epoch, __ATOMIC_RELAXED,
+                    __hip_atomic_store(flags + ptile(ut0 + (s / NC - 1) * ustep), epoch, __ATOMIC_RELAXED,
                                        __HIP_MEMORY_SCOPE_AGENT);
                 const uint32_t sb = ws_lds_addr(reinterpret_cast<int *>(&ust[uw][(int)(s % (DU + 1))][0][0]));
                 d2_t y0, y1, p0, p1, j0, j1;
@@ -444,10 +471,25 @@ __global__ __launch_bounds__(64 * (NC + NL + NU)) void k_wf16(
                     if (cpol & 8) __builtin_amdgcn_raw_buffer_store_b128(*reinterpret_cast<const v4u32_t *>(&v), Or, off, 0, SA | 2);
                     else __builtin_amdgcn_raw_buffer_store_b128(*reinterpret_cast<const v4u32_t *>(&v), Or, off, 0, SA);
                 }
+                if constexpr (SW) {
+                    // V_j's strip (slot part 2, as the DMA laid it out) to Vsave:
+                    // the DMA's own global offsets, so the pieces land unswizzled
+                    v4u32_t vp0, vp1;
+                    asm volatile(
+                        "ds_read_b128 %0, %2 offset:4096\n\t"
+                        "ds_read_b128 %1, %2 offset:5120\n\t"
+                        "s_waitcnt lgkmcnt(0)"
+                        : "=&v"(vp0), "=&v"(vp1)
+                        : "v"(sb + 16u * (uint32_t)lane)
+                        : "memory");
+                    __builtin_amdgcn_raw_buffer_store_b128(vp0, Sr, r0b + goff[0], 0, 2);
+                    __builtin_amdgcn_raw_buffer_store_b128(vp1, Sr, r0b + goff[1], 0, 2);
+                }
             }
             asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
             if (ntl > 0 && lane == 0)
-                __hip_atomic_store(flags + ut0 + (ntl - 1) * ustep, epoch, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                __hip_atomic_store(flags + ptile(ut0 + (ntl - 1) * ustep), epoch, __ATOMIC_RELAXED,
+                                   __HIP_MEMORY_SCOPE_AGENT);
         }
         // the NU updater slabs folded by the last updater to finish (slot 0
         // of each updater is free now)
@@ -479,7 +521,19 @@ __global__ __launch_bounds__(64 * (NC + NL + NU)) void k_wf16(
         else if (pr == 2) __builtin_amdgcn_s_setprio(2);
     }
     const int bytes = (int)(n * 128);
-    const auto xr = __builtin_amdgcn_make_buffer_rsrc(const_cast<double *>(Vg), (short)0, (int)(nx * 128), 0x00020000);
+    // the gather source through a buffer resource: all of it below 2^24 rows,
+    // else a window of kWinRows rows centred on the strip's own row (wb: the
+    // window's first row; the plan proved every column inside it)
+    const bool win = nx >= kWinRows;
+    auto xwin = [&](int64_t s0, int64_t &wb) {
+        const int64_t c = xoff + s0 - kWinRows / 2;
+        wb = win ? (c > 0 ? c : 0) : 0;
+        const int64_t rows = win ? (nx - wb < kWinRows ? nx - wb : kWinRows) : nx;
+        return __builtin_amdgcn_make_buffer_rsrc(const_cast<double *>(Vg + wb * 16), (short)0, (int)(rows * 128),
+                                                 0x00020000);
+    };
+    int64_t wb0 = 0;
+    auto xr = xwin(0, wb0);
     const auto yr = __builtin_amdgcn_make_buffer_rsrc(Yo, (short)0, bytes, 0x00020000);
     double *S0 = scr[cw];
     d4_t macc = {0.0, 0.0, 0.0, 0.0};
@@ -507,6 +561,8 @@ __global__ __launch_bounds__(64 * (NC + NL + NU)) void k_wf16(
         const int64_t s0 = r0 + 16 * cw;
         const int g = lane >> 3, p = lane & 7;
         const uint32_t lane_off = 16u * p;
+        int64_t wb = 0;
+        if (win) xr = xwin(s0, wb);
         long spin = 0;
         while (__hip_atomic_load(&ready[s], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP) != (int)i &&
                ++spin < kWsSpin)
@@ -529,7 +585,9 @@ __global__ __launch_bounds__(64 * (NC + NL + NU)) void k_wf16(
         double y[4] = {0.0, 0.0, 0.0, 0.0};
         if (runlen <= CAP) {  // tile-uniform
             const CT *cp = S.col + co;
-            const uint32_t cb16 = C16 ? (uint32_t)s0 : 0u;
+            // column -> window row: C16 columns are offsets from the strip's own
+            // row (xoff + s0), 32-bit ones gather-source rows
+            const uint32_t cb16 = C16 ? (uint32_t)(xoff + s0 - wb) : (uint32_t)(-wb);
             const double *vp = S.val + vo;
             auto slot = [&](int ff) {
                 const int o = ff < len0 ? o0 + ff : o1 + (ff - len0);
@@ -541,9 +599,8 @@ __global__ __launch_bounds__(64 * (NC + NL + NU)) void k_wf16(
                 for (int tt = 0; tt < 8; ++tt) cc[tt] = cp[slot(f + tt)];
 #pragma unroll
                 for (int tt = 0; tt < 8; ++tt) {
-                    const uint32_t off = f + tt < cnt
-                                             ? __umul24(C16 ? (unsigned)cc[tt] + cb16 : (unsigned)cc[tt], 128u) + lane_off
-                                             : 0x80000000u;
+                    const uint32_t off = f + tt < cnt ? __umul24((unsigned)cc[tt] + cb16, 128u) + lane_off
+                                                      : 0x80000000u;
                     const auto u4 = __builtin_amdgcn_raw_buffer_load_b128(xr, off, 0, GA);
                     __builtin_memcpy(&xs[tt], &u4, 16);
                 }
@@ -572,7 +629,7 @@ __global__ __launch_bounds__(64 * (NC + NL + NU)) void k_wf16(
         } else {  // long run (rare): epilogue first, then gather from global
             if (s0p >= 0) epilogue();
             ws_gather<const int32_t *, const double *, GA>(col + kA, val + kA, o0, len0, o1, cnt, xr, lane_off,
-                                                               y, 0u);
+                                                               y, (uint32_t)wb);
         }
         // the CSR stage is no longer read by this wave
         asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
@@ -603,7 +660,7 @@ __global__ __launch_bounds__(64 * (NC + NL + NU)) void k_wf16(
         for (int h2 = 0; h2 < 2; ++h2) {
             const int c = lane & 15;
             const int64_t row = s0 + 8 * h2 + 4 * (c & 1) + (lane >> 4);
-            const uint32_t off = row < n ? (uint32_t)(row * 128 + (c & ~1) * 8) : 0x80000000u;
+            const uint32_t off = row < n ? (uint32_t)((xoff + row - wb) * 128 + (c & ~1) * 8) : 0x80000000u;
             const auto u = __builtin_amdgcn_raw_buffer_load_b128(xr, off, 0, GA);
             __builtin_memcpy(&v1[2 * h2], &u, 16);
         }
@@ -634,7 +691,8 @@ __global__ __launch_bounds__(64 * (NC + NL + NU)) void k_wf16(
     }
 }
 
-int wf_plan16(lz_handle *h, int64_t n, int64_t nnz, const int64_t *rp, const int32_t *col, WfPlan *pl, int64_t nx)
+int wf_plan16(lz_handle *h, int64_t n, int64_t nnz, const int64_t *rp, const int32_t *col, WfPlan *pl, int64_t nx,
+              int64_t xoff)
 {
     if (nx < 0) nx = n;
     pl->ok = false;
@@ -651,7 +709,11 @@ int wf_plan16(lz_handle *h, int64_t n, int64_t nnz, const int64_t *rp, const int
     pl->var = wide ? 200 : (want == 10 || want == 11 || want == 12) ? 0 : 111;
     pl->nc = pl->var == 200 ? 10 : pl->var ? 11 : want;
     pl->tr = 16 * pl->nc;
-    if ((e && e[0] == '0') || n < pl->tr || nx >= (1 << 24) || (double)nnz > kWfWideRow * (double)n) return LZ_OK;
+    // (a gather source of 2^24+ rows is read through per-strip windows: the
+    // plan below checks that every column falls inside its strip's)
+    if ((e && e[0] == '0') || n < pl->tr || n >= (1 << 24) || xoff < 0 || xoff + n > nx ||
+        (double)nnz > kWfWideRow * (double)n)
+        return LZ_OK;
     const int64_t T = ceil_div(n, (int64_t)pl->tr);
     if ((size_t)T + 64 > h->wf_cap) {
         LZ_HIP_TRY(hipStreamSynchronize(h->stream));
@@ -684,15 +746,16 @@ int wf_plan16(lz_handle *h, int64_t n, int64_t nnz, const int64_t *rp, const int
     // (one tile per block measured slower: its per-block atomics contend)
     const int grid = (int)std::max<int64_t>(1, std::min<int64_t>(T, (int64_t)h->n_cu * 8));
     hipLaunchKernelGGL(k_wf_deps, dim3(grid), dim3(256), 0, h->stream, n, pl->tr, rp, col,
-                       static_cast<int2 *>(h->wf_deps), c16, spans, n);
+                       static_cast<int2 *>(h->wf_deps), c16, spans, xoff, nx >= kWinRows ? 1 : 0);
     LZ_LAUNCH_CHECK();
     int sp[4] = {0, 0, 0, 1};
     LZ_HIP_TRY(hipMemcpyAsync(sp, spans, sizeof(sp), hipMemcpyDeviceToHost, h->stream));
     LZ_HIP_TRY(hipStreamSynchronize(h->stream));
     pl->hback = sp[0];
     pl->hfwd = sp[1];
-    pl->ok = sp[2] <= kWfMaxSpan;
-    if (c16 && sp[3] == 0) pl->col16 = c16;
+    pl->ok = sp[2] <= kWfMaxSpan && !(sp[3] & 2);
+    pl->xoff = xoff;
+    if (c16 && !(sp[3] & 1)) pl->col16 = c16;
     return LZ_OK;
 }
 
@@ -700,30 +763,45 @@ int wf_step16(lz_handle *h, int64_t n, const int64_t *rp, const int32_t *col, co
               const double *val, const uint64_t *pairs, const WfPlan &pl, const double *Yj, const double *Vprev,
               const double *Vj, double *Vout, const double *binv, const double *P1, const double *P2,
               const double *Vg, double *Yo, int epoch, int *nparts, int64_t nx, int64_t p1a, int64_t p1b,
-              double *part)
+              double *part, const int64_t *q, double *Vsave)
 {
     const int64_t T = ceil_div(n, (int64_t)pl.tr);
+    const int64_t xoff = pl.xoff;
     if (nx < 0) nx = n;
     if (p1b < 0) p1b = T;
     if (!part) part = h->partials2;
-    LZ_ARG_CHECK(nx >= n && nx < (1 << 24) && 0 <= p1a && p1a <= p1b && p1b <= T, "wavefront step ranges");
+    // pass-2 tiles [q0, q1) u [q2, q3) (default: all of them)
+    const int64_t q0 = q ? q[0] : 0, q1 = q ? q[1] : T, q2 = q ? q[2] : T, q3 = q ? q[3] : T;
+    LZ_ARG_CHECK(xoff >= 0 && xoff + n <= nx && 0 <= p1a && p1a <= p1b && p1b <= T, "wavefront step ranges");
+    LZ_ARG_CHECK(0 <= q0 && q0 <= q1 && q1 <= q2 && q2 <= q3 && q3 <= T && (p1a == p1b || q2 == q3),
+                 "wavefront step pass-2 ranges");
     LZ_ARG_CHECK(pl.ok && n < (1 << 24), "wavefront step: wf_plan16 first");
     LZ_ARG_CHECK(pairs != nullptr, "strip row orders (strip_pairs) missing");
-    LZ_ARG_CHECK(P2 == nullptr || (Yj && Vj && Vout && binv && Vg == Vout), "wavefront step buffers");
+    LZ_ARG_CHECK(P2 == nullptr || (Yj && Vj && Vout && binv && Vout == Vg + 16 * xoff), "wavefront step buffers");
+    LZ_ARG_CHECK(Vsave == nullptr || (P2 && pl.var != 0), "wavefront step: SW stores (the 111 / wide shapes)");
     static_assert(12 <= kPairPad, "row orders must cover the last tile's strips");
-    // pass 2 covers every tile when it runs; a pass-1-only launch its range
-    const int64_t work = P2 ? T : p1b - p1a;
+    // pass 2 covers its tile ranges when it runs; a pass-1-only launch its range
+    const int64_t nq = (q1 - q0) + (q3 - q2);
+    const int64_t work = P2 ? std::max(nq, p1b - p1a) : p1b - p1a;
     if (work <= 0) {
         *nparts = 0;
         return LZ_OK;
     }
-    // (virtual ranks sharing the device: each rank's share, so every grid is resident)
-    const int grid = (int)std::max<int64_t>(1, std::min<int64_t>(work, h->grid_cap > 0 ? h->grid_cap : h->n_cu));
+    // (virtual ranks sharing the device: each rank's share, so every grid is
+    // resident; LZ_GRID_CAP, read per call: a cap for measurement, e.g. one
+    // virtual rank's share of the CUs run alone)
+    const char *gc = getenv("LZ_GRID_CAP");
+    const int cap = gc && atoi(gc) > 0 ? atoi(gc) : (h->grid_cap > 0 ? h->grid_cap : h->n_cu);
+    const int grid = (int)std::max<int64_t>(1, std::min<int64_t>(work, std::min(cap, h->n_cu)));
     // LZ_WF_DBG (timing diagnostics only; results are wrong): bit 0 skips the
     // loaders' flag polls, bit 1 the updaters' work, bit 2 the pass-1 tiles;
     // bit 3 / bit 6 run the updaters at issue priority 0 / 3 (default 2)
     const char *dg = getenv("LZ_WF_DBG");
     const int dbg = dg ? atoi(dg) : 0;
+    if (P2 && nq == 0 && p1a == p1b) {  // nothing to do
+        *nparts = 0;
+        return LZ_OK;
+    }
     // the updaters' pace (tiles ahead of the block's pass 1): at least the
     // tiles a pass-1 tile reaches ahead in the block's order, plus two
     const int KB = grid < 8 ? grid : grid / 8;
@@ -740,12 +818,18 @@ int wf_step16(lz_handle *h, int64_t n, const int64_t *rp, const int32_t *col, co
     const int cpol = cp ? atoi(cp) : 7;
     // Liveness needs every block resident at once (their waits on each other's
     // flags).  The launch is checked: the occupancy of the instantiation at its
-    // block size must admit the grid, and by default it goes out as a
+    // block size must admit the grid (one block per CU, grid <= CUs).  A block
+    // that lands on a CU another kernel still holds starts when that kernel
+    // ends; the bounded waits cover that, so no kernel that itself waits on
+    // this launch may share the device (lz_hip.h).  LZ_WF_COOP=1 makes it a
     // cooperative launch, which the runtime refuses (instead of running part of
-    // the grid later) when the grid cannot be resident.  LZ_WF_COOP=0: an
-    // ordinary launch after the same occupancy check (A/B).
+    // the grid later) when the grid cannot be resident: measured 0.3-0.8 %
+    // slower at C3 (profiles/r04b_coop_ab.log), and the runtime runs such
+    // launches one at a time, so 8 virtual ranks' step launches serialised (C4
+    // at N = 8 virtual ranks: 106 ms per step against 57.4 ordinary) and an
+    // exchange's kernels could not overlap the step launch.
     const char *co = getenv("LZ_WF_COOP");
-    const bool coop = !(co && co[0] == '0');
+    const bool coop = co && co[0] == '1';
     int rc = LZ_OK;
     const int ev = prof_begin(h, PROF_SPMM_PASS);
     // (the block is 64 (NC + NL + NU) threads: the kernel refuses any other size)
@@ -761,8 +845,10 @@ int wf_step16(lz_handle *h, int64_t n, const int64_t *rp, const int32_t *col, co
         }
         const int2 *deps = static_cast<const int2 *>(h->wf_deps);
         int *flags = h->wf_flags, *err = h->err_flag;
-        int64_t a_n = n, a_hb = pl.hback, a_nx = nx, a_p1a = p1a, a_p1b = p1b, a_T = T;
+        int64_t a_n = n, a_hb = pl.hback, a_nx = nx, a_p1a = p1a, a_p1b = p1b, a_T = T, a_xo = xoff, a_q0 = q0,
+                a_q1 = q1, a_q2 = q2, a_q3 = q3;
         int a_ep = epoch, a_lead = lead, a_dbg = dbg, a_cp = cpol;
+        double *a_sv = Vsave;
         const int64_t *a_rp = rp;
         const int32_t *a_col = col;
         const int16_t *a_c16 = col16;
@@ -773,7 +859,8 @@ int wf_step16(lz_handle *h, int64_t n, const int64_t *rp, const int32_t *col, co
         if (coop) {
             void *args[] = {&a_n,  &a_rp, &a_col, &a_c16, &a_val, &a_pr,    &a_Yj, &a_Vp,  &a_Vj, &a_Vo,
                             &a_bi, &a_P1, &a_P2,  &a_Vg,  &a_Yo,  &deps,    &flags, &a_ep, &a_hb, &a_lead,
-                            &a_part, &err, &a_dbg, &a_nx, &a_p1a, &a_p1b, &a_T,   &a_cp};
+                            &a_part, &err, &a_dbg, &a_nx, &a_p1a, &a_p1b, &a_T,   &a_cp, &a_xo, &a_q0,
+                            &a_q1, &a_q2, &a_q3, &a_sv};
             const hipError_t e = hipLaunchCooperativeKernel(reinterpret_cast<const void *>(kern), dim3(grid),
                                                             dim3(64 * waves), args, 0, h->stream);
             if (e != hipSuccess) {
@@ -784,14 +871,19 @@ int wf_step16(lz_handle *h, int64_t n, const int64_t *rp, const int32_t *col, co
         }
         hipLaunchKernelGGL(kern, dim3(grid), dim3(64 * waves), 0, h->stream, a_n, a_rp, a_col, a_c16, a_val, a_pr,
                            a_Yj, a_Vp, a_Vj, a_Vo, a_bi, a_P1, a_P2, a_Vg, a_Yo, deps, flags, a_ep, a_hb, a_lead,
-                           a_part, err, a_dbg, a_nx, a_p1a, a_p1b, a_T, a_cp);
+                           a_part, err, a_dbg, a_nx, a_p1a, a_p1b, a_T, a_cp, a_xo, a_q0, a_q1, a_q2, a_q3, a_sv);
     };
     // LDS (<= 160 KB): strip slots per updater DU + 1, fewer with 32-bit columns
     constexpr int cap12 = 12 * 16 * kWfCapPerRow, cap11 = 11 * 16 * kWfCapPerRow, cap10 = 10 * 16 * kWfCapPerRow;
     // (the instantiation must match pl.tr: the tile count above is the host's)
-    if (pl.var == 200 && col16) go(k_wf16<10, kWfWideCap, 2, 1, 3, 1, true>, 10 + 1 + 3);
+    const bool sw = Vsave != nullptr;
+    if (pl.var == 200 && col16 && sw) go(k_wf16<10, kWfWideCap, 2, 1, 3, 1, true, true>, 10 + 1 + 3);
+    else if (pl.var == 200 && col16) go(k_wf16<10, kWfWideCap, 2, 1, 3, 1, true>, 10 + 1 + 3);
+    else if (pl.var == 200 && sw) go(k_wf16<10, kWfWideCap, 2, 1, 2, 1, false, true>, 10 + 1 + 2);
     else if (pl.var == 200) go(k_wf16<10, kWfWideCap, 2, 1, 2, 1, false>, 10 + 1 + 2);
+    else if (pl.var == 111 && col16 && sw) go(k_wf16<11, cap11, kWfK, 1, 4, 1, true, true>, 11 + 1 + 4);
     else if (pl.var == 111 && col16) go(k_wf16<11, cap11, kWfK, 1, 4, 1, true>, 11 + 1 + 4);
+    else if (pl.var == 111 && sw) go(k_wf16<11, cap11, kWfK, 1, 4, 1, false, true>, 11 + 1 + 4);
     else if (pl.var == 111) go(k_wf16<11, cap11, kWfK, 1, 4, 1, false>, 11 + 1 + 4);
     else if (col16) {
         if (pl.nc == 12) go(k_wf16<12, cap12, kWfK, kWfNL, 2, 3, true>, 12 + kWfNL + 2);
@@ -809,16 +901,16 @@ int wf_step16(lz_handle *h, int64_t n, const int64_t *rp, const int32_t *col, co
     return LZ_OK;
 }
 
-// The wavefront step's three sums: out[0, 256) = S1 over the step launch's G
-// slabs (and, distributed, the boundary launches' G1 and G2), out[256, 512) =
-// S2 and out[512, 768) = G of the step launch.  12 blocks, so that no CU pulls
-// more than an eighth of a megabyte (one CU alone reads ~64 B per clock):
-// block (m, r) sums entries [64 r, 64 r + 64) of matrix m; thread (q, i) adds
-// slabs q, q + 16, ... with four independent accumulators, then the 16 partial
-// sums are added in a fixed tree -- bitwise reproducible.
-__global__ __launch_bounds__(1024) void k_wf_fold(const double *__restrict__ kp, int G, const double *__restrict__ b1,
-                                                  int G1, const double *__restrict__ b2, int G2,
-                                                  double *__restrict__ out)
+// The wavefront step's three sums over the slab sets of one step's launches
+// (one set single-GPU; a distributed step's pass-2 launches, its step launch
+// and its boundary launches): set t holds [S1 | S2 | G] of sl.g[t] block slabs
+// each, at sl.p[t]; out[256 m, 256 m + 256) = matrix m summed over every set,
+// sets in order.  12 blocks, so that no CU pulls more than an eighth of a
+// megabyte (one CU alone reads ~64 B per clock): block (m, r) sums entries
+// [64 r, 64 r + 64) of matrix m; thread (q, i) adds slabs q, q + 16, ... with
+// four independent accumulators, then the 16 partial sums are added in a
+// fixed tree -- bitwise reproducible.
+__global__ __launch_bounds__(1024) void k_wf_fold(WfSlabs sl, double *__restrict__ out)
 {
     __shared__ double ps[16][64];
     const int m = blockIdx.x >> 2, q = threadIdx.x >> 6, i = (blockIdx.x & 3) * 64 + (threadIdx.x & 63);
@@ -834,11 +926,10 @@ __global__ __launch_bounds__(1024) void k_wf_fold(const double *__restrict__ kp,
         for (; g < P; g += 16) a0 += p[(int64_t)g * 256 + i];
         return (a0 + a1) + (a2 + a3);
     };
-    double s = sum(kp + (int64_t)m * G * 256, G);
-    if (m == 0) {
-        s += sum(b1, G1);
-        s += sum(b2, G2);
-    }
+    double s = 0.0;
+    for (int t = 0; t < sl.k; ++t)
+        if (sl.g[t] > 0) s = t == 0 ? sum(sl.p[t] + (int64_t)m * sl.g[t] * 256, sl.g[t])
+                                    : s + sum(sl.p[t] + (int64_t)m * sl.g[t] * 256, sl.g[t]);
     ps[q][threadIdx.x & 63] = s;
     __syncthreads();
     if (q == 0) {
@@ -850,10 +941,11 @@ __global__ __launch_bounds__(1024) void k_wf_fold(const double *__restrict__ kp,
     }
 }
 
-int wf_fold16(lz_handle *h, const double *kp, int G, const double *b1, int G1, const double *b2, int G2, double *out)
+int wf_fold16(lz_handle *h, const WfSlabs &sl, double *out)
 {
+    LZ_ARG_CHECK(sl.k >= 1 && sl.k <= WfSlabs::kMax, "wavefront fold: 1..6 slab sets");
     const int ev = prof_begin(h, PROF_SMALL);
-    hipLaunchKernelGGL(k_wf_fold, dim3(12), dim3(1024), 0, h->stream, kp, G, b1, G1, b2, G2, out);
+    hipLaunchKernelGGL(k_wf_fold, dim3(12), dim3(1024), 0, h->stream, sl, out);
     prof_end(h, ev);
     LZ_LAUNCH_CHECK();
     return LZ_OK;

@@ -232,6 +232,10 @@ int lz_comm_abort(lz_handle *h);
  * beside the exchange in the handle's last distributed solve ({-1, -1}: the
  * solve ran unsplit). */
 int lz_debug_last_split(lz_handle *h, int64_t out[2]);
+/* Test support: out[0] = 1 when the handle's last distributed solve ran the
+ * wavefront step (b = 16 fp64), out[1] = 1 when it also ran the requested rows'
+ * pass 2 first and the halo exchange beside the rest of each step. */
+int lz_debug_last_wf(lz_handle *h, int out[2]);
 
 /* Distributed block Lanczos, all-gather form (the north star's exchange).
  * Every rank's slab is padded to n_pad rows (n_pad >= max rows per rank) and

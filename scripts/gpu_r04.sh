@@ -17,6 +17,11 @@ while [ $# -gt 0 ]; do
       while [ $# -gt 0 ] && [[ "$1" == *=* ]]; do cfgs+=("$1"); shift; done
       timeout -k 10 600 python -u scripts/ab_c3.py "${cfgs[@]}" --rounds 4 > $O/ab.log 2>&1 || { tail -20 $O/ab.log; exit 1; }
       tail -12 $O/ab.log; continue ;;
+    abspmm)
+      shift; cfgs=()
+      while [ $# -gt 0 ] && [[ "$1" == *=* ]]; do cfgs+=("$1"); shift; done
+      timeout -k 10 600 python -u scripts/ab_c3.py "${cfgs[@]}" --spmm-only --rounds 3 > $O/abspmm.log 2>&1 || { tail -20 $O/abspmm.log; exit 1; }
+      tail -12 $O/abspmm.log; continue ;;
     bench)
       timeout -k 10 600 python bench.py > $O/bench.json 2> $O/bench.err || { tail -30 $O/bench.err; exit 1; }
       python -c "import json;d=json.load(open('$O/bench.json'));print(d['value'],d['ms_per_step'],d['roofline']['frac'],d['roofline']['avg_ms'])" ;;

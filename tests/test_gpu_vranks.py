@@ -38,10 +38,11 @@ def _owner(bounds, row):
     return int(np.searchsorted(bounds, row, side="right") - 1)
 
 
-def run_dist(lz, torch, A, B, m, lc, nranks, form, overlap=True, bounds=None):
+def run_dist(lz, torch, A, B, m, lc, nranks, form, overlap=True, bounds=None, wf_out=None):
     """Run the distributed block Lanczos over `nranks` virtual ranks; returns
-    (q, alpha, beta) of lc's owner, the list of every rank's (alpha, beta), and
-    every rank's split (interior rows) or None."""
+    (q, alpha, beta) of lc's owner and every rank's split (interior rows) or
+    None; wf_out (a list) receives every rank's (wavefront step, pass-2-first
+    overlap) flags."""
     n, b = B.shape
     if bounds is None:
         bounds = lz.partition_rows(A, nranks)
@@ -82,7 +83,7 @@ def run_dist(lz, torch, A, B, m, lc, nranks, form, overlap=True, bounds=None):
             h.block_lanczos_dist(Ad, n_pad, n_pad * nranks, Bp, m, lc - bounds[lc_rank], lc_rank, q, al, be,
                                  None, W, X)
         assert h.device_error() == 0
-        return q.cpu().numpy(), al.cpu().numpy(), be.cpu().numpy(), h.last_split()
+        return q.cpu().numpy(), al.cpu().numpy(), be.cpu().numpy(), h.last_split(), h.last_wf()
 
     try:
         res = lz.run_virtual_ranks(nranks, rank_fn)
@@ -93,7 +94,9 @@ def run_dist(lz, torch, A, B, m, lc, nranks, form, overlap=True, bounds=None):
             os.environ["LZ_DIST_OVERLAP"] = old
     for r in range(1, nranks):  # every rank holds the same alpha / beta bits
         assert np.array_equal(res[r][1], res[0][1]) and np.array_equal(res[r][2][:m], res[0][2][:m]), r
-    q, al, be, _ = res[lc_rank]
+    q, al, be = res[lc_rank][:3]
+    if wf_out is not None:
+        wf_out.extend(x[4] for x in res)
     return (q, al, be), [x[3] for x in res]
 
 
@@ -101,12 +104,34 @@ def run_dist(lz, torch, A, B, m, lc, nranks, form, overlap=True, bounds=None):
 @pytest.mark.parametrize("nranks", [2, 4, 8])
 def test_vranks_b16_banded(lz, orc, torch_cuda, form, nranks):
     """Banded operator, nnz-balanced slabs, lc on a rank other than 0; the
-    interior rows' pass 1 runs beside the exchange (split must be on)."""
+    interior rows' pass 1 runs beside the exchange (split must be on).  The
+    halo form runs the wavefront step with the requested rows' pass 2 first and
+    the exchange beside the rest of the step (asserted); the all-gather form
+    the two-pass step (its default at N > 1)."""
     A = lz.gen_banded(120_011, 10.0, 1500, seed=100 + nranks)
     B = lz.uniform_B(A.n, 16, seed=7)
     m, lc = 7, 120_011 * 5 // 8 + 3
-    got, splits = run_dist(lz, torch_cuda, A, B, m, lc, nranks, form)
+    wfs = []
+    got, splits = run_dist(lz, torch_cuda, A, B, m, lc, nranks, form, wf_out=wfs)
     assert all(s is not None for s in splits), splits  # every rank split its rows
+    assert all(w == ((True, True) if form == "halo" else (False, False)) for w in wfs), wfs
+    assert_close_run(lz, m, 16, got, orc.block_lanczos(A, B, m, lc))
+
+
+@pytest.mark.parametrize("nranks", [1, 2, 4, 8])
+def test_vranks_b16_allgather_wavefront(lz, orc, torch_cuda, monkeypatch, nranks):
+    """The all-gather form on the wavefront step (LZ_AG_WF=1; the default at
+    one rank): pass 2 writes V_{j+1} into the rank's slot of X_full and V_j into
+    W, the in-place all-gather fills the peers' slots, then the boundary tiles."""
+    monkeypatch.setenv("LZ_AG_WF", "1")
+    A = lz.gen_banded(120_011, 10.0, 1500, seed=110 + nranks)
+    B = lz.uniform_B(A.n, 16, seed=8)
+    m, lc = 7, 120_011 // 3 + 5
+    wfs = []
+    got, splits = run_dist(lz, torch_cuda, A, B, m, lc, nranks, "allgather", wf_out=wfs)
+    assert all(w[0] for w in wfs), wfs
+    if nranks > 1:
+        assert all(s is not None for s in splits), splits
     assert_close_run(lz, m, 16, got, orc.block_lanczos(A, B, m, lc))
 
 
@@ -197,15 +222,20 @@ def test_vranks_b32_f32(lz, orc, torch_cuda, form):
     assert np.allclose(q, qo, rtol=1e-4, atol=1e-4 * np.abs(qo).max())
 
 
-def test_vranks_allgather_wide_window(lz, orc, torch_cuda):
+@pytest.mark.parametrize("wf", ["0", "1"])
+def test_vranks_allgather_wide_window(lz, orc, torch_cuda, monkeypatch, wf):
     """8 ranks whose gathered block has 8 * n_pad >= 2^24 rows (2.2 GB at b = 16
-    fp64): pass 1 gathers through its 2^24-row window, interior split on."""
+    fp64): pass 1 gathers through its 2^24-row window, interior split on; in
+    the two-pass step and (LZ_AG_WF=1) in the wavefront step."""
+    monkeypatch.setenv("LZ_AG_WF", wf)
     n = 8 * ((1 << 21) + 1000)
     A = lz.gen_banded(n, 3.0, 200, seed=41)
     B = lz.uniform_B(A.n, 16, seed=42)
     m, lc = 3, n - 77
-    got, splits = run_dist(lz, torch_cuda, A, B, m, lc, 8, "allgather")
+    wfs = []
+    got, splits = run_dist(lz, torch_cuda, A, B, m, lc, 8, "allgather", wf_out=wfs)
     assert all(s is not None for s in splits)
+    assert all(w[0] == (wf == "1") for w in wfs), wfs
     assert_close_run(lz, m, 16, got, orc.block_lanczos(A, B, m, lc))
 
 
