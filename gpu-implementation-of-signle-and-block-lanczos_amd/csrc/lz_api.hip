@@ -961,12 +961,16 @@ static int dist_solve_wf16(lz_handle *h, int form, HaloPlan *hp, int64_t n, int6
     LZ_TRY(allreduce(3 * bb));
     LZ_TRY(alpha_wf16(h, slab, 1, binv[0], nullptr, alpha, P2, ag ? slot : X0, lcl, n, q));
     const double *Vm1 = nullptr, *V0 = ag ? slot : X0;
+    // all-gather form at N > 1: V_{j+1} into the slot over V_j, V_j into X1 (=
+    // W) over V_{j-1}, so the slot can be all-gathered in place.  At one rank
+    // there is no all-gather: V_{j+1} goes over V_{j-1}, alternating between
+    // X_full and W as in the halo form (no V_j copy).
+    const bool sw = ag && h->nranks > 1;
     for (int j = 0; j + 1 < m; ++j) {
-        // (all-gather: V_{j+1} into the slot over V_j, V_j into X1 over V_{j-1})
-        double *Vn = ag ? slot : ((j & 1) ? X0 : X1);
-        double *Vg = ag ? X0 : Vn;
-        const double *Vprev = ag ? (j ? X1 : nullptr) : Vm1;
-        double *Vsave = ag ? X1 : nullptr;
+        double *Vn = sw ? slot : ((j & 1) ? X0 : X1);
+        double *Vg = sw ? X0 : Vn;
+        const double *Vprev = sw ? (j ? X1 : nullptr) : Vm1;
+        double *Vsave = sw ? X1 : nullptr;
         WfSlabs sl;
         double *part = h->partials2;
         int Gp = 0, Gk = 0, G1 = 0, G2 = 0;
