@@ -96,6 +96,8 @@ HIP_SYMBOLS = [
     ("lz_comm_abort", _c_int, [_c_vp]),
     ("lz_debug_last_split", _c_int, [_c_vp, _c_vp]),
     ("lz_debug_last_wf", _c_int, [_c_vp, ctypes.POINTER(_c_int)]),
+    ("lz_debug_wf_plan", _c_int, [_c_vp, _c_i64, _c_i64, _c_vp, _c_vp, _c_i64, _c_i64, _c_vp, _c_vp,
+                                  ctypes.POINTER(_c_int)]),
     ("lz_block_lanczos_dist", _c_int, [_c_vp, _c_i64, _c_i64, _c_i64, _c_i64, _c_vp, _c_vp, _c_vp,
                                        _c_int, _c_int, _c_int, _c_i64, _c_int, _c_vp, _c_vp, _c_vp,
                                        _c_vp, _c_vp, _c_vp, _c_vp, _c_vp]),
@@ -602,6 +604,22 @@ class Handle:
         v = (_c_int * 2)()
         _check(self.L.lz_debug_last_wf(self._h, v), "lz_debug_last_wf")
         return bool(v[0]), bool(v[1])
+
+    def wf_plan(self, A, nx=None, xoff=0):
+        """The wavefront step's plan of device operator A (test hook): (info dict,
+        deps (T, 2) int32 tensor, col16 (nnz,) int16 tensor)."""
+        import torch
+        T_max = A.n // 16 + 2
+        deps = torch.zeros(T_max * 2, dtype=torch.int32, device=A.row_ptr.device)
+        c16 = torch.zeros(max(A.nnz, 1), dtype=torch.int16, device=A.row_ptr.device)
+        info = (_c_int * 8)()
+        _check(self.L.lz_debug_wf_plan(self.ptr, A.n, A.nnz, A.row_ptr.data_ptr(), A.col.data_ptr(),
+                                       A.n if nx is None else nx, xoff, deps.data_ptr(), c16.data_ptr(), info),
+               "lz_debug_wf_plan")
+        T = int(info[2])
+        d = {"ok": bool(info[0]), "col16": bool(info[1]), "T": T, "tr": int(info[3]),
+             "spans": [int(info[4 + i]) for i in range(4)]}
+        return d, deps[: 2 * T].view(T, 2), c16[: A.nnz]
 
     def last_split(self):
         """(i0, i1) of the last distributed solve's interior rows (pass 1 beside the

@@ -188,6 +188,27 @@ struct QfreeBufs {
     explicit QfreeBufs(lz_handle *h) : binv{h->scratch + 4 * 256, h->scratch + 5 * 256}, P(h->scratch + 6 * 256) {}
 };
 
+// B^T B's per-block slabs (b = 16 fp64) on the handle's side stream, forked
+// from the main stream; h->ev_join is recorded behind them (the caller waits on
+// it before the slabs are folded).  LZ_GRAM_SIDE=0: on the main stream (A/B).
+static int gram_beside(lz_handle *h, int64_t n, const double *B, int *P)
+{
+    const char *e = getenv("LZ_GRAM_SIDE");
+    if (e && e[0] == '0') {
+        LZ_TRY(gram_partials<double>(h, n, 16, B, B, 16, P));
+        LZ_HIP_TRY(hipEventRecord(h->ev_join, h->stream));
+        return LZ_OK;
+    }
+    LZ_HIP_TRY(hipEventRecord(h->ev_fork, h->stream));
+    LZ_HIP_TRY(hipStreamWaitEvent(h->side, h->ev_fork, 0));
+    std::swap(h->stream, h->side);  // gram_partials launches on h->stream
+    const int rc = gram_partials<double>(h, n, 16, B, B, 16, P);
+    std::swap(h->stream, h->side);
+    LZ_TRY(rc);
+    LZ_HIP_TRY(hipEventRecord(h->ev_join, h->side));
+    return LZ_OK;
+}
+
 // The wavefront form of the same step (lz_wf.hip; default when it applies):
 // one launch runs pass 2 of step j and pass 1 of step j + 1, then the sqrtm of
 // G_{j+1} and the alpha kernel.  Buffers: Y_j in Q0 (every step, in place),
@@ -195,7 +216,7 @@ struct QfreeBufs {
 static int block_lanczos_wf16(lz_handle *h, int64_t n, int64_t nnz, const int64_t *rp, const int32_t *col,
                               const double *val, int m, int64_t lc, const double *B, double *q, double *alpha,
                               double *beta, double *Q0, double *Q1, double *W, const Pass1Plan &pl,
-                              const WfPlan &wp)
+                              const WfPlan &wp, int Pg)
 {
     constexpr int64_t bb = 256;
     (void)nnz;
@@ -203,8 +224,8 @@ static int block_lanczos_wf16(lz_handle *h, int64_t n, int64_t nnz, const int64_
     double *P1 = h->scratch + 6 * 256, *P2 = h->scratch + 7 * 256;
     double *slab = h->scratch + 8 * 256;  // [S1 | S2 | G], 768
     int P = 0;
-    LZ_TRY(gram_partials<double>(h, n, 16, B, B, 16, &P));
-    LZ_TRY(sqrtm_pair<double>(h, 16, nullptr, P, beta, binv[0], nullptr));
+    // B^T B's slabs (Pg of them) were made beside the plan (gram_beside)
+    LZ_TRY(sqrtm_pair<double>(h, 16, nullptr, Pg, beta, binv[0], nullptr));
     LZ_TRY(wf_reset16(h, n, wp));
     // Y_0 = A B, S1_0 = B^T Y_0
     LZ_TRY(wf_step16(h, n, rp, col, pl.col16, val, pl.pairs, wp, nullptr, nullptr, nullptr, nullptr, nullptr,
@@ -254,17 +275,22 @@ static int block_lanczos_fused16(lz_handle *h, int64_t n, int64_t nnz, const int
     QfreeBufs qb(h);
     int P = 0;
     Pass1Plan pl;
+    // B^T B (beta_0's Gram) on the side stream while the once-per-solve plans
+    // (latency-bound passes over the columns, each ending in a host sync) run on
+    // the main one; joined before its sqrtm
+    LZ_TRY(gram_beside(h, n, B, &P));
     {
         WfPlan wp;
         LZ_TRY(wf_plan16(h, n, nnz, rp, col, &wp));  // n < 2^24 only
         if (wp.ok) {
             LZ_TRY(strip_pairs(h, n, rp, &pl.pairs));
             pl.col16 = wp.col16;
-            return block_lanczos_wf16(h, n, nnz, rp, col, val, m, lc, B, q, alpha, beta, Q0, Q1, W, pl, wp);
+            LZ_HIP_TRY(hipStreamWaitEvent(h->stream, h->ev_join, 0));
+            return block_lanczos_wf16(h, n, nnz, rp, col, val, m, lc, B, q, alpha, beta, Q0, Q1, W, pl, wp, P);
         }
     }
     LZ_TRY(pass1_plan(h, n, nnz, rp, col, n, 0, &pl));
-    LZ_TRY(gram_partials<double>(h, n, 16, B, B, 16, &P));
+    LZ_HIP_TRY(hipStreamWaitEvent(h->stream, h->ev_join, 0));
     LZ_TRY(sqrtm_pair<double>(h, 16, nullptr, P, beta, qb.binv[0], nullptr));
     const double *in = B, *prev = nullptr;
     for (int j = 0; j < m; ++j) {
@@ -1444,6 +1470,32 @@ int lz_debug_last_wf(lz_handle *h, int out[2])
     LZ_ARG_CHECK(h && out, "NULL argument");
     out[0] = h->last_wf;
     out[1] = h->last_wf_pre;
+    return LZ_OK;
+}
+
+int lz_debug_wf_plan(lz_handle *h, int64_t n, int64_t nnz, const int64_t *row_ptr, const int32_t *col_idx,
+                     int64_t nx, int64_t xoff, int32_t *deps_out, int16_t *col16_out, int32_t info[8])
+{
+    LZ_HANDLE_CHECK(h);
+    LZ_ARG_CHECK(row_ptr && col_idx && deps_out && col16_out && info, "NULL argument");
+    lz::WfPlan wp;
+    LZ_TRY(lz::wf_plan16(h, n, nnz, row_ptr, col_idx, &wp, nx, xoff));
+    const int64_t T = wp.tr > 0 ? lz::ceil_div(n, (int64_t)wp.tr) : 0;
+    int sp[4] = {0, 0, 0, 0};
+    if (h->wf_cap >= (size_t)T + 64 && T > 0) {
+        LZ_HIP_TRY(hipMemcpyAsync(deps_out, h->wf_deps, sizeof(int32_t) * 2 * (size_t)T, hipMemcpyDeviceToDevice,
+                                  h->stream));
+        LZ_HIP_TRY(hipMemcpyAsync(sp, h->err_flag + 12, sizeof(sp), hipMemcpyDeviceToHost, h->stream));
+    }
+    if (h->c16_cap >= (size_t)nnz * 2 && nnz > 0)
+        LZ_HIP_TRY(hipMemcpyAsync(col16_out, h->c16buf, sizeof(int16_t) * (size_t)nnz, hipMemcpyDeviceToDevice,
+                                  h->stream));
+    LZ_HIP_TRY(hipStreamSynchronize(h->stream));
+    info[0] = wp.ok ? 1 : 0;
+    info[1] = wp.col16 ? 1 : 0;
+    info[2] = (int32_t)T;
+    info[3] = wp.tr;
+    for (int i = 0; i < 4; ++i) info[4 + i] = sp[i];
     return LZ_OK;
 }
 

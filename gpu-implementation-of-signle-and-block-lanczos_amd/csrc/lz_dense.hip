@@ -1133,7 +1133,10 @@ int final_state(lz_handle *h, int64_t n, int b, const T *Y, const T *Vp, const T
     if (n <= 0) return LZ_OK;
     if constexpr (std::is_same<T, double>::value) {
         if (b == 16) {
-            const int grid = (int)std::max<int64_t>(1, std::min<int64_t>(ceil_div(n, 64), (int64_t)h->n_cu * 4));
+            const char *e = getenv("LZ_FS_BPC");  // A/B: blocks per CU (0: one 64-row tile per block)
+            const int bpc = e ? atoi(e) : 4;
+            const int64_t cap = bpc > 0 ? (int64_t)h->n_cu * bpc : ceil_div(n, 64);
+            const int grid = (int)std::max<int64_t>(1, std::min<int64_t>(ceil_div(n, 64), cap));
             hipLaunchKernelGGL(k_final_state16, dim3(grid), dim3(256), 0, h->stream, n, Y, Vp, Vq, Wm, binv, P1, P2,
                                Wout, Q0, Q1);
             LZ_LAUNCH_CHECK();

@@ -237,6 +237,17 @@ int lz_debug_last_split(lz_handle *h, int64_t out[2]);
  * pass 2 first and the halo exchange beside the rest of each step. */
 int lz_debug_last_wf(lz_handle *h, int out[2]);
 
+/* Test hook: the wavefront step's once-per-solve plan of a CSR operator (device
+ * arrays), as lz_block_lanczos would make it for these rows. deps_out (device,
+ * 2 * T int32: each tile's [lo, hi] pass-2 tile range) and col16_out (device,
+ * nnz int16: pass 1's strip-relative columns) receive the plan's arrays; info
+ * (host): [0] plan applies, [1] 16-bit columns valid, [2] T tiles, [3] rows per
+ * tile, [4..7] the span words (max back / forward reach, max width, range
+ * flags). nx, xoff: gather-source rows and the row of local row 0 (n, 0 on one
+ * GPU). The plan kernel is chosen as in a solve (LZ_WF_DEPS4). */
+int lz_debug_wf_plan(lz_handle *h, int64_t n, int64_t nnz, const int64_t *row_ptr, const int32_t *col_idx,
+                     int64_t nx, int64_t xoff, int32_t *deps_out, int16_t *col16_out, int32_t info[8]);
+
 /* Distributed block Lanczos, all-gather form (the north star's exchange).
  * Every rank's slab is padded to n_pad rows (n_pad >= max rows per rank) and
  * ncclAllGather places rank g's slab at rows [g*n_pad, (g+1)*n_pad) of X_full,
