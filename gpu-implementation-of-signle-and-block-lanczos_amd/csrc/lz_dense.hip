@@ -625,7 +625,7 @@ __global__ __launch_bounds__(kRedThreads) void k_sqrtm_b(const T *__restrict__ G
                                                          const double *__restrict__ part, int P,
                                                          T *__restrict__ beta, T *__restrict__ binv,
                                                          T *__restrict__ eig, const T *__restrict__ L,
-                                                         T *__restrict__ LB, WfAlpha wa)
+                                                         T *__restrict__ LB, WfAlpha wa, int ns)
 {
 #pragma clang fp contract(off)
     static_assert(B == 8 || B == 16 || B == 32, "B in {8, 16, 32}");
@@ -657,6 +657,21 @@ __global__ __launch_bounds__(kRedThreads) void k_sqrtm_b(const T *__restrict__ G
     const int jq = B - 1 - j;                      // partner position of j
     const int jn = j == 0 ? 0 : (j == 1 ? B - 1 : j - 1);  // moved position of j
     double *Am = Abuf[0], *An = Abuf[1], *Um = Ubuf[0], *Un = Ubuf[1];
+    bool done = false;
+    if constexpr (B == 16) {
+        // Newton-Schulz on the MFMA when no eigenvalues are asked for and G is
+        // well enough conditioned (sqrtm_ns16); the Jacobi route otherwise
+        if (ns && eig == nullptr) {
+            double ya[4], yb[4], za[4], zb[4], sc = 0.0;
+            if (sqrtm_ns16(g, Abuf[0], Abuf[1], Ubuf[0], ya, yb, za, zb, sc, tid)) {
+                sqrtm_ns16_tail<T>(ya, yb, za, zb, sc, g, beta, binv, L, LB, wfa ? wbi : nullptr,
+                                   wfa ? wp1 : nullptr, tid);
+                done = true;
+            }
+            wave_lds_sync();  // the scratch (Abuf, Ubuf) is the Jacobi route's matrices
+        }
+    }
+    if (!done) {
     sqrtm_init<B>(g, Am, Um, tid);  // symmetrised from the lower triangle, U = I
 #ifdef LZ_SQRTM_PROBE
     const long long t0 = clock64();
@@ -740,6 +755,16 @@ __global__ __launch_bounds__(kRedThreads) void k_sqrtm_b(const T *__restrict__ G
     }
 #endif
     sqrtm_tail<T, B>(Am, Um, cc, ss, g, beta, binv, L, LB, wfa ? wbi : nullptr, wfa ? wp1 : nullptr, tid);
+    if (eig && tid < B) {
+        const double lk = Am[tid * LD + tid];
+        int rank = 0;
+        for (int k = 0; k < B; ++k) {
+            const double lm = Am[k * LD + k];
+            rank += (lm < lk) || (lm == lk && k < tid);
+        }
+        eig[rank] = (T)lk;
+    }
+    }  // !done
     if constexpr (B == 16) {
         if (wfa) {  // k_alpha_wf16's products, same order (one wave)
             wave_lds_sync();
@@ -794,15 +819,6 @@ __global__ __launch_bounds__(kRedThreads) void k_sqrtm_b(const T *__restrict__ G
             }
         }
     }
-    if (eig && tid < B) {
-        const double lk = Am[tid * LD + tid];
-        int rank = 0;
-        for (int k = 0; k < B; ++k) {
-            const double lm = Am[k * LD + k];
-            rank += (lm < lk) || (lm == lk && k < tid);
-        }
-        eig[rank] = (T)lk;
-    }
 }
 
 template <typename T>
@@ -814,10 +830,12 @@ int sqrtm_pair(lz_handle *h, int b, const T *G, int nparts, T *beta, T *beta_inv
     {
     const int ev_ = prof_begin(h, PROF_SMALL);
     const double *sl = slabs ? slabs : h->partials;
+    const char *nse = getenv("LZ_SQRTM_NS");  // "0": the Jacobi route at b = 16 as well (A/B, tests)
+    const int ns = (nse && nse[0] == '0') ? 0 : 1;
 #define LZ_SQRTM_B(BV)                                                                        \
     case BV:                                                                                  \
         hipLaunchKernelGGL((k_sqrtm_b<T, BV>), dim3(1), dim3(kRedThreads), 0, h->stream, G, sl, \
-                           nparts, beta, beta_inv, eig, L, LB, wa ? *wa : WfAlpha{});          \
+                           nparts, beta, beta_inv, eig, L, LB, wa ? *wa : WfAlpha{}, ns);      \
         break;
     switch (b) {
         LZ_SQRTM_B(8) LZ_SQRTM_B(16) LZ_SQRTM_B(32)

@@ -535,14 +535,16 @@ __global__ __launch_bounds__(256) void k_spmm_seg(int64_t n, const int64_t *__re
         return;
     } else {
     // diag > 0 (LZ_SPMM_DIAG, a measurement of the tile structure, results
-    // wrong): block b runs tile (its tile mod diag), so the row pointers, CSR
-    // runs, X window and Y rows of all blocks are those of `diag` tiles -- L2-
-    // resident -- with the same per-tile instruction mix
+    // wrong): block b runs tile mid + (its tile mod diag), so the row pointers,
+    // CSR runs, X window and Y rows of all blocks are those of `diag` tiles --
+    // L2-resident -- from the middle of the operator (rows with the full band,
+    // so the same entries per row and per-tile instruction mix as the real run)
     // (diag bit 30: the Y rows stored stay the block's own, so only the reads
     // are L2-resident)
     const int64_t tdx = xcd_remap(blockIdx.x, gridDim.x);
     const int dmod = diag & 0x3fffffff;
-    const int64_t r0 = (dmod > 0 ? tdx % dmod : tdx) * TR;
+    const int64_t dmid = dmod > 0 ? ((int64_t)gridDim.x / 2 / dmod) * dmod : 0;
+    const int64_t r0 = (dmod > 0 ? tdx % dmod + dmid : tdx) * TR;
     const int64_t ry = (diag & (1 << 30)) ? tdx * TR : r0;  // the Y tile's first row
     const int nrows = (int)((n - r0) < TR ? (n - r0) : TR);
     const int64_t kA = rp[r0];

@@ -215,4 +215,129 @@ __device__ void sqrtm_tail(const double *Am, const double *Um, double *cc, doubl
     }
 }
 
+// Coupled Newton-Schulz square root for B = 16 on the f64 MFMA (one wave):
+// A = G / |G|_F (G symmetrised from its lower triangle, as sqrtm_init),
+// Y_0 = A, Z_0 = I, T = (3 I - Z_k Y_k) / 2, Y_{k+1} = Y_k T, Z_{k+1} = T Z_k,
+// so Y -> A^{1/2} and Z -> A^{-1/2} (quadratically once the smallest
+// eigenvalue of Z Y is near 1; about log(kappa(G)) / log(2.25) + 5
+// iterations).  The same beta = G^{1/2}, beta^-1 = G^{-1/2} as the Jacobi
+// route for a well-conditioned SPD G, in ~20 dependent 16 x 16 products
+// instead of ~7 sweeps of 15 rotation rounds.  Returns false -- the caller
+// then runs the Jacobi route, whose small eigenvalues keep high relative
+// accuracy -- unless |Z Y - I|_max fell to the rounding floor within kNsMax
+// iterations (kappa(G) up to ~1e6: beta within ~4e-14 and beta^-1 within
+// ~3e-12 of the Jacobi route's, scripts/probe/sqrtm_probe.hip), so an
+// ill-conditioned or nearly rank-deficient G (Krylov breakdown) takes the
+// reference's eigendecomposition path.
+// Lane l = (c = l & 15, q = l >> 4) keeps rows/columns in the MFMA operand
+// layouts: xa[k] = X[c][4q + k] (A operand, permuted contraction order),
+// xb[k] = X[4q + k][c] (B operand); a product comes back as D[q + 4 r][c].
+// S0, S1, S2: 16 x 17 LDS doubles of scratch each.  On success ya / yb / za /
+// zb hold the converged Y and Z, and scale = |G|_F.
+constexpr int kNsMax = 22;
+__device__ __forceinline__ bool sqrtm_ns16(const double *g, double *S0, double *S1, double *S2, double ya[4],
+                                           double yb[4], double za[4], double zb[4], double &scale, int tid)
+{
+    constexpr int LD = 17;
+    const int c = tid & 15, q = tid >> 4;
+    double f = 0.0;
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+        const int j = 4 * q + k;
+        const double a = c < j ? g[j * 16 + c] : g[c * 16 + j];  // symmetric: A[c][j] = A[j][c]
+        ya[k] = a;
+        f = fma(a, a, f);
+    }
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) f += __shfl_xor(f, o, 64);
+    if (!(f > 0.0) || !(f < 1e300)) return false;
+    scale = sqrt(f);
+    const double is = 1.0 / scale;
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+        ya[k] *= is;
+        yb[k] = ya[k];
+        za[k] = zb[k] = (c == 4 * q + k) ? 1.0 : 0.0;
+    }
+    double prev = 1e300;
+    for (int it = 0; it < kNsMax; ++it) {
+        d4_t m = {0.0, 0.0, 0.0, 0.0};
+#pragma unroll
+        for (int k = 0; k < 4; ++k) m = mfma16(za[k], yb[k], m);  // M = Z Y
+        double e = 0.0;
+#pragma unroll
+        for (int r = 0; r < 4; ++r) e = fmax(e, fabs(m[r] - ((q + 4 * r == c) ? 1.0 : 0.0)));
+#pragma unroll
+        for (int o = 32; o > 0; o >>= 1) e = fmax(e, __shfl_xor(e, o, 64));
+        if (!(e < 1e3)) return false;              // diverging, or NaN
+        if (e <= 1.5e-14 || (e < 1e-10 && e >= 0.5 * prev)) return true;  // at the rounding floor
+        prev = e;
+#pragma unroll
+        for (int r = 0; r < 4; ++r) S0[(q + 4 * r) * LD + c] = ((q + 4 * r == c) ? 1.5 : 0.0) - 0.5 * m[r];
+        wave_lds_sync();
+        double ta[4], tb[4];
+#pragma unroll
+        for (int k = 0; k < 4; ++k) {
+            ta[k] = S0[c * LD + 4 * q + k];
+            tb[k] = S0[(4 * q + k) * LD + c];
+        }
+        d4_t y = {0.0, 0.0, 0.0, 0.0}, z = {0.0, 0.0, 0.0, 0.0};
+#pragma unroll
+        for (int k = 0; k < 4; ++k) {
+            y = mfma16(ya[k], tb[k], y);  // Y T
+            z = mfma16(ta[k], zb[k], z);  // T Z
+        }
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+            S1[(q + 4 * r) * LD + c] = y[r];
+            S2[(q + 4 * r) * LD + c] = z[r];
+        }
+        wave_lds_sync();
+#pragma unroll
+        for (int k = 0; k < 4; ++k) {
+            ya[k] = S1[c * LD + 4 * q + k];
+            yb[k] = S1[(4 * q + k) * LD + c];
+            za[k] = S2[c * LD + 4 * q + k];
+            zb[k] = S2[(4 * q + k) * LD + c];
+        }
+        wave_lds_sync();  // S0..S2 rewritten next iteration
+    }
+    return false;
+}
+
+// beta = |G|_F^{1/2} Y and beta^-1 = Z / |G|_F^{1/2} (symmetrised) from
+// sqrtm_ns16, stored as sqrtm_tail stores the Jacobi route's: beta / binv
+// (global, T), g <- beta when L (LB = L beta), wbi / wp1 (LDS, optional).
+template <typename T>
+__device__ void sqrtm_ns16_tail(const double ya[4], const double yb[4], const double za[4], const double zb[4],
+                                double scale, double *g, T *beta, T *binv, const T *L, T *LB, double *wbi,
+                                double *wp1, int tid)
+{
+    const int c = tid & 15, q = tid >> 4;
+    const double rs = sqrt(scale), irs = 1.0 / rs;
+    wave_lds_sync();  // every lane's reads of g (the Gram) are done
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+        const int e = c * 16 + 4 * q + k;
+        const double b = (0.5 * (ya[k] + yb[k])) * rs, bi = (0.5 * (za[k] + zb[k])) * irs;
+        if (beta) beta[e] = (T)b;
+        if (binv) binv[e] = (T)bi;
+        if (L) g[e] = b;
+        if (wbi) wbi[e] = (double)(T)bi;
+    }
+    if (L) {
+        wave_lds_sync();
+        const int j = tid % 16, r0 = tid / 16;
+#pragma unroll 1
+        for (int k = 0; k < 4; ++k) {
+            const int i = r0 + 4 * k;
+            double s = 0.0;
+#pragma unroll 4
+            for (int kk = 0; kk < 16; ++kk) s = fma((double)L[i * 16 + kk], g[kk * 16 + j], s);
+            LB[i * 16 + j] = (T)s;
+            if (wp1) wp1[i * 16 + j] = (double)(T)s;
+        }
+    }
+}
+
 }  // namespace lz

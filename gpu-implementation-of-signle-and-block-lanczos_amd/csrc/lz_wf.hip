@@ -143,111 +143,6 @@ __global__ __launch_bounds__(256) void k_wf_deps(int64_t n, int TR, const int64_
     }
 }
 
-// The same plan with one wave per tile and four columns per lane per 16-B load
-// (a 16-B-aligned column array): a tile's loads issue in groups of four before
-// any is used, and no block-wide barrier sits between tiles.  An entry's strip
-// comes from the tile's strip boundaries (rp at every 16th row, read into
-// scalar registers once per tile).  Same outputs as k_wf_deps.
-__global__ __launch_bounds__(256) void k_wf_deps4(int64_t n, int TR, const int64_t *__restrict__ rp,
-                                                  const int32_t *__restrict__ col, int2 *__restrict__ deps,
-                                                  int16_t *__restrict__ col16, int *__restrict__ spans, int64_t xoff,
-                                                  int win)
-{
-    const int64_t T = ceil_div(n, (int64_t)TR);
-    const int lane = threadIdx.x & 63;
-    const int64_t nw = (int64_t)gridDim.x * 4;
-    const int ns = TR / 16;  // strips per tile (<= 12)
-    const int64_t nnz = rp[n];  // the column array's end
-    int sb = 0, sf = 0, sw = 0, bad = 0, far = 0;
-    for (int64_t t = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6); t < T; t += nw) {
-        const int64_t r0 = t * TR;
-        const int64_t rr = r0 + 16 * (int64_t)(lane < ns ? lane : ns);
-        const int64_t kb_l = rp[rr < n ? rr : n];  // lane i <= ns: the start of strip i (lane ns: the tile's end)
-        const int64_t k0 = __shfl(kb_l, 0, 64), k1 = __shfl(kb_l, ns, 64);
-        const int rel_l = (int)(kb_l - k0);
-        int bo[13];
-#pragma unroll
-        for (int i = 0; i < 13; ++i) bo[i] = __builtin_amdgcn_readlane(rel_l, i < 12 ? i : 12);
-        int mn = INT_MAX, mx = -1;
-        const int64_t kA = k0 & ~(int64_t)3;
-        for (int64_t kb = kA + 4 * lane; kb < k1; kb += 1024) {
-            int4 cv[4];
-#pragma unroll
-            for (int u = 0; u < 4; ++u) {
-                const int64_t k = kb + 256 * u;
-                if (k + 4 <= nnz) cv[u] = *reinterpret_cast<const int4 *>(col + k);
-                else {  // the array's last group: no read past its end
-                    cv[u] = make_int4(0, 0, 0, 0);
-                    if (k < nnz) cv[u].x = col[k];
-                    if (k + 1 < nnz) cv[u].y = col[k + 1];
-                    if (k + 2 < nnz) cv[u].z = col[k + 2];
-                }
-            }
-#pragma unroll
-            for (int u = 0; u < 4; ++u) {
-                const int64_t kq = kb + 256 * u;
-                if (kq >= k1) break;
-                const int cc[4] = {cv[u].x, cv[u].y, cv[u].z, cv[u].w};
-                short dd[4];
-                bool all = kq >= k0 && kq + 4 <= k1;
-#pragma unroll
-                for (int e = 0; e < 4; ++e) {
-                    const int64_t k = kq + e;
-                    const bool in = k >= k0 && k < k1;
-                    const int rel = (int)(k - k0);
-                    int st = 0;
-#pragma unroll
-                    for (int i = 1; i < 12; ++i) st += (i < ns && rel >= bo[i]) ? 1 : 0;
-                    const int64_t s0 = r0 + 16 * st;
-                    const int64_t c = (int64_t)cc[e] - xoff;
-                    if (in && c >= 0 && c < n) {
-                        mn = c < mn ? (int)c : mn;
-                        mx = c > mx ? (int)c : mx;
-                    }
-                    const int64_t d = c - s0;
-                    if (in && win) far |= (d < -(kWinRows / 2) + 32) | (d > kWinRows / 2 - 32);
-                    if (in && col16) bad |= (d < -32768) | (d > 32767);
-                    dd[e] = (short)d;
-                }
-                if (col16) {
-                    if (all) {
-                        short4 v = make_short4(dd[0], dd[1], dd[2], dd[3]);
-                        *reinterpret_cast<short4 *>(col16 + kq) = v;
-                    } else {
-#pragma unroll
-                        for (int e = 0; e < 4; ++e)
-                            if (kq + e >= k0 && kq + e < k1) col16[kq + e] = dd[e];
-                    }
-                }
-            }
-        }
-#pragma unroll
-        for (int o = 32; o > 0; o >>= 1) {
-            const int a = __shfl_xor(mn, o, 64), b = __shfl_xor(mx, o, 64);
-            mn = a < mn ? a : mn;
-            mx = b > mx ? b : mx;
-        }
-        int lo = (int)t, hi = (int)t;
-        if (mx >= 0) {
-            const int a = (int)(mn / TR), b = (int)(mx / TR);
-            lo = a < lo ? a : lo;
-            hi = b > hi ? b : hi;
-        }
-        if (lane == 0) deps[t] = make_int2(lo, hi);
-        sb = (int)t - lo > sb ? (int)t - lo : sb;
-        sf = hi - (int)t > sf ? hi - (int)t : sf;
-        sw = hi - lo + 1 > sw ? hi - lo + 1 : sw;
-    }
-    const bool bb = __ballot(bad) != 0, bf = __ballot(far) != 0;
-    if (lane == 0) {
-        if (bb) atomicOr(&spans[3], 1);
-        if (bf) atomicOr(&spans[3], 2);
-        atomicMax(&spans[0], sb);
-        atomicMax(&spans[1], sf);
-        atomicMax(&spans[2], sw);
-    }
-}
-
 typedef unsigned v4u32_t __attribute__((ext_vector_type(4)));
 typedef double d2_t __attribute__((ext_vector_type(2)));
 
@@ -848,17 +743,12 @@ int wf_plan16(lz_handle *h, int64_t n, int64_t nnz, const int64_t *rp, const int
     }
     int *spans = h->err_flag + 12;  // err_flag[0]: device error word; [8], [9]: other plans
     LZ_HIP_TRY(hipMemsetAsync(spans, 0, 4 * sizeof(int), h->stream));
-    // (one tile per block measured slower: its per-block atomics contend)
-    const char *d4 = getenv("LZ_WF_DEPS4");  // A/B: "0" the block-per-tile plan kernel
-    if (!(d4 && d4[0] == '0') && ((uintptr_t)col & 15) == 0) {
-        const int grid = (int)std::max<int64_t>(1, std::min<int64_t>(ceil_div(T, 4), (int64_t)h->n_cu * 8));
-        hipLaunchKernelGGL(k_wf_deps4, dim3(grid), dim3(256), 0, h->stream, n, pl->tr, rp, col,
-                           static_cast<int2 *>(h->wf_deps), c16, spans, xoff, nx >= kWinRows ? 1 : 0);
-    } else {
-        const int grid = (int)std::max<int64_t>(1, std::min<int64_t>(T, (int64_t)h->n_cu * 8));
-        hipLaunchKernelGGL(k_wf_deps, dim3(grid), dim3(256), 0, h->stream, n, pl->tr, rp, col,
-                           static_cast<int2 *>(h->wf_deps), c16, spans, xoff, nx >= kWinRows ? 1 : 0);
-    }
+    // (one tile per block measured slower: its per-block atomics contend; one
+    // wave per tile with 16-B column loads, 525 against 295 us at C3: the
+    // per-entry strip search costs more VALU than the loads save)
+    const int grid = (int)std::max<int64_t>(1, std::min<int64_t>(T, (int64_t)h->n_cu * 8));
+    hipLaunchKernelGGL(k_wf_deps, dim3(grid), dim3(256), 0, h->stream, n, pl->tr, rp, col,
+                       static_cast<int2 *>(h->wf_deps), c16, spans, xoff, nx >= kWinRows ? 1 : 0);
     LZ_LAUNCH_CHECK();
     int sp[4] = {0, 0, 0, 1};
     LZ_HIP_TRY(hipMemcpyAsync(sp, spans, sizeof(sp), hipMemcpyDeviceToHost, h->stream));

@@ -3,7 +3,8 @@
 #   bash scripts/pmc_cmd.sh TAG KERNEL_SUBSTRING script.py args...
 # (set LZ_* env vars before calling)
 R=$GRAFT_REPO_ROOT
-TAG=$1; K=$2; shift 2
+TAG=$1; K=$2; S=$3; shift 3
+case "$S" in /*) ;; *) S=$R/$S ;; esac  # (the passes run from /tmp)
 O=$R/gpurun_out/pmc_$TAG
 mkdir -p $O
 cd /tmp
@@ -11,7 +12,7 @@ i=0
 while read -r grp; do
   [ -z "$grp" ] && continue
   i=$((i+1))
-  timeout -k 10 150 rocprofv3 --pmc $grp --output-format csv -d $O/p$i -o p -- python3 "$@" > $O/p$i.log 2>&1 || { echo "pass $i ($grp) failed rc=$?"; exit 1; }
+  timeout -k 10 150 rocprofv3 --pmc $grp --output-format csv -d $O/p$i -o p -- python3 "$S" "$@" > $O/p$i.log 2>&1 || { echo "pass $i ($grp) failed rc=$?"; exit 1; }
 done <<'GROUPS'
 SQ_INSTS_VMEM_RD SQ_INSTS_VMEM_WR SQ_INSTS_VALU SQ_INSTS_LDS SQ_WAVES GRBM_GUI_ACTIVE SQ_BUSY_CYCLES SQ_WAVE_CYCLES
 TA_TA_BUSY_sum TA_ADDR_STALLED_BY_TD_CYCLES_sum

@@ -1,6 +1,5 @@
-"""The wavefront step's once-per-solve plan (lz_wf.hip wf_plan16: k_wf_deps4,
-and k_wf_deps for column arrays that are not 16-byte aligned) against a numpy
-restatement of what it must hold: per pass-1 tile t of TR rows the range
+"""The wavefront step's once-per-solve plan (lz_wf.hip wf_plan16, k_wf_deps)
+against a numpy restatement of what it must hold: per pass-1 tile t of TR rows the range
 [lo, hi] of tiles its own-row columns fall in (t included), the span maxima,
 and pass 1's 16-bit columns (column - the start row of the entry's 16-row
 strip).  Integer work: bit-exact.
@@ -32,7 +31,7 @@ def plan_ref(A, tr, xoff=0):
 
 def check(lz, handle, torch, A, xoff=0, nx=None, misalign=False):
     Ad = lz.CsrDevice.from_host(A)
-    if misalign:  # a column array at an odd 4-byte offset: the block-per-tile kernel
+    if misalign:  # a column array at an odd 4-byte offset
         buf = torch.zeros(A.nnz + 1, dtype=torch.int32, device="cuda")
         buf[1:] = Ad.col
         Ad = lz.CsrDevice(Ad.n, Ad.n_cols, Ad.row_ptr, buf[1:], Ad.val)
@@ -52,9 +51,7 @@ def check(lz, handle, torch, A, xoff=0, nx=None, misalign=False):
 
 @pytest.mark.parametrize("n,per_row,hw", [(200_003, 10.0, 4096), (100_000, 25.0, 20_000),
                                           (176 * 50, 10.0, 100), (40_017, 6.0, 60_000)])
-@pytest.mark.parametrize("deps4", ["1", "0"])
-def test_wf_plan_vs_numpy(lz, handle, torch_cuda, monkeypatch, n, per_row, hw, deps4):
-    monkeypatch.setenv("LZ_WF_DEPS4", deps4)
+def test_wf_plan_vs_numpy(lz, handle, torch_cuda, n, per_row, hw):
     A = lz.gen_banded(n, per_row, hw, seed=n + 7)
     info = check(lz, handle, torch_cuda, A)
     assert info["ok"] == (info["spans"][2] <= 1024)
@@ -65,26 +62,10 @@ def test_wf_plan_misaligned_columns(lz, handle, torch_cuda):
     check(lz, handle, torch_cuda, A, misalign=True)
 
 
-@pytest.mark.parametrize("deps4", ["1", "0"])
-def test_wf_plan_rank_rows(lz, handle, torch_cuda, monkeypatch, deps4):
+def test_wf_plan_rank_rows(lz, handle, torch_cuda):
     """A rank's rows [xoff, xoff + n) of a larger gather source: columns outside
     them (peers' rows) are left out of the ranges, the 16-bit columns keep
     their strip offsets."""
-    monkeypatch.setenv("LZ_WF_DEPS4", deps4)
     n_all, r0, r1 = 300_000, 100_000, 200_000
     A = lz.gen_banded_local(n_all, r0, r1, 10.0, 3000, 5)
     check(lz, handle, torch_cuda, A, xoff=r0, nx=n_all)
-
-
-def test_wf_plan_kernels_bitwise_solve(lz, handle, torch_cuda, monkeypatch):
-    """The two plan kernels give the same solve, bit for bit."""
-    A = lz.gen_banded(150_001, 10.0, 4096, seed=11)
-    B = lz.uniform_B(A.n, 16, seed=2)
-    Ad = lz.CsrDevice.from_host(A)
-    outs = []
-    for v in ("1", "0"):
-        monkeypatch.setenv("LZ_WF_DEPS4", v)
-        q, al, be = lz.run_block_lanczos(handle, Ad, torch_cuda.from_numpy(B).cuda(), 6, 84)
-        torch_cuda.cuda.synchronize()
-        outs.append(al.cpu().numpy())
-    assert np.array_equal(outs[0], outs[1])
