@@ -743,9 +743,7 @@ int wf_plan16(lz_handle *h, int64_t n, int64_t nnz, const int64_t *rp, const int
     }
     int *spans = h->err_flag + 12;  // err_flag[0]: device error word; [8], [9]: other plans
     LZ_HIP_TRY(hipMemsetAsync(spans, 0, 4 * sizeof(int), h->stream));
-    // (one tile per block measured slower: its per-block atomics contend; one
-    // wave per tile with 16-B column loads, 525 against 295 us at C3: the
-    // per-entry strip search costs more VALU than the loads save)
+    // (one tile per block measured slower: its per-block atomics contend)
     const int grid = (int)std::max<int64_t>(1, std::min<int64_t>(T, (int64_t)h->n_cu * 8));
     hipLaunchKernelGGL(k_wf_deps, dim3(grid), dim3(256), 0, h->stream, n, pl->tr, rp, col,
                        static_cast<int2 *>(h->wf_deps), c16, spans, xoff, nx >= kWinRows ? 1 : 0);
