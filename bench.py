@@ -128,7 +128,7 @@ def spmm_kernel(nnz, n):
 
 # the source file of each profiled kernel: a committed counter file is used only
 # while that file is byte-identical to the one profiled (profiles record its sha256)
-KERNEL_SRC = {"k_wf16": "lz_wf.hip", "k_vl_spmv_win": "lz_fused.hip", "k_vl_wf": "lz_fused.hip", "k_fused_pp16": "lz_fused.hip", "k_fused_update16": "lz_fused.hip", "k_spmm_seg": "lz_spmm.hip",
+KERNEL_SRC = {"k_wf16": "lz_wf.hip", "k_vl_spmv_win": "lz_fused.hip", "k_fused_pp16": "lz_fused.hip", "k_fused_update16": "lz_fused.hip", "k_spmm_seg": "lz_spmm.hip",
               "k_fused_el32": "lz_fused32.hip", "k_fused_ub32": "lz_fused32.hip", "k_gram16_f64": "lz_dense.hip",
               "k_gram32_f32": "lz_dense.hip"}
 CSRC = os.path.join(ROOT, "gpu-implementation-of-signle-and-block-lanczos_amd", "csrc")
@@ -529,19 +529,11 @@ def main():
         h.vector_lanczos(A2d, b2, k2, 84, q2, al2, be2, v0, v1, v2)
         torch.cuda.synchronize()
         dt2 = time.perf_counter() - t0c
-        # the step form lz_vector_lanczos takes here (lz_fused.hip): one launch per step
-        # (k_vl_wf) unless LZ_VL_WF=0 (C2's band fits the <512, 9216> window)
-        vl_wf = os.environ.get("LZ_VL_WF", "1") != "0"
-        a2b = A2.nnz * 12 + (n2 + 1) * 8
         c2 = {"workload": f"C2 single-vector Lanczos fp64, banded-random n={n2} nnz={A2.nnz}",
               "iters_per_s": round(k2 / dt2, 1), "us_per_iter": round(dt2 / k2 * 1e6, 2),
-              "step_form": "one launch per step (k_vl_wf)" if vl_wf else "SpMV pass + update pass",
-              "iteration_GBs": round((a2b + (5 if vl_wf else 7) * n2 * 8) / (dt2 / k2) / 1e9, 1),
-              "note": ("A + 5 n s bytes per step: Y_{j-1}, v_{j-1}, v_{j-2} read, v_j and Y_j written "
-                       "(v_j formed in each block's band window, gathered from LDS); m launches and one final "
-                       "pass (3 n s read, 3 n s written) per solve") if vl_wf else
-                      ("A + 7 n s bytes per step: SpMV pass A + 4 n s (w_j gathered, q_{j-1} read, q_j and w' "
-                       "written), update pass 3 n s (w', q_j read, w' written)")}
+              "iteration_GBs": round((A2.nnz * 12 + (n2 + 1) * 8 + 7 * n2 * 8) / (dt2 / k2) / 1e9, 1),
+              "note": "A + 7 n s bytes per step: SpMV pass A + 4 n s (w_j gathered, q_{j-1} read, q_j and w' "
+                      "written), update pass 3 n s (w', q_j read, w' written)"}
         # the dominant kernel (the SpMV pass) against the HBM roofline: HIP events of a separate
         # solve with the two vector classes recorded
         k2p = min(k2, 50)
@@ -552,27 +544,21 @@ def main():
         up_ms, up_cnt = h.prof_read(h.PROF_UPDATE_PASS)
         h.prof_enable(False)
         if sv_cnt and up_cnt:
+            spmv_b = A2.nnz * 12 + (n2 + 1) * 8 + 4 * n2 * 8
             t_sv, t_up = sv_ms / sv_cnt * 1e-3, up_ms / up_cnt * 1e-3
-            if vl_wf:  # launch 0: A + 2ns, launch 1: A + 4ns, then A + 5ns; the final pass 6ns
-                spmv_b = a2b + (2 + 4 + 5 * (sv_cnt - 2)) * n2 * 8 // sv_cnt if sv_cnt >= 2 else a2b + 2 * n2 * 8
-                kn2, ks2 = "k_vl_wf<8,512,9216>", "k_vl_wf"
-                upd = {"kernel": "k_vl_wf_final", "bytes_per_launch": 6 * n2 * 8}
-            else:
-                spmv_b = a2b + 4 * n2 * 8
-                kn2, ks2 = "k_vl_spmv_win<double,8,512,9216>", "k_vl_spmv_win"
-                upd = {"kernel": "k_vl_update<double>", "bytes_per_launch": 3 * n2 * 8}
-            tr2, src2 = pmc_traffic(ks2, n2, A2.nnz, 4096, kn2)
-            upd.update({"avg_ms": round(t_up * 1e3, 5),
-                        "frac": round(upd["bytes_per_launch"] / t_up / 1e9 / HBM_PEAK_GBS, 4)})
+            kn2 = "k_vl_spmv_win<double,8,512,9216>"
+            tr2, src2 = pmc_traffic("k_vl_spmv_win", n2, A2.nnz, 4096, kn2)
             c2["roofline"] = {"bound": "hbm", "kernel": kn2, "bytes_per_launch": spmv_b,
                               "avg_ms": round(t_sv * 1e3, 5), "achieved": round(spmv_b / t_sv / 1e9, 1),
                               "peak": HBM_PEAK_GBS, "unit": "GB/s",
                               "frac": round(spmv_b / t_sv / 1e9 / HBM_PEAK_GBS, 4),
                               "traffic": tr2, "traffic_source": src2,
-                              ("final_pass" if vl_wf else "update_pass"): upd,
-                              "note": f"HIP events around each launch of a separate {k2p}-step solve; a launch "
-                                      f"moves {spmv_b / 1e6:.0f} MB in ~{t_sv * 1e6:.0f} us, so launch ramp-up "
-                                      "and tail are a visible share of it"}
+                              "update_pass": {"kernel": "k_vl_update<double>", "bytes_per_launch": 3 * n2 * 8,
+                                              "avg_ms": round(t_up * 1e3, 5),
+                                              "frac": round(3 * n2 * 8 / t_up / 1e9 / HBM_PEAK_GBS, 4)},
+                              "note": "HIP events around each launch of a separate solve; a launch moves "
+                                      f"{spmv_b / 1e6:.0f} MB in ~{t_sv * 1e6:.0f} us, so launch ramp-up and "
+                                      "tail are a visible share of it"}
         if not args.no_cpu_baseline:
             orc = ge.load_oracle()
             m2 = min(k2, 12)

@@ -1432,234 +1432,6 @@ __global__ __launch_bounds__(NT) void k_vl_spmv_win(
     block_store_slab(dot, red, part_out);
 }
 
-// ------------------------------------------ single-vector wavefront step
-// One launch per step (fp64, band window) on the unnormalised residuals
-// v_j = w_j = beta_j q_j and Y_j = A v_j -- the block form's reassociation
-// (lz_wf.hip) at b = 1:
-//   beta_{j-1} = sqrt(G_{j-1}),  alpha_{j-1} = S1_{j-1} / beta_{j-1}^2 - S2_{j-1} / beta_{j-2}
-//   v_j = Y_{j-1} / beta_{j-1} - (beta_{j-1} / beta_{j-2}) v_{j-2} - (alpha_{j-1} / beta_{j-1}) v_{j-1}
-//   Y_j = A v_j;  slabs S1_j = v_j.Y_j, S2_j = v_{j-1}.v_j, G_j = v_j.v_j
-// (the reference's w' = A q_j - beta_j q_{j-1}, alpha_j = w'.q_j, w_{j+1} =
-// w' - alpha_j q_j, beta_{j+1} = |w_{j+1}|: vector_lanczos.hpp:8-67).  v_j is
-// never read back before its gathers: every block forms the band window's v_j
-// values itself from the three inputs as it fills its LDS ring (the same
-// arithmetic in every block, so the same bits), and stores only its own rows.
-// So the separate update pass (k_vl_update) and its launch go, and a step moves
-// A + 5 n s (Y_{j-1}, v_{j-1}, v_{j-2} read once; v_j, Y_j written) against
-// A + 7 n s for the two passes.  The scalars are finished redundantly by every
-// block from the previous launch's slabs; block 0 writes alpha / beta / q of
-// step j - 1.
-struct VlWf {
-    const double *Yin, *Vm, *Vmm;  // Y_{j-1}, v_{j-1}, v_{j-2} (Vmm null: j < 2; Yin null: j == 0, v_0 = Vm = b)
-    double *Vout, *Yout;           // v_j (own rows; null at j == 0), Y_j
-    const double *part_in;         // 3 x P slabs of step j - 1 (S1 | S2 | G)
-    int P;
-    double *part_out;              // 3 x gridDim slabs of step j
-    double *alpha, *beta, *q;      // step j - 1's (block 0)
-    int64_t lc;
-    int j;
-};
-
-// the step's coefficients from the previous launch's slabs (every block, same
-// fixed order: the same bits): sums of P partials of S1, S2, G
-__device__ __forceinline__ void vl_wf_scalars(const VlWf &a, double *red, double &cY, double &cM, double &cMM,
-                                              double &al, double &be)
-{
-    const int t = threadIdx.x, nt = blockDim.x, lane = t & 63, w = t >> 6;
-    double s[3] = {0.0, 0.0, 0.0};
-    for (int i = t; i < a.P; i += nt)
-#pragma unroll
-        for (int k = 0; k < 3; ++k) s[k] += a.part_in[(int64_t)k * a.P + i];
-#pragma unroll
-    for (int k = 0; k < 3; ++k)
-#pragma unroll
-        for (int o = 32; o > 0; o >>= 1) s[k] += __shfl_xor(s[k], o, 64);
-    if (lane == 0)
-#pragma unroll
-        for (int k = 0; k < 3; ++k) red[3 * w + k] = s[k];
-    __syncthreads();
-    double S1 = 0.0, S2 = 0.0, G = 0.0;
-    for (int i = 0; i < nt / 64; ++i) {
-        S1 += red[3 * i];
-        S2 += red[3 * i + 1];
-        G += red[3 * i + 2];
-    }
-    __syncthreads();
-    be = sqrt(G);
-    const double bp = a.Vmm ? (double)a.beta[a.j - 2] : 0.0;  // beta_{j-2}
-    al = S1 / (be * be) - (a.Vmm ? S2 / bp : 0.0);
-    cY = 1.0 / be;
-    cM = al / be;
-    cMM = a.Vmm ? be / bp : 0.0;
-}
-
-template <int LV, int NT, int RING>
-__global__ __launch_bounds__(NT) void k_vl_wf(int64_t n, const int64_t *__restrict__ rp,
-                                              const int32_t *__restrict__ col, const double *__restrict__ val,
-                                              VlWf a, const unsigned long long *__restrict__ band)
-{
-    constexpr int R = NT, NI = (RING + NT - 1) / NT;
-    constexpr int RPP = NT / LV, PASSES = R / RPP;  // rows per pass, passes per tile
-    __shared__ double ring[RING];
-    __shared__ double yrow[R];
-    __shared__ int32_t rps[R];
-    __shared__ double red[3 * (NT / 64)];
-    const int t = threadIdx.x, g = t / LV, p = t % LV, lane = t & 63, wv = t >> 6;
-    const int64_t H = (int64_t)*band;
-    const int64_t c0 = n * blockIdx.x / gridDim.x, c1 = n * (blockIdx.x + 1) / gridDim.x;
-    const bool first = a.Yin == nullptr;
-    double cY = 0.0, cM = 0.0, cMM = 0.0;
-    const int64_t lo = c0 - H < 0 ? 0 : c0 - H, hi = c0 + R + H < n ? c0 + R + H : n;
-    if (!first) {
-        double al, be;
-        vl_wf_scalars(a, red, cY, cM, cMM, al, be);
-        if (blockIdx.x == 0 && t == 0) {
-            a.alpha[a.j - 1] = al;
-            a.beta[a.j - 1] = be;
-            if (a.lc >= 0 && a.lc < n) a.q[a.j - 1] = a.Vm[a.lc] * (1.0 / be);
-        }
-    }
-    // v_j[i] from the three inputs (the same expression in every block)
-    auto vform = [&](double y, double m, double mm) -> double {
-        if (first) return m;
-        double v = y * cY;
-        v = fma(-cM, m, v);
-        if (a.Vmm) v = fma(-cMM, mm, v);
-        return v;
-    };
-    const int64_t base = c0 - H;  // ring slot of v[i]: (i - base) mod RING
-    auto slot = [&](int64_t i) -> int { return (int)((uint32_t)(i - base) % (uint32_t)RING); };
-    // the first window [c0 - H, c0 + R + H) of v_j
-#pragma unroll 6
-    for (int k = 0; k < NI; ++k) {
-        const int64_t i = lo + t + (int64_t)k * NT;
-        if (i < hi)
-            ring[slot(i)] = vform(first ? 0.0 : a.Yin[i], a.Vm[i], a.Vmm ? a.Vmm[i] : 0.0);
-    }
-    __syncthreads();
-    double s1 = 0.0, s2 = 0.0, gg = 0.0;
-    auto rows_at = [&](int64_t r) { return (int)(c1 - r < R ? c1 - r : R); };
-    int64_t nkb = 0, nke = 0, nrp = 0;
-    if (c0 < c1) {
-        const int rw = rows_at(c0);
-        nkb = rp[c0];
-        nke = rp[c0 + rw];
-        nrp = t < rw ? rp[c0 + t] : 0;
-    }
-    for (int64_t r0 = c0; r0 < c1; r0 += R) {
-        const int rows = rows_at(r0);
-        // the next tile's slab of v_j (its three inputs) and this thread's row's v_{j-1}
-        const int64_t si = r0 + R + H + t;
-        const bool sin = si < n;
-        const double sy = (sin && !first) ? a.Yin[si] : 0.0, sm = sin ? a.Vm[si] : 0.0,
-                     smm = (sin && a.Vmm) ? a.Vmm[si] : 0.0;
-        const int64_t erow = r0 + t;
-        const double vprev = (t < rows && !first) ? a.Vm[erow] : 0.0;
-        const int64_t kb = nkb, kend = nke;
-        if (t < rows) rps[t] = (int)(nrp - kb);
-        __syncthreads();
-        if (r0 + R < c1) {
-            const int rw = rows_at(r0 + R);
-            nkb = kend;
-            nke = rp[r0 + R + rw];
-            nrp = t < rw ? rp[r0 + R + t] : 0;
-        }
-        const int32_t *cb = col + kb;
-        const double *vb = val + kb;
-        int ks[PASSES], ke[PASSES];
-#pragma unroll
-        for (int s = 0; s < PASSES; ++s) {
-            const int lr = s * RPP + g;
-            ks[s] = lr < rows ? rps[lr] : 0;
-            ke[s] = lr < rows ? (lr + 1 < rows ? rps[lr + 1] : (int)(kend - kb)) : 0;
-        }
-        int c[PASSES][2];
-        double v[PASSES][2];
-#pragma unroll
-        for (int s = 0; s < PASSES; ++s)
-#pragma unroll
-            for (int h2 = 0; h2 < 2; ++h2) {
-                const int k = ks[s] + p + h2 * LV;
-                c[s][h2] = k < ke[s] ? cb[k] : -1;
-                v[s][h2] = k < ke[s] ? vb[k] : 0.0;
-            }
-#pragma unroll
-        for (int s = 0; s < PASSES; ++s) {
-            double acc = 0.0;
-#pragma unroll
-            for (int h2 = 0; h2 < 2; ++h2)
-                if (c[s][h2] >= 0) acc = fma(v[s][h2], ring[slot(c[s][h2])], acc);
-            for (int k = ks[s] + p + 2 * LV; k < ke[s]; k += LV) acc = fma(vb[k], ring[slot(cb[k])], acc);
-#pragma unroll
-            for (int off = LV / 2; off > 0; off >>= 1) acc += __shfl_xor(acc, off, 64);
-            if (p == 0) yrow[s * RPP + g] = acc;
-        }
-        __syncthreads();
-        if (t < rows) {
-            const double vj = ring[slot(erow)], y = yrow[t];
-            if (!first) a.Vout[erow] = vj;
-            a.Yout[erow] = y;
-            s1 = fma(vj, y, s1);
-            s2 = fma(vprev, vj, s2);
-            gg = fma(vj, vj, gg);
-        }
-        if (sin) ring[slot(si)] = vform(sy, sm, smm);  // disjoint from this tile's window (2H + 2R <= RING)
-        __syncthreads();
-    }
-    // the block's three slabs: wave trees, then the waves in order
-#pragma unroll
-    for (int o = 32; o > 0; o >>= 1) {
-        s1 += __shfl_xor(s1, o, 64);
-        s2 += __shfl_xor(s2, o, 64);
-        gg += __shfl_xor(gg, o, 64);
-    }
-    if (lane == 0) {
-        red[3 * wv] = s1;
-        red[3 * wv + 1] = s2;
-        red[3 * wv + 2] = gg;
-    }
-    __syncthreads();
-    if (t == 0) {
-        double x1 = 0.0, x2 = 0.0, x3 = 0.0;
-        for (int i = 0; i < NT / 64; ++i) {
-            x1 += red[3 * i];
-            x2 += red[3 * i + 1];
-            x3 += red[3 * i + 2];
-        }
-        a.part_out[blockIdx.x] = x1;
-        a.part_out[gridDim.x + blockIdx.x] = x2;
-        a.part_out[2 * gridDim.x + blockIdx.x] = x3;
-    }
-}
-
-// After the last step launch: alpha / beta / q of step m - 1, and the
-// reference's post-call state (vector_lanczos.hpp:60,62): w = the last residual
-// v_m, q0 = q1 = q_{m-1} = v_{m-1} / beta_{m-1} (q1 null at m = 1).  Row-local:
-// each thread reads its row's inputs before writing (the outputs alias them).
-__global__ __launch_bounds__(kVlThreads) void k_vl_wf_final(int64_t n, VlWf a, double *w, double *q0,
-                                                            double *q1)
-{
-    __shared__ double red[3 * (kVlThreads / 64)];
-    double cY, cM, cMM, al, be;
-    vl_wf_scalars(a, red, cY, cM, cMM, al, be);
-    const double rb = 1.0 / be;
-    if (blockIdx.x == 0 && threadIdx.x == 0) {
-        a.alpha[a.j - 1] = al;
-        a.beta[a.j - 1] = be;
-        if (a.lc >= 0 && a.lc < n) a.q[a.j - 1] = a.Vm[a.lc] * rb;
-    }
-    for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x) {
-        const double y = a.Yin[i], m = a.Vm[i], mm = a.Vmm ? a.Vmm[i] : 0.0;
-        double v = y * cY;
-        v = fma(-cM, m, v);
-        if (a.Vmm) v = fma(-cMM, mm, v);
-        const double qv = m * rb;
-        w[i] = v;
-        q0[i] = qv;
-        if (q1) q1[i] = qv;
-    }
-}
-
 template <typename T>
 __global__ __launch_bounds__(kVlThreads) void k_vl_update(int64_t n, T *__restrict__ wn,
                                                           const T *__restrict__ q,
@@ -1681,78 +1453,6 @@ __global__ __launch_bounds__(kVlThreads) void k_vl_update(int64_t n, T *__restri
     block_store_slab(s, red, part_out);
 }
 
-// The wavefront form's launches (k_vl_wf): v_0 = b, v_j (j >= 1) in q0, q1, w
-// in turn (three live: v_{j-2}, v_{j-1} read while v_j is written), Y_j in two
-// alternating workspace vectors; the slabs alternate between two regions of
-// h->partials.  m step launches and one final launch.
-static int vector_lanczos_wf(lz_handle *h, int64_t n, const int64_t *rp, const int32_t *col, const double *val,
-                             int m, int64_t lc, const double *b, double *q, double *alpha, double *beta,
-                             double *q0, double *q1, double *w, int win, int lv,
-                             const unsigned long long *band)
-{
-    const size_t need = sizeof(double) * (size_t)std::max<int64_t>(n, 1) * 2;
-    if (need > h->ybuf_cap) {
-        LZ_HIP_TRY(hipStreamSynchronize(h->stream));
-        (void)hipFree(h->ybuf);
-        h->ybuf = nullptr;
-        h->ybuf_cap = 0;
-        LZ_HIP_TRY(hipMalloc(&h->ybuf, need));
-        h->ybuf_cap = need;
-    }
-    double *Y[2] = {static_cast<double *>(h->ybuf), static_cast<double *>(h->ybuf) + n};
-    double *X[3] = {q0, q1, w};
-    double *pr[2] = {h->partials, h->partials + 4096};
-    const int grid = win == 1 ? (int)std::max<int64_t>(1, std::min<int64_t>(ceil_div(n, 512), (int64_t)h->n_cu * 2))
-                              : (int)std::max<int64_t>(1, std::min<int64_t>(ceil_div(n, 1024), (int64_t)h->n_cu));
-    auto vbuf = [&](int j) -> const double * { return j == 0 ? b : X[(j - 1) % 3]; };
-    int P = 0;
-    for (int j = 0; j < m; ++j) {
-        VlWf a{};
-        a.Yin = j ? Y[(j - 1) & 1] : nullptr;
-        a.Vm = vbuf(j ? j - 1 : 0);
-        a.Vmm = j >= 2 ? vbuf(j - 2) : nullptr;
-        a.Vout = j ? X[(j - 1) % 3] : nullptr;
-        a.Yout = Y[j & 1];
-        a.part_in = pr[(j + 1) & 1];
-        a.P = P;
-        a.part_out = pr[j & 1];
-        a.alpha = alpha;
-        a.beta = beta;
-        a.q = q;
-        a.lc = lc;
-        a.j = j;
-        const int ev_s = prof_begin(h, PROF_SPMM_PASS);  // the step launch (bench: C2 roofline)
-#define LZ_VLWF(LV, NT, RING) \
-    hipLaunchKernelGGL((k_vl_wf<LV, NT, RING>), dim3(grid), dim3(NT), 0, h->stream, n, rp, col, val, a, band)
-        if (win == 1) {
-            if (lv == 4) LZ_VLWF(4, 512, 9216); else LZ_VLWF(8, 512, 9216);
-        } else {
-            if (lv == 4) LZ_VLWF(4, 1024, 16384); else LZ_VLWF(8, 1024, 16384);
-        }
-#undef LZ_VLWF
-        prof_end(h, ev_s);
-        LZ_LAUNCH_CHECK();
-        P = grid;
-    }
-    VlWf a{};
-    a.Yin = Y[(m - 1) & 1];
-    a.Vm = vbuf(m - 1);
-    a.Vmm = m >= 2 ? vbuf(m - 2) : nullptr;
-    a.part_in = pr[(m - 1) & 1];
-    a.P = P;
-    a.alpha = alpha;
-    a.beta = beta;
-    a.q = q;
-    a.lc = lc;
-    a.j = m;
-    const int gf = (int)std::max<int64_t>(1, std::min<int64_t>(ceil_div(n, kVlThreads), (int64_t)h->n_cu * 4));
-    const int ev_u = prof_begin(h, PROF_UPDATE_PASS);
-    hipLaunchKernelGGL(k_vl_wf_final, dim3(gf), dim3(kVlThreads), 0, h->stream, n, a, w, q0, m >= 2 ? q1 : nullptr);
-    prof_end(h, ev_u);
-    LZ_LAUNCH_CHECK();
-    return LZ_OK;
-}
-
 template <typename T>
 int vector_lanczos_dev(lz_handle *h, int64_t n, int64_t nnz, const int64_t *rp, const int32_t *col,
                        const T *val, int m, int64_t lc, const T *b, T *q, T *alpha, T *beta, T *q0,
@@ -1770,7 +1470,6 @@ int vector_lanczos_dev(lz_handle *h, int64_t n, int64_t nnz, const int64_t *rp, 
     const int cs = !(F64 && vk && al16) ? 0 : !strcmp(vk, "cs") ? 1 : !strcmp(vk, "cs2") ? 2 : 0;
     unsigned long long *band = reinterpret_cast<unsigned long long *>(h->partials + 8192);
     int win = 0;  // 1: <512, 9216>, 2: <1024, 16384>
-    unsigned long long Hb = ~0ull;  // the operator's half band (when measured)
     if (!cs && lv <= 8 && !(vk && !strcmp(vk, "row"))) {
         LZ_HIP_TRY(hipMemsetAsync(band, 0, sizeof(*band), h->stream));
         hipLaunchKernelGGL(k_vl_band, dim3((unsigned)std::max<int64_t>(1, std::min<int64_t>(ceil_div(n, 256), h->n_cu * 4))),
@@ -1779,18 +1478,10 @@ int vector_lanczos_dev(lz_handle *h, int64_t n, int64_t nnz, const int64_t *rp, 
         unsigned long long H = 0;
         LZ_HIP_TRY(hipMemcpyAsync(&H, band, sizeof(H), hipMemcpyDeviceToHost, h->stream));
         LZ_HIP_TRY(hipStreamSynchronize(h->stream));
-        Hb = H;
         win = (vk && !strcmp(vk, "win512")) ? 1 : (vk && !strcmp(vk, "win1024")) ? 2
               : 2 * H + 2 * 512 <= 9216     ? 1
               : 2 * H + 2 * 1024 <= 16384   ? 2
                                             : 0;
-    }
-    if constexpr (F64) {
-        const char *vw = getenv("LZ_VL_WF");  // "0": the two-pass step (A/B); read per call
-        // (only where the shape's ring holds the band: no global-gather form)
-        const bool fits = Hb != ~0ull && (win == 1 ? 2 * Hb + 2 * 512 <= 9216 : win == 2 && 2 * Hb + 2 * 1024 <= 16384);
-        if (fits && !(vw && vw[0] == '0') && m >= 1)
-            return vector_lanczos_wf(h, n, rp, col, val, m, lc, b, q, alpha, beta, q0, q1, w, win, lv, band);
     }
     const int grid = win == 1  ? (int)std::max<int64_t>(1, std::min<int64_t>(ceil_div(n, 512), (int64_t)h->n_cu * 2))
                      : win == 2 ? (int)std::max<int64_t>(1, std::min<int64_t>(ceil_div(n, 1024), (int64_t)h->n_cu))

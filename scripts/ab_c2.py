@@ -21,7 +21,8 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("cfgs", nargs="+")
     ap.add_argument("--rounds", type=int, default=4)
-    ap.add_argument("--steps", type=int, default=200)
+    ap.add_argument("--steps", "--m", type=int, default=200)
+    ap.add_argument("--no-check", action="store_true", help="skip the alpha / beta comparison")
     args = ap.parse_args()
     lz = ge.load_package()
     h = lz.Handle(0)
@@ -53,7 +54,7 @@ def main():
             if ref is None:
                 ref = a
             d = float(np.max(np.abs(a[:30] - ref[:30])) / np.max(np.abs(ref[:30])))
-            if not d < 1e-9:
+            if not d < 1e-9 and not args.no_check:
                 raise RuntimeError(f"alpha/beta (first 15 steps) differ under {c}: {d}")
             res[c].append(e0.elapsed_time(e1) * 1e3 / m)
             print(f"round {rnd} [{c}] {res[c][-1]:.2f} us/step  d(first 15 steps) {d:.1e}", flush=True)

@@ -23,6 +23,11 @@ run() {  # name timeout rocprof-args -- bench-args
   timeout -k 10 $t rocprofv3 "$@" > $O/$name.log 2>&1 || { echo "$name failed rc=$?"; tail -5 $O/$name.log; exit 1; }
   echo "$name ok"
 }
+# the bench lines themselves first (no profiler): headline + C4 per-rank share
+(cd $ROOT && timeout -k 10 600 python3 bench.py > $O/bench.json 2> $O/bench.err) || { echo "bench failed"; tail -5 $O/bench.err; exit 1; }
+echo "bench ok"; cat $O/bench.json | cut -c1-300
+(cd $ROOT && timeout -k 10 400 python3 bench.py --config c4rank --no-cpu-baseline > $O/bench_c4rank.json 2> $O/bench_c4rank.err) || { echo "c4rank failed"; tail -5 $O/bench_c4rank.err; exit 1; }
+echo "c4rank ok"
 run trace_c3 400 --kernel-trace --stats --output-format csv -d $O/trace_c3 -o run -- python3 $ROOT/bench.py $C3
 run trace_c4r 300 --kernel-trace --stats --output-format csv -d $O/trace_c4r -o run -- python3 $ROOT/bench.py --config c4rank --no-cpu-baseline
 run fetch_c3 300 --pmc FETCH_SIZE --output-format csv -d $O/fetch_c3 -o p -- python3 $ROOT/bench.py $C3P

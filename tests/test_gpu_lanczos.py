@@ -310,12 +310,7 @@ def test_block_b16_window_2e24_rows(lz, orc, handle, torch_cuda):
     assert handle.device_error() == 0
 
 
-@pytest.mark.parametrize("vl_wf", ["1", "0"])
-def test_vector_lanczos(lz, orc, handle, torch_cuda, golden, monkeypatch, vl_wf):
-    """fp64 single-vector Lanczos against the oracle: the one-launch-per-step
-    form (LZ_VL_WF=1, default where the band window holds the operator's band)
-    and the two-pass form."""
-    monkeypatch.setenv("LZ_VL_WF", vl_wf)
+def test_vector_lanczos(lz, orc, handle, torch_cuda, golden):
     torch = torch_cuda
     for A, m, lc in ((lz.gen_banded(200003, 10.0, 4096, seed=1), 12, 84),
                      (golden_csr(lz, golden, 10), 10, int(golden["lc"]))):
@@ -603,13 +598,11 @@ def test_block_final_state_off(lz, orc, handle, torch_cuda):
         assert np.array_equal(x, y)
 
 
-@pytest.mark.parametrize("vl_wf", ["1", "0"])
 @pytest.mark.parametrize("m", [1, 2, 3, 6])
-def test_vector_final_state(lz, handle, torch_cuda, monkeypatch, m, vl_wf):
+def test_vector_final_state(lz, handle, torch_cuda, m):
     """vector_lanczos leaves q0 = q1 = q_{m-1} and w = the last residual
-    (methods/vector_lanczos.hpp:60,62; q1 untouched at m = 1), in both step forms."""
+    (methods/vector_lanczos.hpp:60,62; q1 untouched at m = 1)."""
     import scipy.sparse as sp
-    monkeypatch.setenv("LZ_VL_WF", vl_wf)
     torch = torch_cuda
     A = lz.gen_banded(20_011, 10.0, 400, seed=80 + m)
     bv = lz.uniform_B(A.n, 1, seed=81)[:, 0].copy()
