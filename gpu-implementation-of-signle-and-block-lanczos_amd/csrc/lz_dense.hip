@@ -1142,6 +1142,80 @@ __global__ __launch_bounds__(256) void k_final_state16(int64_t n, const double *
     }
 }
 
+// The wavefront step's post-call state (Y != null, b = 16 fp64) on the f64
+// MFMA, one wave per 16-row strip, no LDS: W = Y beta^-1 - Vp P1 - Vq P2 and
+// Q = Vq beta^-1 (Q0, and Q1 when given) as three / one 16 x 16 x 16 products
+// per strip.  Lane (c, g) = (l & 15, l >> 4) loads row c's entries 4g .. 4g+3
+// of each input (two 16-B loads: the A operand in the permuted contraction
+// order of lz_wf.hip's updaters) and keeps B[4g + k][c] of each 16 x 16 matrix;
+// a product comes back as D[g + 4 r][c], stored as 4 rows x 128 B per
+// instruction.  Row-local: a wave loads its next strip's inputs before it
+// stores the current strip (other rows), and no other wave touches its rows,
+// so outputs may alias inputs.  A streaming pass: 3 reads + 3 writes of n x 16
+// doubles (the LDS form read each row 16 times from LDS and ran at 4.3 TB/s).
+__global__ __launch_bounds__(256) void k_final_state16m(int64_t n, const double *Y, const double *Vp,
+                                                        const double *Vq, const double *__restrict__ binv,
+                                                        const double *__restrict__ P1,
+                                                        const double *__restrict__ P2, double *Wout, double *Q0,
+                                                        double *Q1)
+{
+    const int lane = threadIdx.x & 63, c = lane & 15, g = lane >> 4;
+    double bq[3][4];
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+        const int idx = (4 * g + k) * 16 + c;
+        bq[0][k] = binv[idx];
+        bq[1][k] = P1 ? -P1[idx] : 0.0;
+        bq[2][k] = -P2[idx];
+    }
+    const int64_t S = (n + 15) / 16;
+    const int64_t wid = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6), nw = (int64_t)gridDim.x * 4;
+    typedef double d2v __attribute__((ext_vector_type(2)));
+    auto load = [&](const double *X, int64_t s, double out[4]) {
+        const int64_t r = s * 16 + c;
+        if (X && r < n) {
+            const d2v a = *reinterpret_cast<const d2v *>(X + r * 16 + 4 * g);
+            const d2v b = *reinterpret_cast<const d2v *>(X + r * 16 + 4 * g + 2);
+            out[0] = a.x; out[1] = a.y; out[2] = b.x; out[3] = b.y;
+        } else {
+            out[0] = out[1] = out[2] = out[3] = 0.0;
+        }
+    };
+    double ya[4], pa[4], ja[4];
+    int64_t s = wid;
+    if (s < S) {
+        load(Y, s, ya);
+        load(Vp, s, pa);
+        load(Vq, s, ja);
+    }
+    for (; s < S; s += nw) {
+        d4_t w = {0.0, 0.0, 0.0, 0.0}, q = {0.0, 0.0, 0.0, 0.0};
+#pragma unroll
+        for (int k = 0; k < 4; ++k) w = mfma16(pa[k], bq[1][k], w);
+#pragma unroll
+        for (int k = 0; k < 4; ++k) w = mfma16(ya[k], bq[0][k], w);
+#pragma unroll
+        for (int k = 0; k < 4; ++k) w = mfma16(ja[k], bq[2][k], w);
+#pragma unroll
+        for (int k = 0; k < 4; ++k) q = mfma16(ja[k], bq[0][k], q);
+        const int64_t sn = s + nw;
+        if (sn < S) {  // the next strip's rows (not this strip's) before this strip's stores
+            load(Y, sn, ya);
+            load(Vp, sn, pa);
+            load(Vq, sn, ja);
+        }
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+            const int64_t row = s * 16 + g + 4 * r;
+            if (row < n) {
+                Wout[row * 16 + c] = w[r];
+                Q0[row * 16 + c] = q[r];
+                if (Q1) Q1[row * 16 + c] = q[r];
+            }
+        }
+    }
+}
+
 template <typename T>
 int final_state(lz_handle *h, int64_t n, int b, const T *Y, const T *Vp, const T *Vq, const T *Wm, const T *binv,
                 const T *P1, const T *P2, T *Wout, T *Q0, T *Q1)
@@ -1150,11 +1224,16 @@ int final_state(lz_handle *h, int64_t n, int b, const T *Y, const T *Vp, const T
                  "final state (internal)");
     if (n <= 0) return LZ_OK;
     if constexpr (std::is_same<T, double>::value) {
+        const char *fm = getenv("LZ_FS_MFMA");  // "0": the LDS form for the wavefront's call too (A/B)
+        if (b == 16 && Y && !(fm && fm[0] == '0')) {
+            const int grid = (int)std::max<int64_t>(1, std::min<int64_t>(ceil_div(ceil_div(n, 16), 4), (int64_t)h->n_cu * 8));
+            hipLaunchKernelGGL(k_final_state16m, dim3(grid), dim3(256), 0, h->stream, n, Y, Vp, Vq, binv, P1, P2, Wout,
+                               Q0, Q1);
+            LZ_LAUNCH_CHECK();
+            return LZ_OK;
+        }
         if (b == 16) {
-            const char *e = getenv("LZ_FS_BPC");  // A/B: blocks per CU (0: one 64-row tile per block)
-            const int bpc = e ? atoi(e) : 4;
-            const int64_t cap = bpc > 0 ? (int64_t)h->n_cu * bpc : ceil_div(n, 64);
-            const int grid = (int)std::max<int64_t>(1, std::min<int64_t>(ceil_div(n, 64), cap));
+            const int grid = (int)std::max<int64_t>(1, std::min<int64_t>(ceil_div(n, 64), (int64_t)h->n_cu * 4));
             hipLaunchKernelGGL(k_final_state16, dim3(grid), dim3(256), 0, h->stream, n, Y, Vp, Vq, Wm, binv, P1, P2,
                                Wout, Q0, Q1);
             LZ_LAUNCH_CHECK();

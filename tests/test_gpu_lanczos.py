@@ -549,7 +549,7 @@ def test_prof_class_mask(lz, handle, torch_cuda, monkeypatch, wf):
 
 
 @pytest.mark.parametrize("m", [1, 2, 5])
-@pytest.mark.parametrize("path", ["wavefront", "twopass", "unfused", "sep_b4", "b2_f32_b32"])
+@pytest.mark.parametrize("path", ["wavefront", "wavefront_lds", "twopass", "unfused", "sep_b4", "b2_f32_b32"])
 def test_block_final_state(lz, orc, handle, torch_cuda, monkeypatch, path, m):
     """On return Q0 = Q1 = Q_{m-1} and W = the last residual, as the reference
     leaves them (methods/block_lanczos.hpp:145,159,162; Q1 is not written at
@@ -558,6 +558,8 @@ def test_block_final_state(lz, orc, handle, torch_cuda, monkeypatch, path, m):
     b, dt = (4, np.float64) if path == "sep_b4" else (32, np.float32) if path == "b2_f32_b32" else (16, np.float64)
     if path == "twopass":
         monkeypatch.setenv("LZ_PASS_WF", "0")
+    if path == "wavefront_lds":  # the LDS form of the post-call pass (default: MFMA strips)
+        monkeypatch.setenv("LZ_FS_MFMA", "0")
     A = lz.gen_banded(30_011, 10.0, 700, seed=70 + m, dtype=dt)
     B = lz.uniform_B(A.n, b, seed=71, dtype=dt)
     lc = 29_000
