@@ -244,7 +244,8 @@ int lz_debug_last_wf(lz_handle *h, int out[2]);
  * (host): [0] plan applies, [1] 16-bit columns valid, [2] T tiles, [3] rows per
  * tile, [4..7] the span words (max back / forward reach, max width, range
  * flags). nx, xoff: gather-source rows and the row of local row 0 (n, 0 on one
- * GPU). */
+ * GPU). deps_out / col16_out / info[4..7] hold this operator's plan only when
+ * info[0] = 1 (the plan ran and applies). */
 int lz_debug_wf_plan(lz_handle *h, int64_t n, int64_t nnz, const int64_t *row_ptr, const int32_t *col_idx,
                      int64_t nx, int64_t xoff, int32_t *deps_out, int16_t *col16_out, int32_t info[8]);
 
