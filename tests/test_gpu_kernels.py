@@ -309,3 +309,33 @@ def test_spmm_fixed_nnz_tiles(lz, orc, handle, torch_cuda, monkeypatch, n, npr, 
     ref = orc.csr_spmm(A, X)
     tol = 1e-13 if dtype == "float64" else 1e-5
     assert np.allclose(Y.cpu().numpy(), ref, rtol=tol, atol=tol * np.abs(ref).max())
+
+
+@pytest.mark.parametrize("cond", [1.0, 1e2, 1e4, 1e6, 1e10, -1.0])
+def test_sqrtm_b16_newton_schulz(lz, orc, handle, torch_cuda, monkeypatch, cond):
+    """b = 16 without eigenvalues asked for: the Newton-Schulz route (lz_sqrtm.hpp
+    sqrtm_ns16) where G is well conditioned, the Jacobi route past ~1e6 (and for
+    an indefinite G, cond < 0: |lambda| as the reference's) -- both against the
+    oracle's eigendecomposition sqrtm and against each other (LZ_SQRTM_NS=0)."""
+    torch = torch_cuda
+    b = 16
+    rng = np.random.default_rng(int(abs(cond)) % 1000 + 5)
+    Q, _ = np.linalg.qr(rng.standard_normal((b, b)))
+    ev = 2.5 * np.power(abs(cond), -np.arange(b) / (b - 1))
+    if cond < 0:
+        ev[[3, 9]] *= -1.0  # indefinite: the eigendecomposition route takes |lambda|
+    G = (Q * ev) @ Q.T
+    G = 0.5 * (G + G.T)
+    s, si = orc.sqrtm_pair(G)
+    out = {}
+    for ns in ("1", "0"):
+        monkeypatch.setenv("LZ_SQRTM_NS", ns)
+        beta = torch.empty(b, b, dtype=torch.float64, device="cuda")
+        binv = torch.empty_like(beta)
+        handle.sqrtm(torch.from_numpy(G).cuda(), beta, binv)
+        out[ns] = (beta.cpu().numpy(), binv.cpu().numpy())
+    kap = abs(cond)
+    for ns, (bg, big) in out.items():
+        assert np.max(np.abs(bg - s)) <= 1e-12 * np.abs(s).max(), ns
+        assert np.max(np.abs(big - si)) <= max(1e-12, 1e-16 * kap) * np.abs(si).max(), ns
+    assert np.max(np.abs(out["1"][1] - out["0"][1])) <= max(1e-12, 1e-16 * kap) * np.abs(si).max()
