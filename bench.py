@@ -146,11 +146,14 @@ def _norm(name):
     return name.replace(" ", "").replace("lz::", "").replace("void", "").split("(")[0]
 
 
-def pmc_record(kind, kernel, n, nnz, hw, kernel_full=None):
+def pmc_record(kind, kernel, n, nnz, hw, kernel_full=None, nnz_tol=0.0):
     """A committed rocprofv3 PMC summary (profiles/*_pmc_<kind>_<kernel>.json or,
     kind "", profiles/*_pmc_<kernel>.json) of this bench's workload, newest first.
     Refused (None, reason) unless it names the kernel instantiation this run
-    launches (kernel_full) and was taken on the current source of that kernel."""
+    launches (kernel_full) and was taken on the current source of that kernel.
+    nnz_tol > 0 (a distributed rank): a summary of the same rows and half width
+    whose nnz is within that fraction (the per-rank share run by --config c4rank,
+    whose columns stop at the share) is taken, and the source says so."""
     pat = f"*_pmc_{kind + '_' if kind else ''}{kernel}.json"
     reason = "no committed counter file for this workload"
     for f in sorted(glob.glob(os.path.join(ROOT, "profiles", pat)), reverse=True):
@@ -159,9 +162,12 @@ def pmc_record(kind, kernel, n, nnz, hw, kernel_full=None):
         except (OSError, ValueError):
             continue
         w = d.get("workload", {})
-        if not (w.get("n") == n and w.get("nnz") == nnz and w.get("halfwidth") == hw):
+        wn = w.get("nnz") or 0
+        if not (w.get("n") == n and w.get("halfwidth") == hw and abs(wn - nnz) <= nnz_tol * nnz):
             continue
         rel = os.path.relpath(f, ROOT)
+        if wn != nnz:
+            rel += f" (the per-rank share: nnz {wn} against this rank's {nnz})"
         if _norm(d.get("kernel_full", "")) != _norm(kernel_full or kernel):
             reason = f"{rel}: kernel {d.get('kernel_full')!r} is not the launched {kernel_full!r}"
             continue
@@ -732,10 +738,12 @@ def main():
             tot = wf_bytes(n, A.nnz, b, K, cb=cb)
             ach = tot / (spmm_ms * 1e-3) / 1e9
             kname, kshort = wf_kernel(n, hw, A.nnz)
-            d, tsrc = pmc_record("", kshort, n, A.nnz, hw, kname)
+            d, tsrc = pmc_record("", kshort, n, A.nnz, hw, kname, nnz_tol=0.01 if world > 1 else 0.0)
             traffic = None
-            if d and d.get("hbm_bytes_first_launch") and spmm_cnt == K:  # the launch mix of bytes_per_launch
-                traffic = round((d["hbm_bytes_first_launch"] + (K - 1) * d["hbm_bytes_per_launch"]) / K)
+            if d and d.get("hbm_bytes_first_launch"):
+                # the solve's bytes spread over its launches, as bytes_per_launch (at N > 1 a step is
+                # several launches over the same rows: the requested tiles' pass 2, the step, the boundary)
+                traffic = round((d["hbm_bytes_first_launch"] + (K - 1) * d["hbm_bytes_per_launch"]) / spmm_cnt)
             roof = {"bound": "hbm", "kernel": kname, "achieved": round(ach, 1),
                     "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": round(ach / HBM_PEAK_GBS, 4),
                     "traffic": traffic, "traffic_unit": "bytes/launch (mean over the profiled solve's launches)",

@@ -336,6 +336,7 @@ def test_sqrtm_b16_newton_schulz(lz, orc, handle, torch_cuda, monkeypatch, cond)
         out[ns] = (beta.cpu().numpy(), binv.cpu().numpy())
     kap = abs(cond)
     for ns, (bg, big) in out.items():
-        assert np.max(np.abs(bg - s)) <= 1e-12 * np.abs(s).max(), ns
+        # (two eigendecomposition routes differ by ~eps sqrt(kappa) in beta at kappa = 1e10)
+        assert np.max(np.abs(bg - s)) <= max(1e-12, 1e-16 * kap ** 0.5) * np.abs(s).max(), ns
         assert np.max(np.abs(big - si)) <= max(1e-12, 1e-16 * kap) * np.abs(si).max(), ns
     assert np.max(np.abs(out["1"][1] - out["0"][1])) <= max(1e-12, 1e-16 * kap) * np.abs(si).max()
