@@ -279,6 +279,12 @@ static int block_lanczos_fused16(lz_handle *h, int64_t n, int64_t nnz, const int
     // (latency-bound passes over the columns, each ending in a host sync) run on
     // the main one; joined before its sqrtm
     LZ_TRY(gram_beside(h, n, B, &P));
+    // every return from here on leaves the main stream behind the Gram (an early
+    // error return too: the side stream's slabs must not race a later call)
+    struct JoinSide {
+        lz_handle *h;
+        ~JoinSide() { (void)hipStreamWaitEvent(h->stream, h->ev_join, 0); }
+    } join_side{h};
     {
         WfPlan wp;
         LZ_TRY(wf_plan16(h, n, nnz, rp, col, &wp));  // n < 2^24 only
