@@ -477,6 +477,12 @@ def main():
         plain = {"kernel": spmm_kernel(A.nnz, n), "avg_ms": round(ms / cnt, 4),
                  "bytes_per_launch": spmm_bytes(n, A.nnz, b), "achieved_GBs": round(gbs, 1),
                  "frac_of_hbm_peak": round(gbs / HBM_PEAK_GBS, 4)}
+        # the same figures as a roofline object, with the kernel's measured HBM traffic
+        trp, srcp = pmc_traffic("k_spmm_seg", n, A.nnz, args.halfwidth, spmm_kernel(A.nnz, n))
+        plain["roofline"] = {"bound": "hbm", "kernel": spmm_kernel(A.nnz, n), "achieved": round(gbs, 1),
+                             "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": round(gbs / HBM_PEAK_GBS, 4),
+                             "traffic": trp, "traffic_source": srcp, "avg_ms": round(ms / cnt, 4),
+                             "bytes_per_launch": spmm_bytes(n, A.nnz, b)}
         if not args.no_cpu_baseline:  # the CPU SpMM on the same operator and block
             orc = ge.load_oracle()
             Yc, tc = orc.csr_spmm_timed(A, B, reps=3)
