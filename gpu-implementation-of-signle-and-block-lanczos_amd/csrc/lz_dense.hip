@@ -1081,6 +1081,45 @@ __global__ __launch_bounds__(256) void k_final_state(int64_t n, int b, const T *
     }
 }
 
+// The post-call state when W is already the last residual (Y == null: the
+// two-pass and separate-SpMM paths): Q = Vq beta^-1 into Q0 (and Q1), W <- Wm
+// when they differ.  Thread (column j, row group) keeps column j of beta^-1 in
+// registers and reads each staged row as LDS broadcasts: B multiply-adds per
+// output (the general kernel above also formed the three Y-path sums and read
+// every matrix entry from LDS: 4.7 ms for C5's 10M x 32 block).  Same products
+// in the same order as k_final_state's q.
+template <typename T, int B>
+__global__ __launch_bounds__(256) void k_final_q(int64_t n, const T *Vq, const T *Wm, const T *__restrict__ binv,
+                                                 T *Wout, T *Q0, T *Q1)
+{
+    constexpr int TR = 64, RG = 256 / B;
+    __shared__ T rs[TR * B];
+    const int tid = threadIdx.x, j = tid % B, rg = tid / B;
+    T mcol[B];
+#pragma unroll
+    for (int i = 0; i < B; ++i) mcol[i] = binv[i * B + j];
+    const bool copyw = Wm != nullptr && Wm != Wout;
+    XcdSched s(ceil_div(n, TR));
+    for (int64_t u = s.begin; u < s.end; u += s.step) {
+        const int64_t r0 = u * TR;
+        const int nr = (int)(n - r0 < TR ? n - r0 : TR), ne = nr * B;
+        __syncthreads();  // the previous tile's rows are no longer read
+        for (int e = tid; e < ne; e += 256) rs[e] = Vq[r0 * B + e];
+        // (element e is staged and copied by the same thread: a W aliasing Vq is read first)
+        if (copyw)
+            for (int e = tid; e < ne; e += 256) Wout[r0 * B + e] = Wm[r0 * B + e];
+        __syncthreads();  // every row staged (and W copied) before any Q row is written
+        for (int r = rg; r < nr; r += RG) {
+            T q = T(0);
+#pragma unroll
+            for (int i = 0; i < B; ++i) q = fma(rs[r * B + i], mcol[i], q);
+            const int64_t g = (r0 + r) * B + j;
+            Q0[g] = q;
+            if (Q1) Q1[g] = q;
+        }
+    }
+}
+
 // b = 16 fp64: thread (column j = t & 15, row group t >> 4) keeps column j of
 // binv, P1, P2 in registers and walks 4 of the tile's 64 rows; a row's values
 // are LDS broadcasts (16-B reads).  Same products and order as k_final_state.
@@ -1223,6 +1262,15 @@ int final_state(lz_handle *h, int64_t n, int b, const T *Y, const T *Vp, const T
     LZ_ARG_CHECK(b >= 1 && b <= 32 && Vq && binv && Wout && Q0 && (Y ? P2 != nullptr : Wm != nullptr),
                  "final state (internal)");
     if (n <= 0) return LZ_OK;
+    if (!Y && (b == 16 || b == 32)) {
+        const int grid = (int)std::max<int64_t>(1, std::min<int64_t>(ceil_div(n, 64), (int64_t)h->n_cu * 4));
+        if (b == 16)
+            hipLaunchKernelGGL((k_final_q<T, 16>), dim3(grid), dim3(256), 0, h->stream, n, Vq, Wm, binv, Wout, Q0, Q1);
+        else
+            hipLaunchKernelGGL((k_final_q<T, 32>), dim3(grid), dim3(256), 0, h->stream, n, Vq, Wm, binv, Wout, Q0, Q1);
+        LZ_LAUNCH_CHECK();
+        return LZ_OK;
+    }
     if constexpr (std::is_same<T, double>::value) {
         const char *fm = getenv("LZ_FS_MFMA");  // "0": the LDS form for the wavefront's call too (A/B)
         if (b == 16 && Y && !(fm && fm[0] == '0')) {

@@ -42,6 +42,7 @@ def main():
             for kv in c.split():
                 k, v = kv.split("=", 1)
                 os.environ[k] = v
+            h.set_final_state(os.environ.get("AB_FS", "1") == "1")  # AB_FS=0: no post-call state pass
             h.block_lanczos_blas(Ad, B, 2, 84, q, al, be, *P)
             torch.cuda.synchronize()
             h.prof_enable(True)
