@@ -60,6 +60,7 @@ HIP_SYMBOLS = [
     ("lz_device_ok", _c_int, [_c_int]),
     ("lz_device_error", _c_int, [_c_vp, ctypes.POINTER(_c_int)]),
     ("lz_debug_poison_lds", _c_int, [_c_vp, ctypes.c_uint32]),
+    ("lz_debug_set_device_error", _c_int, [_c_vp, _c_int]),
     ("lz_prof_enable", _c_int, [_c_vp, _c_int]),
     ("lz_prof_enable_mask", _c_int, [_c_vp, ctypes.c_uint]),
     ("lz_prof_read", _c_int, [_c_vp, _c_int, ctypes.POINTER(_c_dbl), ctypes.POINTER(_c_int)]),
@@ -569,6 +570,10 @@ class Handle:
         _check(self.L.lz_device_error(self._h, ctypes.byref(c)), "lz_device_error")
         return c.value
 
+    def debug_set_device_error(self, code: int):
+        """Store `code` into the device error word (test support)."""
+        _check(self.L.lz_debug_set_device_error(self.ptr, code), "lz_debug_set_device_error")
+
     def debug_poison_lds(self, pattern: int = 0xFFFFFFFF):
         """Fill every CU's LDS with `pattern` (test support: stale-LDS reads show as NaN)."""
         _check(self.L.lz_debug_poison_lds(self._h, pattern), "lz_debug_poison_lds")
@@ -707,11 +712,15 @@ def run_virtual_ranks(nranks: int, fn, device: int = 0, timeout: float = 600.0):
     torch.cuda.synchronize(device)
     group = LocalGroup(nranks, device)
     handles = [Handle(device) for _ in range(nranks)]
+    # the ranks' streams are made here and outlive every handle (closed below
+    # after a device synchronise), so no handle ever refers to a stream whose
+    # Python object a finished thread dropped
+    streams = [torch.cuda.Stream(device) for _ in range(nranks)]
     out, errs = [None] * nranks, [None] * nranks
 
     def body(r):
         try:
-            with torch.cuda.device(device), torch.cuda.stream(torch.cuda.Stream(device)):
+            with torch.cuda.device(device), torch.cuda.stream(streams[r]):
                 handles[r].comm_init_local(group, r)
                 out[r] = fn(r, handles[r])
                 torch.cuda.current_stream(device).synchronize()
@@ -737,6 +746,8 @@ def run_virtual_ranks(nranks: int, fn, device: int = 0, timeout: float = 600.0):
             for h in handles:
                 h.close()
             group.close()
+            group._keep.clear()
+            del streams[:]
     for r, e in enumerate(errs):
         if e is not None:
             raise LanczosError(f"virtual rank {r}: {e}") from e

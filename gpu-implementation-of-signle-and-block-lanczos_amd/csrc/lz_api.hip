@@ -52,8 +52,17 @@ void set_error(const char *fmt, ...)
 
 // The wavefront step and the persistent pass 1 end a wait they would
 // otherwise never leave by setting the device error word (lz_device_error);
-// their results are then wrong.  The solve entry points that launch them read
-// the word once at the end (one host synchronisation per solve) and fail.
+// their results are then wrong.  The solve entry points that launch them clear
+// the word on their stream first (a word an earlier call left behind is not
+// this solve's) and read it once at the end (one host synchronisation per
+// solve); a nonzero word fails the solve and stays readable by
+// lz_device_error.
+static int solve_begin(lz_handle *h)
+{
+    LZ_HIP_TRY(hipMemsetAsync(h->err_flag, 0, sizeof(int), h->stream));
+    return LZ_OK;
+}
+
 static int solve_status(lz_handle *h)
 {
     int e = 0;
@@ -190,15 +199,9 @@ struct QfreeBufs {
 
 // B^T B's per-block slabs (b = 16 fp64) on the handle's side stream, forked
 // from the main stream; h->ev_join is recorded behind them (the caller waits on
-// it before the slabs are folded).  LZ_GRAM_SIDE=0: on the main stream (A/B).
+// it before the slabs are folded).
 static int gram_beside(lz_handle *h, int64_t n, const double *B, int *P)
 {
-    const char *e = getenv("LZ_GRAM_SIDE");
-    if (e && e[0] == '0') {
-        LZ_TRY(gram_partials<double>(h, n, 16, B, B, 16, P));
-        LZ_HIP_TRY(hipEventRecord(h->ev_join, h->stream));
-        return LZ_OK;
-    }
     LZ_HIP_TRY(hipEventRecord(h->ev_fork, h->stream));
     LZ_HIP_TRY(hipStreamWaitEvent(h->side, h->ev_fork, 0));
     std::swap(h->stream, h->side);  // gram_partials launches on h->stream
@@ -1056,18 +1059,15 @@ static int dist_solve_wf16(lz_handle *h, int form, HaloPlan *hp, int64_t n, int6
     return LZ_OK;
 }
 
-// A rank that fails mid-solve wakes the others of a virtual-rank group (they
-// would otherwise wait at its next collective until the barrier timeout); for
-// RCCL the abort is a no-op and the caller's job control applies.
+// The distributed solve itself; the extern "C" wrappers decide on an abort
+// (dist_fail).
 template <typename T>
 static int dist_solve(lz_handle *h, int form, HaloPlan *hp, int64_t n, int64_t n_pad, int64_t nnz, const int64_t *rp,
                       const int32_t *col, const T *val, int b, int m, int64_t lc, const T *B, T *q, T *alpha, T *beta,
                       T *X0, T *X1)
 {
+    LZ_TRY(solve_begin(h));
     int rc = dist_solve_impl<T>(h, form, hp, n, n_pad, nnz, rp, col, val, b, m, lc, B, q, alpha, beta, X0, X1);
-    if (rc != LZ_OK && h->comm) h->comm->abort();
-    // (after the closing fence: every rank has finished its collectives, so a
-    // rank failing here leaves no peer waiting)
     if (rc == LZ_OK) rc = solve_status(h);
     return rc;
 }
@@ -1075,6 +1075,29 @@ static int dist_solve(lz_handle *h, int form, HaloPlan *hp, int64_t n, int64_t n
 }  // namespace lz
 
 using namespace lz;
+
+// A distributed call that fails aborts the handle's communicator when that can
+// release a peer.  A virtual-rank group: always -- its abort wakes every rank
+// waiting at the host barrier at once (they would otherwise wait until the
+// barrier timeout), and the group is a test / rehearsal harness.  RCCL: only
+// once this call has issued a collective (Comm::issued moved).  ncclCommAbort
+// is permanent -- the caller then destroys the communicator (lz_comm_destroy)
+// and initialises a new one with a new unique id -- and RCCL peers blocked in a
+// collective return only when they poll ncclCommGetAsyncError or abort
+// themselves, so a failure before the first collective (arguments, workspace
+// growth, the plans) leaves the communicator usable, and the caller fails every
+// rank alike or calls lz_comm_abort.
+// (LZ_E_DEVICE comes from the status read after the solve's closing fence: no
+// peer waits on this rank then, and the communicator stays usable.)
+static int dist_fail(lz_handle *h, int rc, uint64_t issued0)
+{
+    if (rc != LZ_OK && rc != LZ_E_DEVICE && h && h->comm &&
+        (h->comm->abort_wakes_peers() || h->comm->issued != issued0))
+        h->comm->abort();
+    return rc;
+}
+
+static uint64_t comm_issued(const lz_handle *h) { return h && h->comm ? h->comm->issued : 0; }
 
 #define LZ_HANDLE_CHECK(h)                                                          \
     do {                                                                            \
@@ -1181,6 +1204,13 @@ int lz_device_error(lz_handle *h, int *code)
     LZ_HIP_TRY(hipStreamSynchronize(h->stream));
     LZ_HIP_TRY(hipMemcpy(code, h->err_flag, sizeof(int), hipMemcpyDeviceToHost));
     LZ_HIP_TRY(hipMemset(h->err_flag, 0, sizeof(int)));
+    return LZ_OK;
+}
+
+int lz_debug_set_device_error(lz_handle *h, int code)
+{
+    LZ_HANDLE_CHECK(h);
+    LZ_HIP_TRY(hipMemsetD32Async(reinterpret_cast<hipDeviceptr_t>(h->err_flag), code, 1, h->stream));
     return LZ_OK;
 }
 
@@ -1408,6 +1438,7 @@ int lz_block_lanczos(lz_handle *h, int64_t n, int64_t nnz, const int64_t *rp, co
     LZ_HANDLE_CHECK(h);
     LZ_TRY(block_args(n, nnz, rp, col, val, b, m, lc, B, q, alpha, beta, Q0, Q1, W));
     if (dtype == LZ_F64 && b == 16) {
+        LZ_TRY(solve_begin(h));
         LZ_TRY(block_lanczos_fused16(h, n, nnz, rp, col, (const double *)val, m, lc, (const double *)B, (double *)q,
                                      (double *)alpha, (double *)beta, (double *)Q0, (double *)Q1, (double *)W));
         return solve_status(h);
@@ -1487,15 +1518,24 @@ int lz_debug_wf_plan(lz_handle *h, int64_t n, int64_t nnz, const int64_t *row_pt
     lz::WfPlan wp;
     LZ_TRY(lz::wf_plan16(h, n, nnz, row_ptr, col_idx, &wp, nx, xoff));
     const int64_t T = wp.tr > 0 ? lz::ceil_div(n, (int64_t)wp.tr) : 0;
+    // outputs only from this call's plan (never a stale earlier one): deps and
+    // spans when the plan kernel ran, the 16-bit columns when they were kept;
+    // zero-filled otherwise (the caller sized deps_out for T = n / 16 + 2 tiles)
     int sp[4] = {0, 0, 0, 0};
-    if (h->wf_cap >= (size_t)T + 64 && T > 0) {
+    if (wp.planned && T > 0) {
         LZ_HIP_TRY(hipMemcpyAsync(deps_out, h->wf_deps, sizeof(int32_t) * 2 * (size_t)T, hipMemcpyDeviceToDevice,
                                   h->stream));
         LZ_HIP_TRY(hipMemcpyAsync(sp, h->err_flag + 12, sizeof(sp), hipMemcpyDeviceToHost, h->stream));
+    } else if (T > 0) {
+        LZ_HIP_TRY(hipMemsetAsync(deps_out, 0, sizeof(int32_t) * 2 * (size_t)T, h->stream));
     }
-    if (h->c16_cap >= (size_t)nnz * 2 && nnz > 0)
-        LZ_HIP_TRY(hipMemcpyAsync(col16_out, h->c16buf, sizeof(int16_t) * (size_t)nnz, hipMemcpyDeviceToDevice,
-                                  h->stream));
+    if (nnz > 0) {
+        if (wp.col16)
+            LZ_HIP_TRY(hipMemcpyAsync(col16_out, wp.col16, sizeof(int16_t) * (size_t)nnz, hipMemcpyDeviceToDevice,
+                                      h->stream));
+        else
+            LZ_HIP_TRY(hipMemsetAsync(col16_out, 0, sizeof(int16_t) * (size_t)nnz, h->stream));
+    }
     LZ_HIP_TRY(hipStreamSynchronize(h->stream));
     info[0] = wp.ok ? 1 : 0;
     info[1] = wp.col16 ? 1 : 0;
@@ -1553,10 +1593,10 @@ int lz_block_lanczos_dist(lz_handle *h, int64_t n_local, int64_t n_pad, int64_t 
                           int lc_rank, const void *B_local, void *q, void *alpha, void *beta,
                           void *Q0, void *Q1, void *W, void *X_full)
 {
+    const uint64_t issued0 = comm_issued(h);
     const int rc = lz_block_lanczos_dist_impl(h, n_local, n_pad, n_global, nnz_local, rp, col, val, dtype, b, m,
                                               lc_local, lc_rank, B_local, q, alpha, beta, Q0, Q1, W, X_full);
-    if (rc != LZ_OK && h && h->comm) h->comm->abort();  // peers must not wait for this rank
-    return rc;
+    return dist_fail(h, rc, issued0);
 }
 
 static int halo_init_impl(lz_handle *h, int64_t row0, int64_t n_local, const int64_t *recv_counts,
@@ -1665,12 +1705,10 @@ int lz_halo_init(lz_handle *h, int64_t row0, int64_t n_local, const int64_t *rec
                  const int32_t *halo_rows)
 {
     LZ_HANDLE_CHECK(h);
+    const uint64_t issued0 = comm_issued(h);
     const int rc = halo_init_impl(h, row0, n_local, recv_counts, halo_rows);
-    if (rc != LZ_OK) {
-        if (h->comm) h->comm->abort();  // a peer blocked in the same set-up must not wait for this rank
-        halo_free(h);                   // never leave a half-built plan behind
-    }
-    return rc;
+    if (rc != LZ_OK) halo_free(h);  // never leave a half-built plan behind
+    return dist_fail(h, rc, issued0);  // a peer blocked in the same set-up must not wait for this rank
 }
 
 int lz_halo_sizes(lz_handle *h, int64_t *n_halo, int64_t *n_send)
@@ -1725,10 +1763,10 @@ int lz_block_lanczos_halo(lz_handle *h, int64_t n_local, int64_t nnz_local, cons
                           int64_t lc_local, int lc_rank, const void *B_local, void *q, void *alpha,
                           void *beta, void *X0, void *X1)
 {
+    const uint64_t issued0 = comm_issued(h);
     const int rc = lz_block_lanczos_halo_impl(h, n_local, nnz_local, rp, col, val, dtype, b, m, lc_local, lc_rank,
                                               B_local, q, alpha, beta, X0, X1);
-    if (rc != LZ_OK && h && h->comm) h->comm->abort();  // peers must not wait for this rank
-    return rc;
+    return dist_fail(h, rc, issued0);
 }
 
 }  // extern "C"

@@ -35,9 +35,11 @@ public:
     }
     bool aborted = false;
     const char *kind() const override { return "rccl"; }
-    // a failing rank aborts its communicator: RCCL operations in flight on it
-    // (a peer's included, once the peers see the failed connection) return
-    // instead of waiting, and every later call here fails
+    // a failing rank aborts its communicator: this rank's RCCL operations in
+    // flight on it return, and every later call here fails (lz_comm_destroy and
+    // a new lz_comm_init with a new unique id make the handle usable again).
+    // Peers blocked in a collective with this rank are released only if they
+    // poll ncclCommGetAsyncError or abort their own communicator.
     void abort() override
     {
         if (c && !aborted) (void)ncclCommAbort(c);
@@ -55,6 +57,7 @@ public:
     int allreduce_sum(double *buf, size_t count, hipStream_t s) override
     {
         LZ_TRY(usable());
+        ++issued;
         LZ_NCCL_CHECK(ncclAllReduce(buf, buf, count, ncclDouble, ncclSum, c, s));
         return LZ_OK;
     }
@@ -62,6 +65,7 @@ public:
     {
         // in place when send is this rank's slot (RCCL then copies nothing locally)
         LZ_TRY(usable());
+        ++issued;
         if (slot_bytes % 8 == 0)
             LZ_NCCL_CHECK(ncclAllGather(send, X, slot_bytes / 8, ncclDouble, c, s));
         else
@@ -71,6 +75,7 @@ public:
     int exchange(const P2POp *ops, int nops, hipStream_t s) override
     {
         LZ_TRY(usable());
+        ++issued;
         LZ_NCCL_CHECK(ncclGroupStart());
         ncclResult_t r = ncclSuccess;
         for (int i = 0; i < nops && r == ncclSuccess; ++i) {
@@ -212,9 +217,11 @@ public:
     }
     const char *kind() const override { return "local"; }
     void abort() override { g->abort("aborted by a rank"); }
+    bool abort_wakes_peers() const override { return true; }
 
     int begin(int op, const void *send, size_t bytes, const P2POp *ops, int nops, hipStream_t s)
     {
+        ++issued;
         par = (int)(seq & 1);
         auto &me = g->slot[rank];
         LocalGroupState::Pub &p = me.pub[par];

@@ -44,6 +44,7 @@ struct P2POp {
 class Comm {
 public:
     int nranks = 1, rank = 0;
+    uint64_t issued = 0;  // collectives issued so far (a failure after one aborts, dist_solve)
     virtual ~Comm() = default;
     virtual const char *kind() const = 0;
     // in place sum of count doubles over the ranks; every rank gets the same bits
@@ -59,8 +60,12 @@ public:
         (void)s;
         return LZ_OK;
     }
-    // wake every rank blocked in a collective of this group with an error
+    // wake every rank blocked in a collective of this group with an error; for
+    // RCCL this is ncclCommAbort, after which the communicator is unusable
     virtual void abort() {}
+    // whether abort() releases peers that wait for a collective this rank never
+    // issued (a virtual-rank group's host barrier: yes; RCCL: no)
+    virtual bool abort_wakes_peers() const { return false; }
 };
 
 // RCCL communicator from a 128-byte ncclUniqueId

@@ -108,6 +108,7 @@ struct WfPlan {
     int var = 0;              // measurement shape (LZ_WF_SHAPE 104 / 111), 0: the standard ones
     const int16_t *col16 = nullptr;  // pass 1's 16-bit columns (made in the same pass), or null
     int64_t xoff = 0;         // gather-source row of local row 0 (the all-gather form's slot)
+    bool planned = false;     // the plan kernel ran (deps and spans are this call's)
 };
 // once per solve: per-tile dependency ranges and the 16-bit columns in one pass
 // over the CSR columns; synchronises the stream once

@@ -1149,11 +1149,17 @@ static int launch_seg(lz_handle *h, int64_t n, const int64_t *rp, const int32_t 
     }
     const int parity = h->longq_parity;
     h->longq_parity ^= 1;
-    // measurement only (results wrong), read per call: LZ_SPMM_DIAG = tiles mod
-    // this; LZ_SPMM_DIAG_Y=1: the Y tiles stay the blocks' own
+    // diag: measurement only (results wrong), in a -DLZ_DIAG build alone:
+    // LZ_SPMM_DIAG = tiles mod this (every input L2-resident, DESIGN.md 4
+    // SpMM); LZ_SPMM_DIAG_Y=1: the Y tiles stay the blocks' own.  The shipped
+    // library always passes 0.
+#ifdef LZ_DIAG
     const char *dg = getenv("LZ_SPMM_DIAG");
     const char *dy = getenv("LZ_SPMM_DIAG_Y");
     const int diag = (dg ? atoi(dg) : 0) | (dy && dy[0] == '1' ? 1 << 30 : 0);
+#else
+    constexpr int diag = 0;
+#endif
     hipLaunchKernelGGL((k_spmm_seg<T, B, TR, CAP, WIN, 0, YCM, EPI>), dim3((unsigned)st), dim3(256), 0, h->stream, n, rp,
                        col, val, X, ldx, nx, Y, ldy, h->longq, parity, Wp, Mm, diag);
     const int g2 = (int)std::max<int64_t>(1, std::min<int64_t>(st, (int64_t)h->n_cu * 4));

@@ -225,16 +225,18 @@ __device__ void sqrtm_tail(const double *Am, const double *Um, double *cc, doubl
 // instead of ~7 sweeps of 15 rotation rounds.  Returns false -- the caller
 // then runs the Jacobi route, whose small eigenvalues keep high relative
 // accuracy -- unless |Z Y - I|_max fell to the rounding floor within kNsMax
-// iterations (kappa(G) up to ~1e6: beta within ~4e-14 and beta^-1 within
-// ~3e-12 of the Jacobi route's, scripts/probe/sqrtm_probe.hip), so an
-// ill-conditioned or nearly rank-deficient G (Krylov breakdown) takes the
-// reference's eigendecomposition path.
+// iterations AND |Z|_F^2 <= kNsKappa, which bounds kappa(G) by 4e6 (kappa(G)
+// up to 1e6: beta within ~4e-14 and beta^-1 within ~3e-12 of the Jacobi
+// route's, scripts/probe/sqrtm_probe.hip), so an ill-conditioned or nearly
+// rank-deficient G (Krylov breakdown) takes the reference's
+// eigendecomposition path.
 // Lane l = (c = l & 15, q = l >> 4) keeps rows/columns in the MFMA operand
 // layouts: xa[k] = X[c][4q + k] (A operand, permuted contraction order),
 // xb[k] = X[4q + k][c] (B operand); a product comes back as D[q + 4 r][c].
 // S0, S1, S2: 16 x 17 LDS doubles of scratch each.  On success ya / yb / za /
 // zb hold the converged Y and Z, and scale = |G|_F.
 constexpr int kNsMax = 22;
+constexpr double kNsKappa = 4e6;  // |Z|_F^2 bound: kappa(G) <= 4e6 (sqrtm_ns16)
 __device__ __forceinline__ bool sqrtm_ns16(const double *g, double *S0, double *S1, double *S2, double ya[4],
                                            double yb[4], double za[4], double zb[4], double &scale, int tid)
 {
@@ -270,7 +272,19 @@ __device__ __forceinline__ bool sqrtm_ns16(const double *g, double *S0, double *
 #pragma unroll
         for (int o = 32; o > 0; o >>= 1) e = fmax(e, __shfl_xor(e, o, 64));
         if (!(e < 1e3)) return false;              // diverging, or NaN
-        if (e <= 1.5e-14 || (e < 1e-10 && e >= 0.5 * prev)) return true;  // at the rounding floor
+        if (e <= 1.5e-14 || (e < 1e-10 && e >= 0.5 * prev)) {  // at the rounding floor
+            // and only for kappa(G) <= kNsKappa: Z ~ A^{-1/2}, so |Z|_F^2 =
+            // sum 1 / lambda_i(A) >= 1 / lambda_min(A) >= kappa(G) (lambda_max(A)
+            // <= 1).  Past it the Newton-Schulz floor (beta^-1 off the Jacobi
+            // route by ~6e-10 at kappa 1e8, profiles/r04v_sqrtm_probe.log) is
+            // above the eigendecomposition route's, which then runs.
+            double z2 = 0.0;
+#pragma unroll
+            for (int k = 0; k < 4; ++k) z2 = fma(za[k], za[k], z2);
+#pragma unroll
+            for (int o = 32; o > 0; o >>= 1) z2 += __shfl_xor(z2, o, 64);
+            return z2 <= kNsKappa;
+        }
         prev = e;
 #pragma unroll
         for (int r = 0; r < 4; ++r) S0[(q + 4 * r) * LD + c] = ((q + 4 * r == c) ? 1.5 : 0.0) - 0.5 * m[r];

@@ -34,6 +34,7 @@
 // every load of V_{j+1} is an sc1 load.  Results do not depend on placement;
 // liveness needs every block resident (one block per CU, grid <= CUs), and
 // every wait is bounded (a timeout sets the device error word).
+#include <atomic>
 #include <climits>
 
 #include "lz_internal.hpp"
@@ -696,6 +697,7 @@ int wf_plan16(lz_handle *h, int64_t n, int64_t nnz, const int64_t *rp, const int
 {
     if (nx < 0) nx = n;
     pl->ok = false;
+    pl->planned = false;
     pl->col16 = nullptr;
     const char *e = getenv("LZ_PASS_WF");  // "0": the two-pass step (A/B); read per call
     // rows of about 11 entries or fewer on average: the tile's CSR run fits the
@@ -751,6 +753,7 @@ int wf_plan16(lz_handle *h, int64_t n, int64_t nnz, const int64_t *rp, const int
     int sp[4] = {0, 0, 0, 1};
     LZ_HIP_TRY(hipMemcpyAsync(sp, spans, sizeof(sp), hipMemcpyDeviceToHost, h->stream));
     LZ_HIP_TRY(hipStreamSynchronize(h->stream));
+    pl->planned = true;
     pl->hback = sp[0];
     pl->hfwd = sp[1];
     pl->ok = sp[2] <= kWfMaxSpan && !(sp[3] & 2);
@@ -793,11 +796,16 @@ int wf_step16(lz_handle *h, int64_t n, const int64_t *rp, const int32_t *col, co
     const char *gc = getenv("LZ_GRID_CAP");
     const int cap = gc && atoi(gc) > 0 ? atoi(gc) : (h->grid_cap > 0 ? h->grid_cap : h->n_cu);
     const int grid = (int)std::max<int64_t>(1, std::min<int64_t>(work, std::min(cap, h->n_cu)));
-    // LZ_WF_DBG (timing diagnostics only; results are wrong): bit 0 skips the
-    // loaders' flag polls, bit 1 the updaters' work, bit 2 the pass-1 tiles;
-    // bit 3 / bit 6 run the updaters at issue priority 0 / 3 (default 2)
+    // dbg: timing diagnostics (results are wrong), only in a -DLZ_DIAG build
+    // (LZ_WF_DBG): bit 0 skips the loaders' flag polls, bit 1 the updaters'
+    // work, bit 2 the pass-1 tiles; bit 3 / bit 6 run the updaters at issue
+    // priority 0 / 3 (default 2).  The shipped library always passes 0.
+#ifdef LZ_DIAG
     const char *dg = getenv("LZ_WF_DBG");
     const int dbg = dg ? atoi(dg) : 0;
+#else
+    constexpr int dbg = 0;
+#endif
     if (P2 && nq == 0 && p1a == p1b) {  // nothing to do
         *nparts = 0;
         return LZ_OK;
@@ -806,37 +814,38 @@ int wf_step16(lz_handle *h, int64_t n, const int64_t *rp, const int32_t *col, co
     // tiles a pass-1 tile reaches ahead in the block's order, plus two
     const int KB = grid < 8 ? grid : grid / 8;
     const int lmin = (int)((pl.hback + pl.hfwd + KB - 1) / KB) + 2;
-    const char *le = getenv("LZ_WF_LEAD");
-    // C3 (lmin 4): shape 111 best at 7 (5: 3.07 ms, 6: 1.90, 7: 1.82, 8: 1.84, 10: 1.87);
-    // the 2-loader shapes at 8
-    const int lead = std::max(lmin, le ? atoi(le) : lmin + (pl.var ? 3 : 4));  // (wide: to be tuned)
-    // LZ_WF_CPOL: streaming (nt) hints, bit 0 the updaters' reads, bit 1 the CSR
-    // stages, bit 2 the Y stores, bit 3 the V_{j+1} stores.  Default 7: every
-    // stream touched once is nt, so the V_{j+1} rows stay in L2 for the gathers
-    // (C3: 1.74-1.81 -> 1.69-1.70 ms; 8, nt on V_{j+1}, 1.84)
-    const char *cp = getenv("LZ_WF_CPOL");
-    const int cpol = cp ? atoi(cp) : 7;
+    // C3 (lmin 4): shape 111 best at lmin + 3 = 7 (5: 3.07 ms, 6: 1.90, 7: 1.82,
+    // 8: 1.84, 10: 1.87); the 2-loader shapes at lmin + 4; the wide shape flat
+    // from lmin to lmin + 16 (profiles/r04_wide_lead_ab.log)
+    const int lead = lmin + (pl.var ? 3 : 4);
+    // streaming (nt) hints: bit 0 the updaters' reads, bit 1 the CSR stages,
+    // bit 2 the Y stores, bit 3 the V_{j+1} stores.  7: every stream touched
+    // once is nt, so the V_{j+1} rows stay in L2 for the gathers (C3: 1.74-1.81
+    // -> 1.69-1.70 ms; 8, nt on V_{j+1} too, 1.84)
+    constexpr int cpol = 7;
     // Liveness needs every block resident at once (their waits on each other's
     // flags).  The launch is checked: the occupancy of the instantiation at its
     // block size must admit the grid (one block per CU, grid <= CUs).  A block
     // that lands on a CU another kernel still holds starts when that kernel
     // ends; the bounded waits cover that, so no kernel that itself waits on
-    // this launch may share the device (lz_hip.h).  LZ_WF_COOP=1 makes it a
-    // cooperative launch, which the runtime refuses (instead of running part of
-    // the grid later) when the grid cannot be resident: measured 0.3-0.8 %
-    // slower at C3 (profiles/r04b_coop_ab.log), and the runtime runs such
-    // launches one at a time, so 8 virtual ranks' step launches serialised (C4
-    // at N = 8 virtual ranks: 106 ms per step against 57.4 ordinary) and an
-    // exchange's kernels could not overlap the step launch.
-    const char *co = getenv("LZ_WF_COOP");
-    const bool coop = co && co[0] == '1';
+    // this launch may share the device (lz_hip.h).  (A cooperative launch was
+    // measured and removed in round 5: 0.3-0.8 % slower at C3,
+    // profiles/r04b_coop_ab.log; the runtime ran such launches one at a time,
+    // so 8 virtual ranks' step launches serialised, 106 against 57.4 ms per C4
+    // step; and the one process that used it ended in a segfault at exit,
+    // DESIGN.md 5.)
     int rc = LZ_OK;
     const int ev = prof_begin(h, PROF_SPMM_PASS);
     // (the block is 64 (NC + NL + NU) threads: the kernel refuses any other size)
     auto go = [&](auto kern, int waves) {
-        static int occ = -1;  // blocks per CU of this instantiation (per process: one device model)
-        if (occ < 0 && hipOccupancyMaxActiveBlocksPerMultiprocessor(&occ, kern, 64 * waves, 0) != hipSuccess)
-            occ = 0;
+        // blocks per CU of this instantiation (per process: one device model;
+        // virtual ranks' threads may race here, each storing the same value)
+        static std::atomic<int> occ_cache{-1};
+        int occ = occ_cache.load(std::memory_order_relaxed);
+        if (occ < 0) {
+            if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&occ, kern, 64 * waves, 0) != hipSuccess) occ = 0;
+            occ_cache.store(occ, std::memory_order_relaxed);
+        }
         if ((int64_t)grid > (int64_t)occ * h->n_cu) {
             set_error("wavefront step: %d blocks of %d threads cannot all be resident (%d per CU x %d CUs)", grid,
                       64 * waves, occ, h->n_cu);
@@ -856,19 +865,6 @@ int wf_step16(lz_handle *h, int64_t n, const int64_t *rp, const int32_t *col, co
                      *a_Vg = Vg;
         const uint64_t *a_pr = pairs;
         double *a_Vo = Vout, *a_Yo = Yo, *a_part = part;
-        if (coop) {
-            void *args[] = {&a_n,  &a_rp, &a_col, &a_c16, &a_val, &a_pr,    &a_Yj, &a_Vp,  &a_Vj, &a_Vo,
-                            &a_bi, &a_P1, &a_P2,  &a_Vg,  &a_Yo,  &deps,    &flags, &a_ep, &a_hb, &a_lead,
-                            &a_part, &err, &a_dbg, &a_nx, &a_p1a, &a_p1b, &a_T,   &a_cp, &a_xo, &a_q0,
-                            &a_q1, &a_q2, &a_q3, &a_sv};
-            const hipError_t e = hipLaunchCooperativeKernel(reinterpret_cast<const void *>(kern), dim3(grid),
-                                                            dim3(64 * waves), args, 0, h->stream);
-            if (e != hipSuccess) {
-                set_error("wavefront step: cooperative launch of %d blocks -> %s", grid, hipGetErrorString(e));
-                rc = LZ_E_HIP;
-            }
-            return;
-        }
         hipLaunchKernelGGL(kern, dim3(grid), dim3(64 * waves), 0, h->stream, a_n, a_rp, a_col, a_c16, a_val, a_pr,
                            a_Yj, a_Vp, a_Vj, a_Vo, a_bi, a_P1, a_P2, a_Vg, a_Yo, deps, flags, a_ep, a_hb, a_lead,
                            a_part, err, a_dbg, a_nx, a_p1a, a_p1b, a_T, a_cp, a_xo, a_q0, a_q1, a_q2, a_q3, a_sv);

@@ -65,8 +65,15 @@ int lz_device_ok(int device);
  * lz_prof_enable resets the record (capacity 4096 launches). */
 /* Synchronises the handle's stream and returns (then clears) the device error
  * word: nonzero if a persistent kernel abandoned a bounded spin-wait (its
- * results are then invalid).  0 in normal operation. */
+ * results are then invalid).  0 in normal operation.  Every solve that checks
+ * the word (lz_block_lanczos at b = 16 fp64, the distributed solves) clears it
+ * on its stream when it starts, so a word left by an earlier call never fails a
+ * later solve; a solve that fails with LZ_E_DEVICE leaves its word readable
+ * here. */
 int lz_device_error(lz_handle *h, int *code);
+/* Test support: store `code` into the device error word (on the handle's
+ * stream), as a kernel that gave up a wait would. */
+int lz_debug_set_device_error(lz_handle *h, int code);
 
 /* Test support: fills the LDS of every CU with a 32-bit pattern (0xFFFFFFFF
  * reads back as a double NaN), and the handle's slab and scratch workspaces
@@ -226,7 +233,13 @@ int lz_local_group_create(int device, int nranks, lz_local_group **g);
 int lz_local_group_destroy(lz_local_group *g);
 int lz_local_group_abort(lz_local_group *g);
 int lz_comm_init_local(lz_handle *h, lz_local_group *g, int rank);
-/* wake every rank of h's group blocked in a collective (local groups; a no-op for RCCL) */
+/* Wake every rank of h's group blocked in a collective (local groups), or
+ * ncclCommAbort h's RCCL communicator.  A distributed solve that fails after
+ * issuing a collective does this itself.  An aborted RCCL communicator stays
+ * unusable (every later collective returns LZ_E_COMM): lz_comm_destroy, then
+ * lz_comm_init with a new unique id.  RCCL peers blocked in a collective with
+ * an aborted rank return only once they abort too (or poll the communicator's
+ * async error). */
 int lz_comm_abort(lz_handle *h);
 /* Test support: the interior row range [out[0], out[1]) whose pass 1 ran
  * beside the exchange in the handle's last distributed solve ({-1, -1}: the
@@ -244,8 +257,9 @@ int lz_debug_last_wf(lz_handle *h, int out[2]);
  * (host): [0] plan applies, [1] 16-bit columns valid, [2] T tiles, [3] rows per
  * tile, [4..7] the span words (max back / forward reach, max width, range
  * flags). nx, xoff: gather-source rows and the row of local row 0 (n, 0 on one
- * GPU). deps_out / col16_out / info[4..7] hold this operator's plan only when
- * info[0] = 1 (the plan ran and applies). */
+ * GPU). deps_out and info[4..7] are this call's plan whenever the plan kernel
+ * ran (info[0] = 1: it also applies), zero otherwise; col16_out is this call's
+ * 16-bit columns when info[1] = 1, zero otherwise. Never a stale earlier plan. */
 int lz_debug_wf_plan(lz_handle *h, int64_t n, int64_t nnz, const int64_t *row_ptr, const int32_t *col_idx,
                      int64_t nx, int64_t xoff, int32_t *deps_out, int16_t *col16_out, int32_t info[8]);
 

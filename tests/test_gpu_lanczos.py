@@ -631,3 +631,33 @@ def test_vector_final_state(lz, handle, torch_cuda, m):
         assert np.array_equal(g1.cpu().numpy(), g0.cpu().numpy())
     else:
         assert bool(torch.isnan(g1).all())
+
+
+def test_device_error_word_cleared_by_next_solve(lz, orc, handle, torch_cuda):
+    """A device error word left behind by an earlier call (here stored by the
+    test hook, as a wait that gave up would) must not fail the next solve: every
+    checked solve clears the word when it starts.  The hook itself
+    is visible through lz_device_error, which reads and clears."""
+    A = lz.gen_banded(20_011, 10.0, 512, seed=31)
+    B = lz.uniform_B(A.n, 16, seed=3)
+    m, lc = 4, 777
+    handle.debug_set_device_error(5)
+    assert handle.device_error() == 5
+    assert handle.device_error() == 0
+    handle.debug_set_device_error(6)
+    got = gpu_block(lz, handle, torch_cuda, A, B, m, lc)  # raises on LZ_E_DEVICE
+    assert handle.device_error() == 0
+    assert_close_run(lz, m, 16, got, orc.block_lanczos(A, B, m, lc))
+
+
+@pytest.mark.parametrize("cap", ["32", "7"])
+def test_block_b16_wavefront_grid_cap(lz, orc, handle, torch_cuda, monkeypatch, cap):
+    """LZ_GRID_CAP (read per call): the wavefront step on at most `cap` blocks,
+    as one virtual rank's share of the CUs runs (bench --config c4rank with the
+    cap measures that share alone); same results as the oracle."""
+    monkeypatch.setenv("LZ_GRID_CAP", cap)
+    A = lz.gen_banded(60_013, 10.0, 2048, seed=77)
+    B = lz.uniform_B(A.n, 16, seed=2)
+    m, lc = 5, 30_000
+    got = gpu_block(lz, handle, torch_cuda, A, B, m, lc)
+    assert_close_run(lz, m, 16, got, orc.block_lanczos(A, B, m, lc))

@@ -379,3 +379,51 @@ def test_vranks_halo_exchange_back_to_back(lz, torch_cuda):
         nl = int(bounds[r + 1] - bounds[r])
         for b, X in Xs.items():
             assert np.array_equal(X[nl:], Gs[b][rows.astype(np.int64)]), (r, b)
+
+
+def test_vranks_barrier_timeout(lz, torch_cuda, monkeypatch):
+    """LZ_LOCAL_TIMEOUT_S (read when the group is created): a rank that never
+    reaches a collective makes the others' barrier give up after that many
+    seconds with LZ_E_COMM (no abort involved: rank 1 simply returns)."""
+    import time
+    monkeypatch.setenv("LZ_LOCAL_TIMEOUT_S", "2")
+    A = lz.gen_banded(4_000, 5.0, 100, seed=62)
+    bounds = np.array([0, 2000, 4000], np.int64)
+
+    def rank_fn(r, h):
+        if r == 1:
+            return None
+        _, col, _ = _slab(A, 0, 2000)
+        _, cnt, rows = lz.halo_plan(col, bounds, 0)
+        h.halo_init(0, 2000, cnt, rows)  # collective: rank 1 never arrives
+
+    t0 = time.time()
+    with pytest.raises(lz.LanczosError, match="timeout"):
+        lz.run_virtual_ranks(2, rank_fn)
+    assert 1.5 < time.time() - t0 < 60
+
+
+@pytest.mark.timeout(900)
+def test_vranks_c4_full_size_halo(lz, orc, torch_cuda):
+    """BASELINE config C4 at full size: n = 4e7 rows, ~25 entries per row
+    (nnz ~ 1e9), half width 2^16, row-partitioned over 8 virtual ranks in the
+    halo form (the wavefront step with the requested rows' pass 2 first and the
+    exchange beside the rest of each step, asserted), 3 steps against the
+    oracle on the GLOBAL operator (methods/block_lanczos.hpp:131-166).  The 8
+    ranks share one device here; over RCCL each is one MI355X (bench.py --gpus
+    8)."""
+    import time
+    N, n, m, lc = 8, 40_000_000, 3, 84
+    t0 = time.time()
+    A = lz.gen_banded(n, 25.0, 1 << 16, seed=20261015)
+    B = lz.uniform_B(n, 16, seed=20261015)
+    assert 0.99e9 < A.nnz < 1.01e9
+    ref = orc.block_lanczos(A, B, m, lc)
+    t1 = time.time()
+    bounds = np.array([n * g // N for g in range(N + 1)], np.int64)
+    wfs = []
+    got, _ = run_dist(lz, torch_cuda, A, B, m, lc, N, "halo", bounds=bounds, wf_out=wfs)
+    t2 = time.time()
+    assert all(w == (True, True) for w in wfs), wfs
+    assert_close_run(lz, m, 16, got, ref)
+    print(f"C4 8 virtual ranks: operator + oracle {t1 - t0:.1f} s, distributed solve {t2 - t1:.1f} s")
