@@ -87,25 +87,34 @@ PASS1_MFMA_FLOP_PER_ROW = 16 * 2048 // 16
 PASS2_MFMA_FLOP_PER_ROW = 8 * 2048 // 16
 
 
-def wf_kernel(n, hw, nnz=None):
+def wf_kernel(n, hw, nnz=None, one_gpu=True):
     """(full name, PMC short name) of the wavefront-step kernel (lz_wf.hip wf_step16):
     <consumers, stage entries, stages, loaders, updaters, strip slots - 1, 16-bit columns,
-    SW = false (the all-gather save-V_j form runs only at N > 1)>."""
+    SW = false (the all-gather save-V_j form runs only at N > 1), GEN> -- GEN false for
+    the one-GPU solve's launches of the default shapes (the specialised form, round 5)."""
     c16 = col_bytes(n, hw) == 2
     sh = os.environ.get("LZ_WF_SHAPE", "111")
     tf = 'true' if c16 else 'false'
+    gen = 'false' if one_gpu else 'true'
     if nnz is not None and nnz > 10.2 * n:  # the wide shape (C4's density)
-        return f"k_wf16<10,4400,2,1,{3 if c16 else 2},1,{tf},false>", "k_wf16"
+        return f"k_wf16<10,4400,2,1,{3 if c16 else 2},1,{tf},false,{gen}>", "k_wf16"
     if sh not in ("10", "11", "12"):  # default: 1 loader + 11 consumers + 4 updaters
-        return f"k_wf16<11,{11 * 16 * 11},3,1,4,1,{tf},false>", "k_wf16"
+        return f"k_wf16<11,{11 * 16 * 11},3,1,4,1,{tf},false,{gen}>", "k_wf16"
     nc = int(sh)
     du = {10: 2 if c16 else 1, 11: 2, 12: 3 if c16 else 2}[nc]
-    return f"k_wf16<{nc},{nc * 16 * 11},3,2,{14 - nc},{du},{tf},false>", "k_wf16"
+    return f"k_wf16<{nc},{nc * 16 * 11},3,2,{14 - nc},{du},{tf},false,true>", "k_wf16"
 
 
 # MFMA work of the wavefront step per row: updaters 12 (V_{j+1}) + 4 (G) + 4 (S2),
-# consumers 4 (S1) per 16-row strip
+# consumers 4 (S1) per 16-row strip (lz_wf.hip: 20 mfma16 per updater strip, 4 per
+# consumer strip); a solve's first launch is pass 1 only (the consumers' 4)
 WF_MFMA_FLOP_PER_ROW = 24 * 2048 // 16
+WF_MFMA_FLOP_PER_ROW_FIRST = 4 * 2048 // 16
+
+
+def wf_mfma_flop(n, launches):
+    """MFMA FLOP of one wavefront solve of `launches` launches (the first pass 1 only)."""
+    return (WF_MFMA_FLOP_PER_ROW_FIRST + max(launches - 1, 0) * WF_MFMA_FLOP_PER_ROW) * n
 
 
 def fused_kernel(nnz, n):
@@ -743,7 +752,7 @@ def main():
             # boundary tiles' pass 1 is a launch of its own: same bytes, more launches)
             tot = wf_bytes(n, A.nnz, b, K, cb=cb)
             ach = tot / (spmm_ms * 1e-3) / 1e9
-            kname, kshort = wf_kernel(n, hw, A.nnz)
+            kname, kshort = wf_kernel(n, hw, A.nnz, one_gpu=not dist_path)
             d, tsrc = pmc_record("", kshort, n, A.nnz, hw, kname, nnz_tol=0.01 if world > 1 else 0.0)
             traffic = None
             if d and d.get("hbm_bytes_first_launch"):
@@ -758,14 +767,20 @@ def main():
                     "bytes_note": f"{K} steps per solve in {spmm_cnt} launches: the first step pass 1 only (A + 2nbs), "
                                   f"the others pass 2 of step j + pass 1 of step j+1 (A + 5nbs); A with {cb}-byte "
                                   f"columns"}
-            fl = WF_MFMA_FLOP_PER_ROW * n
+            # the timed solve's MFMA FLOP (its first launch pass 1 only) over its launches' kernel time
+            fl = wf_mfma_flop(n, spmm_cnt) / spmm_cnt
             tf = fl / t_pass / 1e12
-            ent = {"kernel": kshort, "mfma_flop_per_launch": fl, "avg_ms": round(t_pass * 1e3, 4),
-                   "achieved": round(tf, 3), "frac": round(tf / FP64_MFMA_PEAK_TFS, 4)}
+            ent = {"kernel": kshort, "mfma_flop_per_launch": round(fl), "avg_ms": round(t_pass * 1e3, 4),
+                   "achieved": round(tf, 3), "frac": round(tf / FP64_MFMA_PEAK_TFS, 4),
+                   "mfma_flop_per_steady_launch": WF_MFMA_FLOP_PER_ROW * n,
+                   "flop_note": f"{spmm_cnt} launches: the first 4 v_mfma_f64_16x16x4f64 per 16-row strip (S1), "
+                                f"the others 24 (V_(j+1) 12, G 4, S2 4, S1 4); 2048 FLOP each"}
             d, src = pmc_record("mfma", kshort, n, A.nnz, hw, kname)
             if d:
                 ent.update({"pmc_MfmaUtil_pct": d.get("MfmaUtil_pct"),
-                            "pmc_mfma_flop_per_launch": d.get("mfma_flop_per_launch"), "pmc_source": src})
+                            "pmc_mfma_flop_per_launch": d.get("mfma_flop_per_launch"),
+                            "pmc_mfma_flop_per_steady_launch": d.get("mfma_flop_per_steady_launch"),
+                            "pmc_dispatch_mix": d.get("dispatch_mix"), "pmc_source": src})
             else:
                 ent["pmc_note"] = src
             mfma = {"unit": "TFLOP/s", "peak": FP64_MFMA_PEAK_TFS, "dtype": "f64 (v_mfma_f64_16x16x4f64)",

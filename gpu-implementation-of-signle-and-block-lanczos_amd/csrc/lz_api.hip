@@ -369,7 +369,10 @@ static int block_lanczos_b2_32(lz_handle *h, int64_t n, int64_t nnz, const int64
             LZ_HIP_TRY(hipStreamWaitEvent(h->side, h->ev_fork, 0));
             hipStream_t main = h->stream;
             h->stream = h->side;
-            const int rc = sqrtm_pair<float>(h, b, nullptr, np, beta + (j + 1) * bb, binv[(j + 1) & 1], nullptr);
+            // (from the 32 folded slabs m_b2 read: the same G bits, and the
+            // one-workgroup kernel pulls 256 KB instead of the passes' 8 MB)
+            const int rc = sqrtm_pair<float>(h, b, nullptr, ng, beta + (j + 1) * bb, binv[(j + 1) & 1], nullptr,
+                                             h->partials2);
             h->stream = main;
             LZ_TRY(rc);
             LZ_HIP_TRY(hipEventRecord(h->ev_join, h->side));

@@ -652,6 +652,21 @@ __global__ __launch_bounds__(kRedThreads) void k_sqrtm_b(const T *__restrict__ G
         reduce_slabs(wa.part, wa.P, BB, ws1, scratch);
         if (L) reduce_slabs(wa.part + (int64_t)wa.P * BB, wa.P, BB, ws2, scratch);
     }
+    if constexpr (B == 32) {
+        // Newton-Schulz on the MFMA by four waves (sqrtm_ns32) when no
+        // eigenvalues are asked for and G is well enough conditioned; the
+        // whole workgroup takes part (its barriers), then the one-wave Jacobi
+        // route otherwise.  (Abuf / Ubuf: 4 x 32 x 33 doubles of scratch.)
+        if (ns && eig == nullptr) {
+            double sc = 0.0;
+            const bool ok = sqrtm_ns32(g, Abuf[0], Abuf[1], Ubuf[0], scratch, sc, tid);
+            if (ok) {
+                sqrtm_ns32_tail<T>(Abuf[0], Abuf[1], sc, g, beta, binv, L, LB, tid);
+                return;
+            }
+            __syncthreads();  // the scratch is the Jacobi route's matrices
+        }
+    }
     if (tid >= 64) return;  // one wave from here on
     const int j = tid % B, r0 = tid / B;  // column, first row of this lane
     const int jq = B - 1 - j;                      // partner position of j
@@ -830,7 +845,7 @@ int sqrtm_pair(lz_handle *h, int b, const T *G, int nparts, T *beta, T *beta_inv
     {
     const int ev_ = prof_begin(h, PROF_SMALL);
     const double *sl = slabs ? slabs : h->partials;
-    const char *nse = getenv("LZ_SQRTM_NS");  // "0": the Jacobi route at b = 16 as well (A/B, tests)
+    const char *nse = getenv("LZ_SQRTM_NS");  // "0": the Jacobi route at b = 16 and 32 as well (A/B, tests)
     const int ns = (nse && nse[0] == '0') ? 0 : 1;
 #define LZ_SQRTM_B(BV)                                                                        \
     case BV:                                                                                  \

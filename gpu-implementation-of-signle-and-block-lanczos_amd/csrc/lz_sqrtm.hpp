@@ -354,4 +354,134 @@ __device__ void sqrtm_ns16_tail(const double ya[4], const double yb[4], const do
     }
 }
 
+// Coupled Newton-Schulz square root for B = 32 (sqrtm_ns16's iteration and
+// exits) on the f64 MFMA, by waves 0..3 of the workgroup: wave w owns block
+// (I, J) = (w >> 1, w & 1) of every 32 x 32 product, C_IJ = sum_K A_IK B_KJ,
+// 8 v_mfma_f64_16x16x4f64 per product (lane (c, q) supplies A[16I + c][16K +
+// 4q + k] and B[16K + 4q + k][16J + c]; C comes back as C[16I + q + 4r][16J +
+// c]).  Y, Z, T live in LDS (32 x 33 doubles each); one iteration is three
+// products and three workgroup barriers.  EVERY thread of the workgroup calls
+// this (the barriers); threads past 256 only keep the count.  red: 8 doubles
+// of LDS.  On success Ys / Zs hold the converged Y and Z, scale = |G|_F.
+// Replaces the one-wave Jacobi of the reference's syevjBatched route
+// (utils/lib_utils.hpp:696-745) at b = 32 for kappa(G) <= kNsKappa.
+__device__ __forceinline__ bool sqrtm_ns32(const double *g, double *Ys, double *Zs, double *Ts, double *red,
+                                           double &scale, int tid)
+{
+    constexpr int LD = 33;
+    const bool act = tid < 256;
+    const int w = (tid >> 6) & 3, lane = tid & 63, c = lane & 15, q = lane >> 4;
+    const int I = w >> 1, J = w & 1;
+    // A = sym(G) / |G|_F (lower triangle read, as sqrtm_init), Z = I
+    double f = 0.0;
+    if (act) {
+        for (int e = tid; e < 1024; e += 256) {
+            const int i = e >> 5, j = e & 31;
+            const double a = j < i ? g[i * 32 + j] : g[j * 32 + i];
+            Ys[i * LD + j] = a;
+            Zs[i * LD + j] = i == j ? 1.0 : 0.0;
+            f = fma(a, a, f);
+        }
+#pragma unroll
+        for (int o = 32; o > 0; o >>= 1) f += __shfl_xor(f, o, 64);
+        if (lane == 0) red[w] = f;
+    }
+    __syncthreads();
+    f = (red[0] + red[1]) + (red[2] + red[3]);
+    if (!(f > 0.0) || !(f < 1e300)) return false;  // (uniform)
+    scale = sqrt(f);
+    const double is = 1.0 / scale;
+    if (act)
+        for (int e = tid; e < 1024; e += 256) Ys[(e >> 5) * LD + (e & 31)] *= is;
+    __syncthreads();
+    auto prod = [&](const double *A, const double *B) {
+        d4_t m = {0.0, 0.0, 0.0, 0.0};
+#pragma unroll
+        for (int K = 0; K < 2; ++K)
+#pragma unroll
+            for (int k = 0; k < 4; ++k)
+                m = mfma16(A[(16 * I + c) * LD + 16 * K + 4 * q + k], B[(16 * K + 4 * q + k) * LD + 16 * J + c], m);
+        return m;
+    };
+    double prev = 1e300;
+    for (int it = 0; it < kNsMax; ++it) {
+        if (act) {
+            const d4_t m = prod(Zs, Ys);  // M = Z Y
+            double e = 0.0;
+#pragma unroll
+            for (int r = 0; r < 4; ++r) {
+                const bool d = 16 * I + q + 4 * r == 16 * J + c;
+                e = fmax(e, fabs(m[r] - (d ? 1.0 : 0.0)));
+                Ts[(16 * I + q + 4 * r) * LD + 16 * J + c] = (d ? 1.5 : 0.0) - 0.5 * m[r];
+            }
+#pragma unroll
+            for (int o = 32; o > 0; o >>= 1) e = fmax(e, __shfl_xor(e, o, 64));
+            if (lane == 0) red[w] = e;
+        }
+        __syncthreads();
+        const double e = fmax(fmax(red[0], red[1]), fmax(red[2], red[3]));
+        if (!(e < 1e3)) return false;  // diverging, or NaN (uniform)
+        if (e <= 3e-14 || (e < 1e-10 && e >= 0.5 * prev)) {  // at the rounding floor
+            // and only for kappa(G) <= kNsKappa (sqrtm_ns16: |Z|_F^2 >= kappa(G))
+            double z2 = 0.0;
+            if (act) {
+                for (int x = tid; x < 1024; x += 256) {
+                    const double z = Zs[(x >> 5) * LD + (x & 31)];
+                    z2 = fma(z, z, z2);
+                }
+#pragma unroll
+                for (int o = 32; o > 0; o >>= 1) z2 += __shfl_xor(z2, o, 64);
+                if (lane == 0) red[4 + w] = z2;
+            }
+            __syncthreads();
+            return (red[4] + red[5]) + (red[6] + red[7]) <= kNsKappa;
+        }
+        prev = e;
+        d4_t y = {0.0, 0.0, 0.0, 0.0}, z = {0.0, 0.0, 0.0, 0.0};
+        if (act) {
+            y = prod(Ys, Ts);  // Y T
+            z = prod(Ts, Zs);  // T Z
+        }
+        __syncthreads();  // every read of Y, Z, T done
+        if (act) {
+#pragma unroll
+            for (int r = 0; r < 4; ++r) {
+                Ys[(16 * I + q + 4 * r) * LD + 16 * J + c] = y[r];
+                Zs[(16 * I + q + 4 * r) * LD + 16 * J + c] = z[r];
+            }
+        }
+        __syncthreads();
+    }
+    return false;
+}
+
+// beta = |G|_F^{1/2} sym(Y), beta^-1 = sym(Z) / |G|_F^{1/2} from sqrtm_ns32
+// (every thread of the workgroup calls it), stored as sqrtm_tail stores the
+// Jacobi route's: beta / binv (global, T), g <- beta when L (LB = L beta).
+template <typename T>
+__device__ void sqrtm_ns32_tail(const double *Ys, const double *Zs, double scale, double *g, T *beta, T *binv,
+                                const T *L, T *LB, int tid)
+{
+    constexpr int LD = 33;
+    const double rs = sqrt(scale), irs = 1.0 / rs;
+    for (int e = tid; e < 1024; e += blockDim.x) {
+        const int i = e >> 5, j = e & 31;
+        const double b = (0.5 * (Ys[i * LD + j] + Ys[j * LD + i])) * rs;
+        const double bi = (0.5 * (Zs[i * LD + j] + Zs[j * LD + i])) * irs;
+        if (beta) beta[e] = (T)b;
+        if (binv) binv[e] = (T)bi;
+        if (L) g[e] = b;  // g (the Gram) is dead: park beta for LB
+    }
+    if (L) {
+        __syncthreads();
+        for (int e = tid; e < 1024; e += blockDim.x) {
+            const int i = e >> 5, j = e & 31;
+            double s = 0.0;
+#pragma unroll 4
+            for (int kk = 0; kk < 32; ++kk) s = fma((double)L[i * 32 + kk], g[kk * 32 + j], s);
+            LB[e] = (T)s;
+        }
+    }
+}
+
 }  // namespace lz

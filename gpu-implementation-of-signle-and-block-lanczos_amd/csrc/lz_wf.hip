@@ -172,7 +172,10 @@ __device__ __forceinline__ double dpp_swap1(double x)
 // per-strip window of kWinRows rows (the plan proved every column inside);
 // SW: pass 2 also stores V_j's rows into Vsave (over V_{j-1}, read earlier by
 // the same wave), so V_{j+1} can take V_j's place in the all-gather slot.
-template <int NC, int CAP, int K, int NL, int NU, int DU, bool C16, bool SW = false>
+// GEN: the general form above; false: the one-GPU solve's launch (pass 2 over
+// every tile, xoff = 0, the whole gather source below 2^24 rows, no SW), whose
+// range arithmetic then folds away at compile time.
+template <int NC, int CAP, int K, int NL, int NU, int DU, bool C16, bool SW = false, bool GEN = true>
 __global__ __launch_bounds__(64 * (NC + NL + NU)) void k_wf16(
     int64_t n, const int64_t *__restrict__ rp, const int32_t *__restrict__ col, const int16_t *__restrict__ col16,
     const double *__restrict__ val, const uint64_t *__restrict__ pairs, const double *Yj, const double *Vprev,
@@ -204,6 +207,13 @@ __global__ __launch_bounds__(64 * (NC + NL + NU)) void k_wf16(
     }
     __syncthreads();  // the only block barrier
     const int64_t T = ceil_div(n, (int64_t)TR);
+    static_assert(GEN || !SW, "SW stores are a distributed form");
+    if constexpr (!GEN) {  // the host launches this form only for these values
+        xoff = 0;
+        q0 = 0;
+        q1 = q2 = q3 = T;
+        nx = n;
+    }
     if (T != Th || blockDim.x != 64 * (NC + NL + NU)) {
         // the host planned other tiles (flags, ranges) or launched another
         // block shape (waves past the roles would index past the tile): refuse loudly
@@ -220,7 +230,10 @@ __global__ __launch_bounds__(64 * (NC + NL + NU)) void k_wf16(
     // else q2 + v - nq1; region bounds pbeg / pend are virtual)
     int64_t begin, end, kb, KB, pbeg, pend;
     const int64_t NP1 = p1b - p1a, nq1 = q1 - q0, NQ = nq1 + (q3 - q2);
-    auto ptile = [&](int64_t v) { return v < nq1 ? q0 + v : q2 + (v - nq1); };
+    auto ptile = [&](int64_t v) {
+        if constexpr (!GEN) return v;
+        return v < nq1 ? q0 + v : q2 + (v - nq1);
+    };
     auto clampq = [&](int64_t v) { return v < 0 ? (int64_t)0 : (v > NQ ? NQ : v); };
     if (G < 8) {
         begin = p1a; end = p1b; kb = bid; KB = G; pbeg = 0; pend = NQ;
@@ -525,7 +538,7 @@ __global__ __launch_bounds__(64 * (NC + NL + NU)) void k_wf16(
     // the gather source through a buffer resource: all of it below 2^24 rows,
     // else a window of kWinRows rows centred on the strip's own row (wb: the
     // window's first row; the plan proved every column inside it)
-    const bool win = nx >= kWinRows;
+    const bool win = GEN && nx >= kWinRows;
     auto xwin = [&](int64_t s0, int64_t &wb) {
         const int64_t c = xoff + s0 - kWinRows / 2;
         wb = win ? (c > 0 ? c : 0) : 0;
@@ -873,13 +886,26 @@ int wf_step16(lz_handle *h, int64_t n, const int64_t *rp, const int32_t *col, co
     constexpr int cap12 = 12 * 16 * kWfCapPerRow, cap11 = 11 * 16 * kWfCapPerRow, cap10 = 10 * 16 * kWfCapPerRow;
     // (the instantiation must match pl.tr: the tile count above is the host's)
     const bool sw = Vsave != nullptr;
+    // the one-GPU solve's launches (every pass-2 tile, whole source, no SW) take
+    // the specialised form (GEN = false) of the default shapes
+    const bool one = !sw && xoff == 0 && nx == n && q0 == 0 && q1 == T && q2 == T && q3 == T;
+#ifdef LZ_WF_GEN_ONLY  // (measurement build: the general form everywhere)
+    const bool spec = false;
+    (void)one;
+#else
+    const bool spec = one;
+#endif
     if (pl.var == 200 && col16 && sw) go(k_wf16<10, kWfWideCap, 2, 1, 3, 1, true, true>, 10 + 1 + 3);
+    else if (pl.var == 200 && col16 && spec) go(k_wf16<10, kWfWideCap, 2, 1, 3, 1, true, false, false>, 10 + 1 + 3);
     else if (pl.var == 200 && col16) go(k_wf16<10, kWfWideCap, 2, 1, 3, 1, true>, 10 + 1 + 3);
     else if (pl.var == 200 && sw) go(k_wf16<10, kWfWideCap, 2, 1, 2, 1, false, true>, 10 + 1 + 2);
+    else if (pl.var == 200 && spec) go(k_wf16<10, kWfWideCap, 2, 1, 2, 1, false, false, false>, 10 + 1 + 2);
     else if (pl.var == 200) go(k_wf16<10, kWfWideCap, 2, 1, 2, 1, false>, 10 + 1 + 2);
     else if (pl.var == 111 && col16 && sw) go(k_wf16<11, cap11, kWfK, 1, 4, 1, true, true>, 11 + 1 + 4);
+    else if (pl.var == 111 && col16 && spec) go(k_wf16<11, cap11, kWfK, 1, 4, 1, true, false, false>, 11 + 1 + 4);
     else if (pl.var == 111 && col16) go(k_wf16<11, cap11, kWfK, 1, 4, 1, true>, 11 + 1 + 4);
     else if (pl.var == 111 && sw) go(k_wf16<11, cap11, kWfK, 1, 4, 1, false, true>, 11 + 1 + 4);
+    else if (pl.var == 111 && spec) go(k_wf16<11, cap11, kWfK, 1, 4, 1, false, false, false>, 11 + 1 + 4);
     else if (pl.var == 111) go(k_wf16<11, cap11, kWfK, 1, 4, 1, false>, 11 + 1 + 4);
     else if (col16) {
         if (pl.nc == 12) go(k_wf16<12, cap12, kWfK, kWfNL, 2, 3, true>, 12 + kWfNL + 2);

@@ -39,6 +39,11 @@ for k in kernels:
         print(f"{k}: no dispatches")
         continue
     avg = {c: sum(x[c] for x in disp) / len(disp) for c in disp[0] if all(c in x for x in disp)}
+    # per-dispatch MFMA MOPs: the launches of the largest count are a solve's
+    # steady-state ones (a wavefront solve's first launch is pass 1 only)
+    mops_d = [x.get("SQ_INSTS_VALU_MFMA_MOPS_F64", 0.0) + x.get("SQ_INSTS_VALU_MFMA_MOPS_F32", 0.0) for x in disp]
+    top = max(mops_d)
+    steady = [x for x, mo in zip(disp, mops_d) if mo >= 0.999 * top]
     busy, grbm = avg.get("SQ_VALU_MFMA_BUSY_CYCLES", 0.0), avg.get("GRBM_GUI_ACTIVE", 0.0)
     mops = avg.get("SQ_INSTS_VALU_MFMA_MOPS_F64", 0.0) + avg.get("SQ_INSTS_VALU_MFMA_MOPS_F32", 0.0)
     cyc = grbm / 8.0
@@ -48,6 +53,12 @@ for k in kernels:
            "counters_avg_per_launch": avg,
            "MfmaUtil_pct": round(100.0 * busy / (cyc * 1024), 3) if cyc else None,
            "mfma_flop_per_launch": int(512 * mops),
+           "mfma_flop_per_steady_launch": int(512 * top),
+           "dispatch_mix": {"dispatches": len(disp), "steady": len(steady),
+                            "mfma_flop_per_dispatch": sorted({int(512 * mo) for mo in mops_d})},
+           "MfmaUtil_pct_steady": round(100.0 * sum(x.get("SQ_VALU_MFMA_BUSY_CYCLES", 0.0) for x in steady) /
+                                        (sum(x.get("GRBM_GUI_ACTIVE", 0.0) for x in steady) / 8.0 * 1024), 3)
+           if steady and all("GRBM_GUI_ACTIVE" in x for x in steady) else None,
            "effective_clock_GHz": round(cyc / avg["_ns"], 3) if avg.get("_ns") else None,
            "achieved_TFLOPs_profiled": round(512 * mops / avg["_ns"] / 1e3, 3) if avg.get("_ns") else None,
            "note": "one --pmc pass (no tracing); MfmaUtil = MFMA busy cycles / (GRBM_GUI_ACTIVE/8 x 1024 SIMDs); "

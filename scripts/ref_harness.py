@@ -112,6 +112,23 @@ be1, bi1 = torch.empty(b, b, **f32), torch.empty(b, b, **f32)
 ms = timed(lambda: h.sqrtm(G, be1, bi1), 50)
 emit("sqrtm 16x16 (+ inverse)", "lanczos_plots.m:120-121", "b=16, fp32", ms, 0.1156, None, None,
      "reference custom kernel 115.6 us, cusolver syevjBatched 76.6 us")
+# both routes of the one-workgroup sqrtm at b = 16 and 32 (round 5: Newton-Schulz on the
+# f64 MFMA by one wave at b = 16, four waves at b = 32; LZ_SQRTM_NS=0: the Jacobi route),
+# on a well-conditioned SPD G (kappa ~ 1e3, inside the Newton-Schulz bound of 4e6)
+for bs in (16, 32):
+    Gd = torch.rand(bs, bs, **f64)
+    Gd = Gd @ Gd.T + 0.05 * bs * torch.eye(bs, **f64)
+    for dt, kw in (("fp64", f64), ("fp32", f32)):
+        Gx = Gd.to(kw["dtype"])
+        bo, bi = torch.empty(bs, bs, **kw), torch.empty(bs, bs, **kw)
+        for route, env in (("Newton-Schulz", "1"), ("Jacobi", "0")):
+            os.environ["LZ_SQRTM_NS"] = env
+            ms = timed(lambda: h.sqrtm(Gx, bo, bi), 50)
+            emit(f"sqrtm {bs}x{bs} (+ inverse), {route}", "lanczos_plots.m:120-121; utils/lib_utils.hpp:696-745",
+                 f"b={bs}, {dt}, kappa(G)={float(torch.linalg.cond(Gd)):.1e}", ms,
+                 0.1156 if bs == 16 else None, None, None,
+                 "the reference publishes b = 16 only (custom kernel 115.6 us, syevjBatched 76.6 us)")
+        os.environ.pop("LZ_SQRTM_NS", None)
 
 # ---- structured C3 companion: Yee N=120, fp64, b=16, fused iteration
 A = lz.matrix_a(120)

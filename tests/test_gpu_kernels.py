@@ -311,6 +311,41 @@ def test_spmm_fixed_nnz_tiles(lz, orc, handle, torch_cuda, monkeypatch, n, npr, 
     assert np.allclose(Y.cpu().numpy(), ref, rtol=tol, atol=tol * np.abs(ref).max())
 
 
+@pytest.mark.parametrize("dtype", [np.float64, np.float32])
+@pytest.mark.parametrize("cond", [1.0, 1e2, 1e4, 1e6, 1e8, 1e10, -1.0])
+def test_sqrtm_b32_newton_schulz(lz, orc, handle, torch_cuda, monkeypatch, cond, dtype):
+    """b = 32 (config C5's block): the Newton-Schulz route on the f64 MFMA by four
+    waves (lz_sqrtm.hpp sqrtm_ns32) where |Z|_F^2 bounds kappa(G) by 4e6, the
+    one-wave Jacobi route past it and for an indefinite G -- both against the
+    oracle's eigendecomposition sqrtm (utils/lib_utils.hpp:696-745) and against
+    each other (LZ_SQRTM_NS=0: Jacobi always)."""
+    torch = torch_cuda
+    b = 32
+    rng = np.random.default_rng(int(abs(cond)) % 1000 + 7)
+    Q, _ = np.linalg.qr(rng.standard_normal((b, b)))
+    ev = 3.0 * np.power(abs(cond), -np.arange(b) / (b - 1))
+    if cond < 0:
+        ev[[2, 17]] *= -1.0
+    G = (Q * ev) @ Q.T
+    G = (0.5 * (G + G.T)).astype(dtype)
+    s, si = orc.sqrtm_pair(G.astype(np.float64))
+    tdt = torch.float64 if dtype == np.float64 else torch.float32
+    out = {}
+    for ns in ("1", "0"):
+        monkeypatch.setenv("LZ_SQRTM_NS", ns)
+        beta = torch.empty(b, b, dtype=tdt, device="cuda")
+        binv = torch.empty_like(beta)
+        handle.sqrtm(torch.from_numpy(G).cuda(), beta, binv)
+        out[ns] = (beta.cpu().numpy().astype(np.float64), binv.cpu().numpy().astype(np.float64))
+    kap = abs(cond)
+    floor = 1e-12 if dtype == np.float64 else 2e-6
+    for ns, (bg, big) in out.items():
+        assert np.max(np.abs(bg - s)) <= max(floor, 1e-16 * kap ** 0.5) * np.abs(s).max(), ns
+        assert np.max(np.abs(big - si)) <= max(floor, 1e-16 * kap) * np.abs(si).max(), ns
+    if kap >= 1e7:  # past the kappa bound both take the Jacobi route: the same bits
+        assert np.array_equal(out["1"][0], out["0"][0]) and np.array_equal(out["1"][1], out["0"][1])
+
+
 @pytest.mark.parametrize("cond", [1.0, 1e2, 1e4, 1e6, 1e8, 1e10, -1.0])
 def test_sqrtm_b16_newton_schulz(lz, orc, handle, torch_cuda, monkeypatch, cond):
     """b = 16 without eigenvalues asked for: the Newton-Schulz route (lz_sqrtm.hpp
