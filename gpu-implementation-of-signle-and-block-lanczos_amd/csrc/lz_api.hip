@@ -1142,15 +1142,19 @@ static int init_handle(lz_handle *h, int device)
     LZ_HIP_TRY(hipMalloc(&h->partials2, sizeof(double) * (256 * kMaxB * kMaxB + 4096 * 256)));
     LZ_HIP_TRY(hipMalloc(&h->scratch, sizeof(double) * 8 * kMaxB * kMaxB));
     LZ_HIP_TRY(hipMalloc(&h->err_flag, 64));
-    LZ_HIP_TRY(hipMemset(h->err_flag, 0, 64));
+    // (every fill below is stream-ordered and waited for here: later work runs
+    // on whatever stream lz_set_stream names, which need not order against the
+    // null stream a plain hipMemset uses)
+    LZ_HIP_TRY(hipMemsetAsync(h->err_flag, 0, 64, h->stream));
     LZ_HIP_TRY(hipStreamCreateWithFlags(&h->side, hipStreamNonBlocking));
     LZ_HIP_TRY(hipEventCreateWithFlags(&h->ev_fork, hipEventDisableTiming));
     LZ_HIP_TRY(hipEventCreateWithFlags(&h->ev_join, hipEventDisableTiming));
     if (const char *pz = getenv("LZ_POISON"); pz && pz[0] == '1') {  // test support: NaN-filled workspaces
-        LZ_HIP_TRY(hipMemset(h->partials, 0xFF, sizeof(double) * h->partials_cap));
-        LZ_HIP_TRY(hipMemset(h->partials2, 0xFF, sizeof(double) * (256 * kMaxB * kMaxB + 4096 * 256)));
-        LZ_HIP_TRY(hipMemset(h->scratch, 0xFF, sizeof(double) * 8 * kMaxB * kMaxB));
+        LZ_HIP_TRY(hipMemsetAsync(h->partials, 0xFF, sizeof(double) * h->partials_cap, h->stream));
+        LZ_HIP_TRY(hipMemsetAsync(h->partials2, 0xFF, sizeof(double) * (256 * kMaxB * kMaxB + 4096 * 256), h->stream));
+        LZ_HIP_TRY(hipMemsetAsync(h->scratch, 0xFF, sizeof(double) * 8 * kMaxB * kMaxB, h->stream));
     }
+    LZ_HIP_TRY(hipStreamSynchronize(h->stream));
     return LZ_OK;
 }
 
@@ -1204,9 +1208,11 @@ int lz_finalize(lz_handle *h)
 int lz_device_error(lz_handle *h, int *code)
 {
     LZ_ARG_CHECK(h && code, "null argument");
+    int c = 0;
+    LZ_HIP_TRY(hipMemcpyAsync(&c, h->err_flag, sizeof(int), hipMemcpyDeviceToHost, h->stream));
+    LZ_HIP_TRY(hipMemsetAsync(h->err_flag, 0, sizeof(int), h->stream));
     LZ_HIP_TRY(hipStreamSynchronize(h->stream));
-    LZ_HIP_TRY(hipMemcpy(code, h->err_flag, sizeof(int), hipMemcpyDeviceToHost));
-    LZ_HIP_TRY(hipMemset(h->err_flag, 0, sizeof(int)));
+    *code = c;
     return LZ_OK;
 }
 
@@ -1630,8 +1636,11 @@ static int halo_init_impl(lz_handle *h, int64_t row0, int64_t n_local, const int
     std::vector<int64_t> scnt(nr, 0);
     int rc = LZ_OK;
     do {
-        if (hipMemcpy(dcnt, recv_counts, sizeof(int64_t) * nr, hipMemcpyHostToDevice) != hipSuccess ||
-            hipMemset(dcnt + nr, 0, sizeof(int64_t) * nr) != hipSuccess) {
+        // (stream-ordered: a plain hipMemset / pageable hipMemcpy need not be
+        // done, or ordered, before a non-blocking stream's exchange reads them)
+        if (hipMemcpyAsync(dcnt, recv_counts, sizeof(int64_t) * nr, hipMemcpyHostToDevice, h->stream) != hipSuccess ||
+            hipMemsetAsync(dcnt + nr, 0, sizeof(int64_t) * nr, h->stream) != hipSuccess ||
+            hipStreamSynchronize(h->stream) != hipSuccess) {
             set_error("lz_halo_init: staging counts failed");
             rc = LZ_E_HIP;
             break;
@@ -1642,7 +1651,9 @@ static int halo_init_impl(lz_handle *h, int64_t row0, int64_t n_local, const int
         rc = cm->exchange(ops.data(), (int)ops.size(), h->stream);
         if (rc != LZ_OK) break;
         if (hipStreamSynchronize(h->stream) != hipSuccess ||
-            hipMemcpy(scnt.data(), dcnt + nr, sizeof(int64_t) * nr, hipMemcpyDeviceToHost) != hipSuccess) {
+            hipMemcpyAsync(scnt.data(), dcnt + nr, sizeof(int64_t) * nr, hipMemcpyDeviceToHost, h->stream) !=
+                hipSuccess ||
+            hipStreamSynchronize(h->stream) != hipSuccess) {
             set_error("lz_halo_init: reading counts failed");
             rc = LZ_E_HIP;
         }
@@ -1663,7 +1674,9 @@ static int halo_init_impl(lz_handle *h, int64_t row0, int64_t n_local, const int
     std::vector<int32_t> sidx(hp->n_send);
     do {
         if (hp->n_halo &&
-            hipMemcpy(dreq, halo_rows, sizeof(int32_t) * hp->n_halo, hipMemcpyHostToDevice) != hipSuccess) {
+            (hipMemcpyAsync(dreq, halo_rows, sizeof(int32_t) * hp->n_halo, hipMemcpyHostToDevice, h->stream) !=
+                 hipSuccess ||
+             hipStreamSynchronize(h->stream) != hipSuccess)) {
             set_error("lz_halo_init: staging requests failed");
             rc = LZ_E_HIP;
             break;
@@ -1679,8 +1692,9 @@ static int halo_init_impl(lz_handle *h, int64_t row0, int64_t n_local, const int
         rc = cm->exchange(ops.data(), (int)ops.size(), h->stream);
         if (rc != LZ_OK) break;
         if (hipStreamSynchronize(h->stream) != hipSuccess ||
-            (hp->n_send && hipMemcpy(sidx.data(), hp->send_idx, sizeof(int32_t) * hp->n_send,
-                                     hipMemcpyDeviceToHost) != hipSuccess)) {
+            (hp->n_send && (hipMemcpyAsync(sidx.data(), hp->send_idx, sizeof(int32_t) * hp->n_send,
+                                           hipMemcpyDeviceToHost, h->stream) != hipSuccess ||
+                            hipStreamSynchronize(h->stream) != hipSuccess))) {
             set_error("lz_halo_init: reading requests failed");
             rc = LZ_E_HIP;
         }
@@ -1699,8 +1713,11 @@ static int halo_init_impl(lz_handle *h, int64_t row0, int64_t n_local, const int
         if (2 * g < n_local) hp->send_head = std::max(hp->send_head, g + 1);
         else hp->send_tail = std::min(hp->send_tail, g);
     }
-    if (hp->n_send)
-        LZ_HIP_TRY(hipMemcpy(hp->send_idx, sidx.data(), sizeof(int32_t) * hp->n_send, hipMemcpyHostToDevice));
+    if (hp->n_send) {
+        LZ_HIP_TRY(hipMemcpyAsync(hp->send_idx, sidx.data(), sizeof(int32_t) * hp->n_send, hipMemcpyHostToDevice,
+                                  h->stream));
+        LZ_HIP_TRY(hipStreamSynchronize(h->stream));  // sidx is a local
+    }
     return LZ_OK;
 }
 

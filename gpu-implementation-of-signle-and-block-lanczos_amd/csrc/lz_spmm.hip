@@ -381,6 +381,9 @@ __device__ __forceinline__ Vec<T, VEC> epi_piece(Vec<T, VEC> y, const T *__restr
     return y;
 }
 
+#ifndef LZ_SPMM_F32_UNR
+#define LZ_SPMM_F32_UNR 8
+#endif
 template <typename T, int B, int TR, int CAP, bool WIN, int MODE, bool YCM = false, bool EPI = false>
 __global__ __launch_bounds__(256) void k_spmm_seg(int64_t n, const int64_t *__restrict__ rp,
                                                   const int32_t *__restrict__ col,
@@ -399,7 +402,10 @@ __global__ __launch_bounds__(256) void k_spmm_seg(int64_t n, const int64_t *__re
     //         reproducible).  A row-wise walk would leave one 8-lane group
     //         serialising a 10^5-entry row (power-law degrees, config 5).
     using S = SpmmShape<T, B>;
-    constexpr int VEC = S::VEC, LPR = S::LPR, G = 256 / LPR, UNR = 8;
+    constexpr int VEC = S::VEC, LPR = S::LPR, G = 256 / LPR;
+    // gathers in flight per lane per step: 8 (C3: 16 took 118 VGPRs and ran
+    // slower); the fp32 tile pass takes LZ_SPMM_F32_UNR (a build-time A/B)
+    constexpr int UNR = (MODE == 0 && sizeof(T) == 4) ? LZ_SPMM_F32_UNR : 8;
     static_assert(TR <= 255, "row ids are bytes");
     __shared__ int32_t rel[TR + 1];
     __shared__ int32_t cs[CAP + UNR];
@@ -1143,7 +1149,12 @@ static int launch_seg(lz_handle *h, int64_t n, const int64_t *rp, const int32_t 
         (void)hipFree(h->longq);
         h->longq = nullptr;
         LZ_HIP_TRY(hipMalloc(&h->longq, sizeof(int) * ((size_t)st + 2)));
-        LZ_HIP_TRY(hipMemset(h->longq, 0, 2 * sizeof(int)));  // both count slots
+        // both count slots, on the handle's stream: a plain hipMemset runs on the
+        // null stream, which does not order against a non-blocking stream (a
+        // torch pool stream, a virtual rank's), so the kernels below could read
+        // the fresh allocation's garbage as a queue count (round 5: wrong tiles
+        // recomputed by the long-tile pass, or an illegal address)
+        LZ_HIP_TRY(hipMemsetAsync(h->longq, 0, 2 * sizeof(int), h->stream));
         h->longq_cap = (size_t)st + 2;
         h->longq_parity = 0;
     }

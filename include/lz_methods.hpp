@@ -115,9 +115,16 @@ public:
     {
         if (n) hip_check(hipMalloc(&p_, sizeof(T) * n), "hipMalloc");
     }
+    // The containers' transfers are blocking, as the reference's are: the copy
+    // or fill has landed when the call returns, and a read-back sees every
+    // stream's earlier work (a context may run on a non-blocking stream, which
+    // the null-stream hipMemcpy / hipMemset would not order against).
     DeviceArray(const T *host, size_t n) : DeviceArray(n)
     {
-        if (n) hip_check(hipMemcpy(p_, host, sizeof(T) * n, hipMemcpyHostToDevice), "hipMemcpy H2D");
+        if (n) {
+            hip_check(hipMemcpy(p_, host, sizeof(T) * n, hipMemcpyHostToDevice), "hipMemcpy H2D");
+            hip_check(hipDeviceSynchronize(), "hipDeviceSynchronize");
+        }
     }
     ~DeviceArray() { (void)hipFree(p_); }
     DeviceArray(DeviceArray &&o) noexcept : p_(o.p_), n_(o.n_) { o.p_ = nullptr; o.n_ = 0; }
@@ -135,10 +142,19 @@ public:
     std::vector<T> copy_to_host() const
     {
         std::vector<T> h(n_);
-        if (n_) hip_check(hipMemcpy(h.data(), p_, sizeof(T) * n_, hipMemcpyDeviceToHost), "hipMemcpy D2H");
+        if (n_) {
+            hip_check(hipDeviceSynchronize(), "hipDeviceSynchronize");
+            hip_check(hipMemcpy(h.data(), p_, sizeof(T) * n_, hipMemcpyDeviceToHost), "hipMemcpy D2H");
+        }
         return h;
     }
-    void fill_zero() { if (n_) hip_check(hipMemset(p_, 0, sizeof(T) * n_), "hipMemset"); }
+    void fill_zero()
+    {
+        if (n_) {
+            hip_check(hipMemset(p_, 0, sizeof(T) * n_), "hipMemset");
+            hip_check(hipDeviceSynchronize(), "hipDeviceSynchronize");
+        }
+    }
 
 private:
     T *p_ = nullptr;
