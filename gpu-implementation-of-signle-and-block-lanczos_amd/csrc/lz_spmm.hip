@@ -381,9 +381,6 @@ __device__ __forceinline__ Vec<T, VEC> epi_piece(Vec<T, VEC> y, const T *__restr
     return y;
 }
 
-#ifndef LZ_SPMM_F32_UNR
-#define LZ_SPMM_F32_UNR 8
-#endif
 template <typename T, int B, int TR, int CAP, bool WIN, int MODE, bool YCM = false, bool EPI = false>
 __global__ __launch_bounds__(256) void k_spmm_seg(int64_t n, const int64_t *__restrict__ rp,
                                                   const int32_t *__restrict__ col,
@@ -402,10 +399,10 @@ __global__ __launch_bounds__(256) void k_spmm_seg(int64_t n, const int64_t *__re
     //         reproducible).  A row-wise walk would leave one 8-lane group
     //         serialising a 10^5-entry row (power-law degrees, config 5).
     using S = SpmmShape<T, B>;
-    constexpr int VEC = S::VEC, LPR = S::LPR, G = 256 / LPR;
-    // gathers in flight per lane per step: 8 (C3: 16 took 118 VGPRs and ran
-    // slower); the fp32 tile pass takes LZ_SPMM_F32_UNR (a build-time A/B)
-    constexpr int UNR = (MODE == 0 && sizeof(T) == 4) ? LZ_SPMM_F32_UNR : 8;
+    // UNR: gathers in flight per lane per step.  16 measured slower at both C3
+    // (118 VGPRs, 1.34 vs 1.15 ms) and C5 (124 VGPRs, 4 waves per SIMD: 3.25
+    // vs 2.96 ms, profiles/r05b_c5_unr_ab.log)
+    constexpr int VEC = S::VEC, LPR = S::LPR, G = 256 / LPR, UNR = 8;
     static_assert(TR <= 255, "row ids are bytes");
     __shared__ int32_t rel[TR + 1];
     __shared__ int32_t cs[CAP + UNR];

@@ -12,6 +12,7 @@ mkdir -p $O
 timeout -k 10 900 python -u -m pytest tests -m gpu -x -q --timeout 300 --timeout-method thread -p no:cacheprovider > $O/pytest_gpu.log 2>&1 || { tail -40 $O/pytest_gpu.log; exit 1; }
 tail -2 $O/pytest_gpu.log
 bash scripts/gpu_lib_ab.sh $T/fs1 "--steps 20" cur genonly || exit 1
+AB_SCRIPT=ab_c5.py bash scripts/gpu_lib_ab.sh $T/c5unr "--steps 10" cur unr16 || exit 1
 timeout -k 10 400 python -u scripts/ab_c5.py "LZ_SQRTM_NS=1" "LZ_SQRTM_NS=0" --rounds 3 --steps 10 > $O/c5_ns_ab.log 2>&1 || { tail -20 $O/c5_ns_ab.log; exit 1; }
 tail -12 $O/c5_ns_ab.log
 timeout -k 10 400 python -u scripts/ref_harness.py > $O/ref_harness.json 2> $O/ref_harness.err || { tail -20 $O/ref_harness.err; exit 1; }
