@@ -781,6 +781,15 @@ def main():
                             "pmc_mfma_flop_per_launch": d.get("mfma_flop_per_launch"),
                             "pmc_mfma_flop_per_steady_launch": d.get("mfma_flop_per_steady_launch"),
                             "pmc_dispatch_mix": d.get("dispatch_mix"), "pmc_source": src})
+                # MfmaUtil is busy / elapsed cycles at the profiled run's clock; the FLOP
+                # fraction above is against the 2.4 GHz peak: the same quantity is
+                # MfmaUtil x (profiled clock / 2.4 GHz)
+                clk = d.get("effective_clock_GHz")
+                if clk and d.get("MfmaUtil_pct") is not None:
+                    ent["pmc_frac_at_peak_clock"] = round(d["MfmaUtil_pct"] / 100.0 * clk / 2.4, 4)
+                    ent["pmc_note"] = (f"profiled clock {clk} GHz; MfmaUtil {d['MfmaUtil_pct']} % of the SIMD cycles "
+                                       f"= {ent['pmc_frac_at_peak_clock']} of the 2.4 GHz peak, against frac {ent['frac']} "
+                                       f"from the model FLOP and this run's kernel time")
             else:
                 ent["pmc_note"] = src
             mfma = {"unit": "TFLOP/s", "peak": FP64_MFMA_PEAK_TFS, "dtype": "f64 (v_mfma_f64_16x16x4f64)",
