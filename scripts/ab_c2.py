@@ -3,7 +3,7 @@ half width 4096, fp64): configurations (environment variables read per call)
 alternated over rounds, microseconds per step of an m-step solve, alpha / beta
 checked against the first configuration.
 
-  python scripts/ab_c2.py "LZ_VL_WF=1" "LZ_VL_WF=0" [--rounds 4] [--steps 200]
+  python scripts/ab_c2.py "LZ_VL_KERNEL=win1024" "LZ_VL_KERNEL=row" [--rounds 4] [--steps 200]
 """
 import argparse
 import json

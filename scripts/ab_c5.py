@@ -3,7 +3,7 @@ configurations (environment variables read per call) alternated over rounds,
 ms per block step of an m-step solve and the SpMM class time, alpha checked
 against the first configuration (fp32: 1e-4 relative).
 
-  python scripts/ab_c5.py "LZ_C5_TILE=48" "LZ_C5_TILE=96" [--rounds 3] [--steps 10]
+  python scripts/ab_c5.py "LZ_C5_B2=1" "LZ_C5_B2=0" [--rounds 3] [--steps 10]
 """
 import argparse
 import json
