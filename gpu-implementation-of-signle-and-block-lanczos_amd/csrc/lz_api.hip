@@ -168,9 +168,12 @@ static int block_lanczos_unfused(lz_handle *h, int64_t n, int64_t nnz, const int
 // 16 x 16 products: Q_{j-1} beta_j = W_{j-1} (beta_{j-1}^-1 beta_j) in pass 1,
 // Q_j alpha_j = W_j (beta_j^-1 alpha_j) in pass 2), so no pass writes or reads
 // Q: A + 6 n b s bytes per step instead of A + 7 n b s.  Residual buffers:
-// W_0 = B (read only); step j's output W' -> W'' goes to W at j = 0, Q1 at
+// W_0 = B (read only); step j's output W' -> W'' goes to r0 at j = 0, r1 at
 // j = 1 and from then on in place over W_{j-1} (row r read, then written, by
-// the same wave).  The inverse square roots of two consecutive steps live in
+// the same wave).  residual_order: {r0, r1} = {W, Q1} for odd m, {Q1, W} for
+// even m, so the last residual W_m is written into W itself and the post-call
+// pass only forms Q0 = Q1 = W_{m-1} beta^-1 (in place over W_{m-1}, in Q1) --
+// copying W_m over from Q1 cost C5's 10-step solve 2.56 GB.  The inverse square roots of two consecutive steps live in
 // two scratch slots; beta[m] gets the last one, as the reference's.
 // Once-per-solve set-up of pass 1: the strips' row orders and, for a gather
 // source of 2^24+ rows, whether the windowed kernel applies.
@@ -302,8 +305,9 @@ static int block_lanczos_fused16(lz_handle *h, int64_t n, int64_t nnz, const int
     LZ_HIP_TRY(hipStreamWaitEvent(h->stream, h->ev_join, 0));
     LZ_TRY(sqrtm_pair<double>(h, 16, nullptr, P, beta, qb.binv[0], nullptr));
     const double *in = B, *prev = nullptr;
+    double *r0 = (m & 1) ? W : Q1, *r1 = (m & 1) ? Q1 : W;  // W_m lands in W (residual_order)
     for (int j = 0; j < m; ++j) {
-        double *out = j == 0 ? W : j == 1 ? Q1 : const_cast<double *>(prev);
+        double *out = j == 0 ? r0 : j == 1 ? r1 : const_cast<double *>(prev);
         const double *bi = qb.binv[j & 1];
         LZ_TRY(fused_spmm16(h, n, rp, col, val, in, n, in, prev, out, bi, j ? qb.P : nullptr, lc, q + j * 16, &P,
                             pl.pairs, nnz, 0, pl.win, 0, pl.col16));
@@ -331,7 +335,8 @@ static int block_lanczos_fused16(lz_handle *h, int64_t n, int64_t nnz, const int
 // that power-law rows need) writing Y into the API's Q0 buffer, then pass E
 // and pass U: A + 9 n b s bytes per step against the reference order's
 // A + 13 n b s.  The residual buffers rotate as in block_lanczos_fused16
-// (B = W_0 read only, then W, Q1, in place).
+// (B = W_0 read only, then r0, r1 -- W and Q1 in the order residual_order
+// picks -- then in place).
 // The b = 32 fp32 step in its beta^2 form (default; LZ_C5_B2=0 selects the
 // pass-E form below): the SpMM's
 // epilogue stores U = W' beta_j = A W_j - W_{j-1} M_j with M_j =
@@ -352,8 +357,9 @@ static int block_lanczos_b2_32(lz_handle *h, int64_t n, int64_t nnz, const int64
     LZ_TRY(gram_partials<float>(h, n, b, B, B, b, &np));
     LZ_TRY(sqrtm_pair<float>(h, b, nullptr, np, beta, binv[0], nullptr));
     const float *in = B, *prev = nullptr;
+    float *r0 = (m & 1) ? W : Q1, *r1 = (m & 1) ? Q1 : W;  // W_m lands in W (residual_order)
     for (int j = 0; j < m; ++j) {
-        float *out = j == 0 ? W : j == 1 ? Q1 : const_cast<float *>(prev);
+        float *out = j == 0 ? r0 : j == 1 ? r1 : const_cast<float *>(prev);
         const float *bi = binv[j & 1];
         LZ_TRY(spmm_rm_b2(h, n, nnz, rp, col, val, in, n, U, prev, j ? M : nullptr));
         if (j > 0) LZ_HIP_TRY(hipStreamWaitEvent(h->stream, h->ev_join, 0));
@@ -405,8 +411,9 @@ static int block_lanczos_sep(lz_handle *h, int64_t n, int64_t nnz, const int64_t
     LZ_TRY(gram_partials<T>(h, n, b, B, B, b, &np));
     LZ_TRY(sqrtm_pair<T>(h, b, nullptr, np, beta, binv[0], nullptr));
     const T *in = B, *prev = nullptr;
+    T *r0 = (m & 1) ? W : Q1, *r1 = (m & 1) ? Q1 : W;  // W_m lands in W (residual_order)
     for (int j = 0; j < m; ++j) {
-        T *out = j == 0 ? W : j == 1 ? Q1 : const_cast<T *>(prev);
+        T *out = j == 0 ? r0 : j == 1 ? r1 : const_cast<T *>(prev);
         const T *bi = binv[j & 1];
         // the SpMM gathers the unnormalised W_j: it needs no beta, so step j-1's
         // sqrtm runs beside it on the side stream; pass E waits for it

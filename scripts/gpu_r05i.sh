@@ -1,6 +1,6 @@
 #!/bin/bash
-# Round 5: the post-call state pass with 16-B stores and strip_pairs before the
-# plan's host sync -- parity tests and a kernel-trace profile of the default bench.
+# Round 5: kernel-level changes -- parity tests (plan, Lanczos paths) and a
+# kernel-trace profile of the default bench.
 cd "$GRAFT_REPO_ROOT" || exit 1
 export TMPDIR=/tmp
 R=$PWD
