@@ -284,6 +284,19 @@ def test_block_c3_full_size(lz, orc, handle, torch_cuda):
     assert_close_run(lz, m, 16, got, orc.block_lanczos(A, B, m, lc))
 
 
+def test_block_c5_full_size(lz, orc, handle, torch_cuda):
+    """BASELINE config C5 at full size (the bench operator: n = 1e7 power-law
+    rows, alpha 2.1, rows up to 1e5, ~9.9e7 nnz; b = 32 fp32, the beta^2 form
+    with the long-tile queue): alpha, beta, q and the Ritz values against the
+    fp32 oracle (methods/block_lanczos.hpp:104-166) to 1e-4 relative."""
+    A = lz.gen_powerlaw(10_000_000, 10.0, 2.1, 100000, seed=20261015, dtype=np.float32)
+    B = lz.uniform_B(A.n, 32, seed=20261015, dtype=np.float32)
+    m, lc = 4, 9_999_991
+    got = gpu_block(lz, handle, torch_cuda, A, B, m, lc)
+    assert handle.device_error() == 0
+    _f32_checks(lz, m, 32, got, orc.block_lanczos(A, B, m, lc), F32_RTOL)
+
+
 def test_block_b16_c4_density(lz, orc, handle, torch_cuda):
     """C4's row density (25 nnz/row, half-width 2^16) at small n: pass 1's
     10-consumer / 4400-entry shape and the SpMM's 1536-entry stage."""
