@@ -105,6 +105,10 @@ struct lz_handle {
     int *longq = nullptr;         // k_spmm_seg long-tile queue: [0], [1] counts (alternate calls), [2..] tile ids
     size_t longq_cap = 0;         // ints
     int longq_parity = 0;         // the count slot of the next call
+    // the long-tile pass of a planned SpMM (the list an earlier call of the
+    // same solve queued) runs on its own stream beside the tile pass
+    hipStream_t lstream = nullptr;
+    hipEvent_t ev_lfork = nullptr, ev_ljoin = nullptr;
     size_t pairs_cap = 0;         // entries
     void *cm_buf = nullptr;       // column-major SpMM: row-major copies of X and Y
     size_t cm_cap = 0;            // bytes

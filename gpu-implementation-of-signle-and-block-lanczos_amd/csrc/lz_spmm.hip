@@ -438,9 +438,12 @@ __global__ __launch_bounds__(256) void k_spmm_seg(int64_t n, const int64_t *__re
             }
         };
         // this launch's count slot; the other slot is zeroed for the next launch
-        // (no memset per call: the queue counts alternate between longq[0] / [1])
-        const int cnt = longq[parity];
-        if (blockIdx.x == 0 && threadIdx.x == 0) longq[parity ^ 1] = 0;
+        // (no memset per call: the queue counts alternate between longq[0] / [1]).
+        // parity 2 / 3: a planned launch -- the list an earlier call queued
+        // (count at longq[parity - 2]), left as it is for the next planned call
+        const bool planned = parity >= 2;
+        const int cnt = longq[planned ? parity - 2 : parity];
+        if (!planned && blockIdx.x == 0 && threadIdx.x == 0) longq[parity ^ 1] = 0;
         for (int qi = blockIdx.x; qi < cnt; qi += gridDim.x) {
             const int64_t r0 = (int64_t)longq[2 + qi] * TR;
             const int nrows = (int)((n - r0) < TR ? (n - r0) : TR);
@@ -559,8 +562,8 @@ __global__ __launch_bounds__(256) void k_spmm_seg(int64_t n, const int64_t *__re
         }
     }
     const int64_t N64 = rp[r0 + nrows] - kA;
-    if (N64 > CAP) {  // block-uniform
-        if (tid == 0) longq[2 + atomicAdd(&longq[parity], 1)] = (int)(r0 / TR);
+    if (N64 > CAP) {  // block-uniform (planned: the listed tile runs in the long-tile pass)
+        if (tid == 0 && parity < 2) longq[2 + atomicAdd(&longq[parity], 1)] = (int)(r0 / TR);
         return;
     }
     const int N = (int)N64;
@@ -652,7 +655,7 @@ __global__ __launch_bounds__(256) void k_spmm_seg(int64_t n, const int64_t *__re
         const int64_t lo = N > 0 ? cmin : 0, span = N > 0 ? (int64_t)cmax - cmin + 1 : 0;
         const int64_t wrows = (int64_t)(0x7fffffff / rowb) < kWinRows ? (int64_t)(0x7fffffff / rowb) : kWinRows;
         if (span > wrows) {  // block-uniform: columns too far apart for one window
-            if (tid == 0) longq[2 + atomicAdd(&longq[parity], 1)] = (int)(r0 / TR);
+            if (tid == 0 && parity < 2) longq[2 + atomicAdd(&longq[parity], 1)] = (int)(r0 / TR);
             return;
         }
         wb = (uint32_t)lo;
@@ -1135,9 +1138,13 @@ static int launch_fnz(lz_handle *h, int64_t nnz, const T *val, const T *X, int64
 
 // nnz-split SpMM with the long-tile queue: the main kernel, then a persistent
 // kernel over the queued tiles (an empty queue costs one short launch).
+// plan_slot >= 0: the long tiles an earlier call on the same operator queued
+// (count slot plan_slot, *slot_out of that call) -- the long-tile pass runs
+// first, on its own stream, beside the main kernel, which then only skips them.
 template <typename T, int B, int TR, int CAP, bool WIN, bool YCM = false, bool EPI = false>
 static int launch_seg(lz_handle *h, int64_t n, const int64_t *rp, const int32_t *col, const T *val, const T *X,
-                      int64_t ldx, int64_t nx, T *Y, int64_t ldy, const T *Wp = nullptr, const T *Mm = nullptr)
+                      int64_t ldx, int64_t nx, T *Y, int64_t ldy, const T *Wp = nullptr, const T *Mm = nullptr,
+                      int plan_slot = -1, int *slot_out = nullptr)
 {
     const int64_t st = ceil_div(n, (int64_t)TR);
     LZ_ARG_CHECK(st < (1LL << 31), "too many row tiles");
@@ -1155,8 +1162,27 @@ static int launch_seg(lz_handle *h, int64_t n, const int64_t *rp, const int32_t 
         h->longq_cap = (size_t)st + 2;
         h->longq_parity = 0;
     }
+    if (plan_slot >= 0) {
+        LZ_ARG_CHECK(plan_slot <= 1 && (size_t)st + 2 <= h->longq_cap, "planned SpMM: no earlier queue");
+        if (!h->lstream) {
+            LZ_HIP_TRY(hipStreamCreateWithFlags(&h->lstream, hipStreamNonBlocking));
+            LZ_HIP_TRY(hipEventCreateWithFlags(&h->ev_lfork, hipEventDisableTiming));
+            LZ_HIP_TRY(hipEventCreateWithFlags(&h->ev_ljoin, hipEventDisableTiming));
+        }
+        const int g2 = (int)std::max<int64_t>(1, std::min<int64_t>(st, (int64_t)h->n_cu * 4));
+        LZ_HIP_TRY(hipEventRecord(h->ev_lfork, h->stream));
+        LZ_HIP_TRY(hipStreamWaitEvent(h->lstream, h->ev_lfork, 0));
+        hipLaunchKernelGGL((k_spmm_seg<T, B, TR, CAP, WIN, 1, YCM, EPI>), dim3(g2), dim3(256), 0, h->lstream, n, rp,
+                           col, val, X, ldx, nx, Y, ldy, h->longq, 2 + plan_slot, Wp, Mm, 0);
+        LZ_HIP_TRY(hipEventRecord(h->ev_ljoin, h->lstream));
+        hipLaunchKernelGGL((k_spmm_seg<T, B, TR, CAP, WIN, 0, YCM, EPI>), dim3((unsigned)st), dim3(256), 0, h->stream,
+                           n, rp, col, val, X, ldx, nx, Y, ldy, h->longq, 2 + plan_slot, Wp, Mm, 0);
+        LZ_HIP_TRY(hipStreamWaitEvent(h->stream, h->ev_ljoin, 0));
+        return LZ_OK;
+    }
     const int parity = h->longq_parity;
     h->longq_parity ^= 1;
+    if (slot_out) *slot_out = parity;
     // diag: measurement only (results wrong), in a -DLZ_DIAG build alone:
     // LZ_SPMM_DIAG = tiles mod this (every input L2-resident, DESIGN.md 4
     // SpMM); LZ_SPMM_DIAG_Y=1: the Y tiles stay the blocks' own.  The shipped
@@ -1242,12 +1268,13 @@ bool spmm_b2_ok(int64_t n, int64_t nnz, int64_t nx)
 }
 
 int spmm_rm_b2(lz_handle *h, int64_t n, int64_t nnz, const int64_t *rp, const int32_t *col, const float *val,
-               const float *X, int64_t nx, float *Y, const float *Wp, const float *Mm)
+               const float *X, int64_t nx, float *Y, const float *Wp, const float *Mm, int plan_slot, int *slot_out)
 {
     LZ_ARG_CHECK(spmm_b2_ok(n, nnz, nx), "beta^2 SpMM epilogue: shape not covered");
     if (n <= 0) return LZ_OK;
     const int ev = prof_begin(h, PROF_SPMM);
-    const int rc = launch_seg<float, 32, 48, 768, false, false, true>(h, n, rp, col, val, X, 32, nx, Y, 32, Wp, Mm);
+    const int rc = launch_seg<float, 32, 48, 768, false, false, true>(h, n, rp, col, val, X, 32, nx, Y, 32, Wp, Mm,
+                                                                      plan_slot, slot_out);
     prof_end(h, ev);
     LZ_TRY(rc);
     LZ_LAUNCH_CHECK();
