@@ -462,8 +462,9 @@ __global__ __launch_bounds__(256) void k_spmm_seg(int64_t n, const int64_t *__re
                 const int Nc = (int)(c1 - c0), cb = (int)(c0 - kA);  // chunk length, offset in the run
                 __syncthreads();  // rel visible; the previous chunk is done with cs / vs / rid / head
                 for (int k = tid; k < Nc; k += 256) {
-                    cs[k] = col[c0 + k];
-                    vs[k] = val[c0 + k];
+                    // (streamed once: non-temporal, as the tile pass's staging)
+                    cs[k] = __builtin_nontemporal_load(&col[c0 + k]);
+                    vs[k] = __builtin_nontemporal_load(&val[c0 + k]);
                     int lo = 0, hi = nrows - 1;  // the row holding entry cb + k: rel[r] <= cb + k < rel[r + 1]
                     while (lo < hi) {
                         const int mid = (lo + hi + 1) >> 1;

@@ -1,7 +1,7 @@
 #!/bin/bash
-# Round 5: non-temporal W_{j-1} loads in the C5 SpMM epilogue -- library A/B
-# on the C5 step (cur: nt loads; epiplain: plain loads).
+# Round 5: C5 library A/Bs (non-temporal stream loads):
+#   bash scripts/gpu_r05o.sh TAG lib1 lib2 ...
 cd "$GRAFT_REPO_ROOT" || exit 1
 export TMPDIR=/tmp
-mkdir -p gpurun_out/r05o
-AB_SCRIPT=ab_c5.py bash scripts/gpu_lib_ab.sh r05o/ab "--steps 10" cur epiplain || exit 1
+mkdir -p gpurun_out/${1:-r05o}
+AB_SCRIPT=ab_c5.py bash scripts/gpu_lib_ab.sh ${1:-r05o}/ab "--steps 10" ${@:2} || exit 1
