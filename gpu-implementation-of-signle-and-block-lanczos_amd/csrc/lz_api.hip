@@ -363,7 +363,7 @@ static int block_lanczos_b2_32(lz_handle *h, int64_t n, int64_t nnz, const int64
         float *out = j == 0 ? r0 : j == 1 ? r1 : const_cast<float *>(prev);
         const float *bi = binv[j & 1];
         // from step 1 on the long-tile pass runs beside the tile pass, over the
-        // list step 0 queued (C5 step 4.401-4.411 -> 4.381-4.385 ms, the same bits)
+        // list step 0 queued (C5 step 4.401-4.411 -> 4.381-4.385 ms, each tile computed as before)
         const int plan = j > 0 ? lslot : -1;
         LZ_TRY(spmm_rm_b2(h, n, nnz, rp, col, val, in, n, U, prev, j ? M : nullptr, plan, j == 0 ? &lslot : nullptr));
         if (j > 0) LZ_HIP_TRY(hipStreamWaitEvent(h->stream, h->ev_join, 0));
