@@ -38,6 +38,9 @@ __device__ __forceinline__ f16v_t mfma32(float a, float b, f16v_t c)
 }
 
 // a[s] = M[row][16 hh + s] for s = 0..15 (zeros past n): four 16-B loads
+// (plain: the two halves of a 128-B row come from two lanes' instructions, so
+// non-temporal loads here fetch each line twice -- C5 pass UB 0.28 ms slower,
+// profiles/r05u_c5_el_ub_nt_ab.log)
 __device__ __forceinline__ void aop32(const float *__restrict__ M, int64_t row, bool ok, int hh, float a[16])
 {
 #pragma unroll
@@ -183,8 +186,11 @@ __global__ __launch_bounds__(64 * kF32Waves) void k_fused_el32(int64_t n, const 
 #pragma unroll
         for (int v = 0; v < 16; ++v) {
             const int64_t rr = r0 + (v & 3) + 8 * (v >> 2) + 4 * hh;
-            wv[v] = rr < n ? Wj[rr * 32 + jr] : 0.0f;
-            uv[v] = rr < n ? U[rr * 32 + jr] : 0.0f;
+            // non-temporal (each instruction reads whole 128-B rows): the
+            // stream leaves the caches to pass UB's rows (C5 step -1 %,
+            // profiles/r05u_c5_el_ub_nt_ab.log)
+            wv[v] = rr < n ? __builtin_nontemporal_load(&Wj[rr * 32 + jr]) : 0.0f;
+            uv[v] = rr < n ? __builtin_nontemporal_load(&U[rr * 32 + jr]) : 0.0f;
         }
 #pragma unroll
         for (int v = 0; v < 16; ++v) g = mfma32(wv[v], uv[v], g);
