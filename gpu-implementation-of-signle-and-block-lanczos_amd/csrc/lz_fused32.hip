@@ -38,9 +38,9 @@ __device__ __forceinline__ f16v_t mfma32(float a, float b, f16v_t c)
 }
 
 // a[s] = M[row][16 hh + s] for s = 0..15 (zeros past n): four 16-B loads
-// (plain: the two halves of a 128-B row come from two lanes' instructions, so
-// non-temporal loads here fetch each line twice -- C5 pass UB 0.28 ms slower,
-// profiles/r05u_c5_el_ub_nt_ab.log)
+// (plain: the two halves of a 128-B row come from two lanes' loads, and with
+// non-temporal loads C5's pass UB took 0.28 ms longer -- presumably each line
+// fetched twice; profiles/r05u_c5_el_ub_nt_ab.log)
 __device__ __forceinline__ void aop32(const float *__restrict__ M, int64_t row, bool ok, int hh, float a[16])
 {
 #pragma unroll
