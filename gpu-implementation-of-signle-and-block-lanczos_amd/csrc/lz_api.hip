@@ -230,13 +230,29 @@ static int block_lanczos_wf16(lz_handle *h, int64_t n, int64_t nnz, const int64_
     double *P1 = h->scratch + 6 * 256, *P2 = h->scratch + 7 * 256;
     double *slab = h->scratch + 8 * 256;  // [S1 | S2 | G], 768
     int P = 0;
-    // B^T B's slabs (Pg of them) were made beside the plan (gram_beside)
-    LZ_TRY(sqrtm_pair<double>(h, 16, nullptr, Pg, beta, binv[0], nullptr));
+    const bool g0 = Pg < 0;  // beta_0's Gram from the first launch (wf_first_gram)
+    // else B^T B's slabs (Pg of them) were made beside the plan (gram_beside)
+    if (!g0) LZ_TRY(sqrtm_pair<double>(h, 16, nullptr, Pg, beta, binv[0], nullptr));
     LZ_TRY(wf_reset16(h, n, wp));
-    // Y_0 = A B, S1_0 = B^T Y_0
-    LZ_TRY(wf_step16(h, n, rp, col, pl.col16, val, pl.pairs, wp, nullptr, nullptr, nullptr, nullptr, nullptr,
-                     nullptr, nullptr, B, Q0, 0, &P));
-    LZ_TRY(alpha_wf16(h, h->partials2, P, binv[0], nullptr, alpha, P2, B, lc, n, q));
+    // Y_0 = A B, S1_0 = B^T Y_0 (g0: and G_0 = B^T B)
+    LZ_TRY(wf_step16(h, n, rp, col, pl.col16, val, pl.pairs, wp, nullptr, nullptr, g0 ? B : nullptr, nullptr,
+                     nullptr, nullptr, nullptr, B, Q0, 0, &P));
+    if (g0) {  // beta_0, its inverse, alpha_0, P2 and q_0 in one kernel, as every later step's
+        WfSlabs sl;
+        sl.add(h->partials2, P);
+        LZ_TRY(wf_fold16(h, sl, slab));
+        WfAlpha wa;
+        wa.part = slab;
+        wa.P = 1;
+        wa.alpha = alpha;
+        wa.P2 = P2;
+        wa.V = B;
+        wa.lc = (lc >= 0 && lc < n) ? lc : -1;
+        wa.qrow = q;
+        LZ_TRY(sqrtm_pair<double>(h, 16, nullptr, 1, beta, binv[0], nullptr, slab + 512, nullptr, nullptr, &wa));
+    } else {
+        LZ_TRY(alpha_wf16(h, h->partials2, P, binv[0], nullptr, alpha, P2, B, lc, n, q));
+    }
     const double *Vm1 = nullptr, *V0 = B;
     for (int j = 0; j + 1 < m; ++j) {
         double *Vn = j == 0 ? W : j == 1 ? Q1 : const_cast<double *>(Vm1);
@@ -281,10 +297,13 @@ static int block_lanczos_fused16(lz_handle *h, int64_t n, int64_t nnz, const int
     QfreeBufs qb(h);
     int P = 0;
     Pass1Plan pl;
-    // B^T B (beta_0's Gram) on the side stream while the once-per-solve plans
-    // (latency-bound passes over the columns, each ending in a host sync) run on
-    // the main one; joined before its sqrtm
-    LZ_TRY(gram_beside(h, n, B, &P));
+    // B^T B (beta_0's Gram): where the wavefront step will run with a shape
+    // whose first launch sums it (wf_first_gram), there; otherwise on the side
+    // stream while the once-per-solve plans (latency-bound passes over the
+    // columns, each ending in a host sync) run on the main one, joined before
+    // its sqrtm
+    const bool g0 = wf_first_gram(n, nnz);
+    if (!g0) LZ_TRY(gram_beside(h, n, B, &P));
     // every return from here on leaves the main stream behind the Gram (an early
     // error return too: the side stream's slabs must not race a later call)
     struct JoinSide {
@@ -297,10 +316,14 @@ static int block_lanczos_fused16(lz_handle *h, int64_t n, int64_t nnz, const int
         if (wp.ok) {
             LZ_TRY(strip_pairs(h, n, rp, &pl.pairs));
             pl.col16 = wp.col16;
-            LZ_HIP_TRY(hipStreamWaitEvent(h->stream, h->ev_join, 0));
-            return block_lanczos_wf16(h, n, nnz, rp, col, val, m, lc, B, q, alpha, beta, Q0, Q1, W, pl, wp, P);
+            if (!g0) LZ_HIP_TRY(hipStreamWaitEvent(h->stream, h->ev_join, 0));
+            else if (wp.var == 200) LZ_TRY(gram_partials<double>(h, n, 16, B, B, 16, &P));  // (the wide shape)
+            const bool first = g0 && wp.var != 200;
+            return block_lanczos_wf16(h, n, nnz, rp, col, val, m, lc, B, q, alpha, beta, Q0, Q1, W, pl, wp,
+                                      first ? -1 : P);
         }
     }
+    if (g0) LZ_TRY(gram_partials<double>(h, n, 16, B, B, 16, &P));  // (the plan refused the wavefront)
     LZ_TRY(pass1_plan(h, n, nnz, rp, col, n, 0, &pl));
     LZ_HIP_TRY(hipStreamWaitEvent(h->stream, h->ev_join, 0));
     LZ_TRY(sqrtm_pair<double>(h, 16, nullptr, P, beta, qb.binv[0], nullptr));

@@ -112,6 +112,7 @@ struct WfPlan {
 };
 // once per solve: per-tile dependency ranges and the 16-bit columns in one pass
 // over the CSR columns; synchronises the stream once
+bool wf_first_gram(int64_t n, int64_t nnz);
 int wf_plan16(lz_handle *h, int64_t n, int64_t nnz, const int64_t *rp, const int32_t *col, WfPlan *pl,
               int64_t nx = -1, int64_t xoff = 0);
 // (nx: rows of the gather source -- a rank's own + halo rows, or the all-gather

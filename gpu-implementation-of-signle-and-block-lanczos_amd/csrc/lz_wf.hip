@@ -160,7 +160,10 @@ __device__ __forceinline__ double dpp_swap1(double x)
 }
 
 // The step kernel.  P2 == nullptr: pass 1 only (the first launch of a solve,
-// on Vg = B, or a distributed rank's boundary tiles; no flags).  P1 ==
+// on Vg = B, or a distributed rank's boundary tiles; no flags); Vj != nullptr
+// there (the one-GPU solve's first launch, shapes with NU * DU * 3 >= NC):
+// the consumers also sum G = Vg^T Vg over their own rows (beta_0's Gram, from
+// the registers the S1 epilogue already holds) into the G slabs.  P1 ==
 // nullptr: no V_{j-1} term (step 0).  Vprev and Vout may alias (V_{j+1} over
 // V_{j-1}: each strip is read, then written, by one wave).  With P2, Vout is
 // the gather source's own rows: Vg + 16 xoff.  part: S1 slabs at [0, G), S2
@@ -196,6 +199,10 @@ __global__ __launch_bounds__(64 * (NC + NL + NU)) void k_wf16(
     __shared__ int p1pub;  // pass-1 tiles this block's loaders have published
     const int lane = threadIdx.x & 63, w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
     const bool has_p2 = P2 != nullptr, has_prev = P1 != nullptr;
+    // beta_0's Gram by the consumers (the first launch; their slabs parked in
+    // the idle updaters' strip slots 1 .. DU)
+    constexpr bool kG0 = DU >= 1 && NU * DU * 3 >= NC;
+    const bool g0 = kG0 && !has_p2 && Vj != nullptr;
     if (threadIdx.x < K) {
         ready[threadIdx.x] = -1;
         done[threadIdx.x] = 0;
@@ -214,9 +221,10 @@ __global__ __launch_bounds__(64 * (NC + NL + NU)) void k_wf16(
         q1 = q2 = q3 = T;
         nx = n;
     }
-    if (T != Th || blockDim.x != 64 * (NC + NL + NU)) {
+    if (T != Th || blockDim.x != 64 * (NC + NL + NU) || (!kG0 && !has_p2 && Vj != nullptr)) {
         // the host planned other tiles (flags, ranges) or launched another
-        // block shape (waves past the roles would index past the tile): refuse loudly
+        // block shape (waves past the roles would index past the tile), or asked
+        // a shape without the slot room for beta_0's Gram: refuse loudly
         if (threadIdx.x == 0) *err = 7;
         return;
     }
@@ -521,8 +529,8 @@ __global__ __launch_bounds__(64 * (NC + NL + NU)) void k_wf16(
             for (int e = lane; e < 512; e += 64) {
                 double a = 0.0;
                 for (int u = 0; u < NU; ++u) a += ust[u][0][0][e];
-                // e < 256: G slab (at 2G), else S2 (at G)
-                part[(e < 256 ? 2 * G : G) * 256 + bid * 256 + (e & 255)] = a;
+                // e < 256: G slab (at 2G; the consumers' when g0), else S2 (at G)
+                if (!(g0 && e < 256)) part[(e < 256 ? 2 * G : G) * 256 + bid * 256 + (e & 255)] = a;
             }
         }
         return;
@@ -550,7 +558,7 @@ __global__ __launch_bounds__(64 * (NC + NL + NU)) void k_wf16(
     auto xr = xwin(0, wb0);
     const auto yr = __builtin_amdgcn_make_buffer_rsrc(Yo, (short)0, bytes, 0x00020000);
     double *S0 = scr[cw];
-    d4_t macc = {0.0, 0.0, 0.0, 0.0};
+    d4_t macc = {0.0, 0.0, 0.0, 0.0}, gcc = {0.0, 0.0, 0.0, 0.0};
     double v1[4] = {0.0, 0.0, 0.0, 0.0};  // the pending strip's own V_{j+1} rows (pair-swapped layout)
     int64_t s0p = -1;
     // S1 += V_{j+1}^T Y over the pending strip (Y parked in S0, swizzled)
@@ -568,6 +576,10 @@ __global__ __launch_bounds__(64 * (NC + NL + NU)) void k_wf16(
         for (int r = 0; r < 4; ++r) ya[r] = S0[fw_sw(4 * r + (lane >> 4), lane & 15)];
 #pragma unroll
         for (int r = 0; r < 4; ++r) macc = mfma16(va[r], ya[r], macc);
+        if (g0) {
+#pragma unroll
+            for (int r = 0; r < 4; ++r) gcc = mfma16(va[r], va[r], gcc);
+        }
     };
     for (int64_t i = 0; i < nt; ++i) {
         const int s = (int)(i % K);
@@ -684,8 +696,16 @@ __global__ __launch_bounds__(64 * (NC + NL + NU)) void k_wf16(
     if (s0p >= 0) epilogue();
     // the block's NC consumer slabs folded into one at part[bid] (S1) by the
     // last consumer to finish, in a fixed order
+    // (g0: consumer cw's G slab in updater strip slot 1 + cw / (3 NU), part
+    // (cw / 3) mod NU, matrix cw mod 3)
+    auto gslab = [&](int c) { return &ust[(c / 3) % NU][1 + c / (3 * NU)][c % 3][0]; };
 #pragma unroll
     for (int r = 0; r < 4; ++r) S0[((lane >> 4) + 4 * r) * 16 + (lane & 15)] = macc[r];
+    if (g0) {
+        double *Gs = gslab(cw);
+#pragma unroll
+        for (int r = 0; r < 4; ++r) Gs[((lane >> 4) + 4 * r) * 16 + (lane & 15)] = gcc[r];
+    }
     int arrived = 0;
     if (lane == 0) arrived = __hip_atomic_fetch_add(&cons_in, 1, __ATOMIC_ACQ_REL, __HIP_MEMORY_SCOPE_WORKGROUP);
     arrived = __shfl(arrived, 0, 64);
@@ -702,7 +722,24 @@ __global__ __launch_bounds__(64 * (NC + NL + NU)) void k_wf16(
             for (; sl < NC; ++sl) a[0] += scr[sl][e];
             slab[e] = (a[0] + a[1]) + (a[2] + a[3]);
         }
+        if (g0) {
+            double *gout = part + (2 * G + bid) * 256;
+            for (int e = lane; e < 256; e += 64) {
+                double a = 0.0;
+                for (int c = 0; c < NC; ++c) a += gslab(c)[e];
+                gout[e] = a;
+            }
+        }
     }
+}
+
+// Whether wf_plan16 will most likely pick a one-GPU wavefront shape whose
+// first launch sums beta_0's Gram (every shape but the wide one): the solve
+// then skips the separate Gram (it would share the fabric with the plan).
+bool wf_first_gram(int64_t n, int64_t nnz)
+{
+    const char *e = getenv("LZ_PASS_WF");
+    return !(e && e[0] == '0') && n < (1 << 24) && !((double)nnz > 10.2 * (double)n);
 }
 
 int wf_plan16(lz_handle *h, int64_t n, int64_t nnz, const int64_t *rp, const int32_t *col, WfPlan *pl, int64_t nx,
