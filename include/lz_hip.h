@@ -10,7 +10,11 @@
  *   - every array argument is a DEVICE pointer owned by the caller unless the
  *     comment says "host"; sizes are element counts.
  *   - work is enqueued on the handle's stream (lz_set_stream; default: the
- *     legacy null stream) and is asynchronous unless stated otherwise.
+ *     legacy null stream) and is asynchronous unless stated otherwise.  Some
+ *     solves fork internal streams of the handle (the b = 32 sqrtm beside the
+ *     next SpMM, the long-tile SpMM pass beside the tile pass, a distributed
+ *     rank's exchange) and join them back into the handle's stream by events
+ *     before the call returns: callers order against the handle's stream only.
  *   - sparse operator: CSR, int64 row_ptr[n_rows+1], int32 col[nnz], values in
  *     `dtype`.  Dense blocks ("tall-skinny", n x b) are ROW-MAJOR with leading
  *     dimension ld >= b (element (r,c) at r*ld + c) unless a layout argument says
