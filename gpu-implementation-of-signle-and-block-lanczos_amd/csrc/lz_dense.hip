@@ -384,17 +384,30 @@ __global__ __launch_bounds__(256) void k_gram32_f32(int64_t n, const float *__re
 #pragma unroll
     for (int v = 0; v < 16; ++v) acc[v] = 0.0f;
     XcdSched s(ceil_div(n, (int64_t)64));  // 64-row units: 16 rows per wave
-    for (int64_t u = s.begin; u < s.end; u += s.step) {
-        const int64_t r0 = u * 64 + 16 * w;
-        float a[8], bq[8];
+    // four units' loads in flight before their MFMAs (one unit at a time, a
+    // wave held 2 KB in flight: 0.386 -> 0.313 ms for C5's 10M x 32; eight
+    // units measured the same, gpurun_out/r05zd*); the MFMAs run in
+    // the same unit order as before
+    constexpr int UU = 4;
+    for (int64_t u0 = s.begin; u0 < s.end; u0 += UU * s.step) {
+        float a[UU][8], bq[UU][8];
 #pragma unroll
-        for (int t = 0; t < 8; ++t) {
-            const int64_t row = r0 + 2 * t + (lane >> 5);
-            a[t] = row < n ? X[row * 32 + (lane & 31)] : 0.0f;
-            if constexpr (!SYM) bq[t] = row < n ? Y[row * 32 + (lane & 31)] : 0.0f;
+        for (int uu = 0; uu < UU; ++uu) {
+            const int64_t u = u0 + uu * s.step;
+            const int64_t r0 = u * 64 + 16 * w;
+#pragma unroll
+            for (int t = 0; t < 8; ++t) {
+                const int64_t row = r0 + 2 * t + (lane >> 5);
+                const bool ok = u < s.end && row < n;
+                a[uu][t] = ok ? X[row * 32 + (lane & 31)] : 0.0f;
+                if constexpr (!SYM) bq[uu][t] = ok ? Y[row * 32 + (lane & 31)] : 0.0f;
+            }
         }
 #pragma unroll
-        for (int t = 0; t < 8; ++t) acc = __builtin_amdgcn_mfma_f32_32x32x2f32(a[t], SYM ? a[t] : bq[t], acc, 0, 0, 0);
+        for (int uu = 0; uu < UU; ++uu)
+#pragma unroll
+            for (int t = 0; t < 8; ++t)
+                acc = __builtin_amdgcn_mfma_f32_32x32x2f32(a[uu][t], SYM ? a[uu][t] : bq[uu][t], acc, 0, 0, 0);
     }
 #pragma unroll
     for (int v = 0; v < 16; ++v)
