@@ -386,7 +386,7 @@ __global__ __launch_bounds__(256) void k_gram32_f32(int64_t n, const float *__re
     XcdSched s(ceil_div(n, (int64_t)64));  // 64-row units: 16 rows per wave
     // four units' loads in flight before their MFMAs (one unit at a time, a
     // wave held 2 KB in flight: 0.386 -> 0.313 ms for C5's 10M x 32; eight
-    // units measured the same, gpurun_out/r05zd*); the MFMAs run in
+    // units measured the same, profiles/r05zd_c5_kernel_stats.csv); the MFMAs run in
     // the same unit order as before
     constexpr int UU = 4;
     for (int64_t u0 = s.begin; u0 < s.end; u0 += UU * s.step) {
