@@ -758,7 +758,7 @@ enum { kFormHalo = 0, kFormAllgather = 1 };
 static int dist_solve_wf16(lz_handle *h, int form, HaloPlan *hp, int64_t n, int64_t n_pad, int64_t nnz,
                            const int64_t *rp, const int32_t *col, const double *val, int m, int64_t lc,
                            const double *B, double *q, double *alpha, double *beta, double *X0, double *X1,
-                           const WfPlan &wp, const SplitPlan &sp);
+                           const WfPlan &wp, const SplitPlan &sp, bool g0);
 
 // The distributed iteration, both exchange forms, any b <= 32, fp64 / fp32.
 //   b = 16 fp64: the fused Q-free passes of block_lanczos_fused16 (pass 1 =
@@ -815,13 +815,17 @@ static int dist_solve_impl(lz_handle *h, int form, HaloPlan *hp, int64_t n, int6
         if (f16 && (!ag || ag_wf)) {
             WfPlan wp;
             LZ_TRY(wf_plan16(h, n, nnz, rp, col, &wp, nx, own_off));
+            // beta_0's Gram from the first launch: every shape but the wide one
+            // (dist_solve_wf16); the ranks must agree, as on the form itself
+            bool g0 = wp.var != 200;
             if (cm && h->nranks > 1) {  // every rank takes the same form (their collectives must match)
-                double v = wp.ok ? 1.0 : 0.0;
-                LZ_HIP_TRY(hipMemcpyAsync(slab, &v, sizeof(double), hipMemcpyHostToDevice, h->stream));
-                LZ_TRY(cm->allreduce_sum(slab, 1, h->stream));
-                LZ_HIP_TRY(hipMemcpyAsync(&v, slab, sizeof(double), hipMemcpyDeviceToHost, h->stream));
+                double v[2] = {wp.ok ? 1.0 : 0.0, g0 ? 1.0 : 0.0};
+                LZ_HIP_TRY(hipMemcpyAsync(slab, v, sizeof(v), hipMemcpyHostToDevice, h->stream));
+                LZ_TRY(cm->allreduce_sum(slab, 2, h->stream));
+                LZ_HIP_TRY(hipMemcpyAsync(v, slab, sizeof(v), hipMemcpyDeviceToHost, h->stream));
                 LZ_HIP_TRY(hipStreamSynchronize(h->stream));
-                wp.ok = v == (double)h->nranks;
+                wp.ok = v[0] == (double)h->nranks;
+                g0 = v[1] == (double)h->nranks;
             }
             h->last_wf = wp.ok ? 1 : 0;
             h->last_wf_pre = 0;
@@ -831,7 +835,7 @@ static int dist_solve_impl(lz_handle *h, int form, HaloPlan *hp, int64_t n, int6
                 h->last_split[0] = sp.on ? sp.i0 : -1;
                 h->last_split[1] = sp.on ? sp.i1 : -1;
                 return dist_solve_wf16(h, form, hp, n, n_pad, nnz, rp, col, val, m, lc, B, q, alpha, beta, X0, X1,
-                                       wp, sp);
+                                       wp, sp, g0);
             }
         }
     }
@@ -959,7 +963,7 @@ static int dist_solve_impl(lz_handle *h, int form, HaloPlan *hp, int64_t n, int6
 static int dist_solve_wf16(lz_handle *h, int form, HaloPlan *hp, int64_t n, int64_t n_pad, int64_t nnz,
                            const int64_t *rp, const int32_t *col, const double *val, int m, int64_t lc,
                            const double *B, double *q, double *alpha, double *beta, double *X0, double *X1,
-                           const WfPlan &wp, const SplitPlan &sp)
+                           const WfPlan &wp, const SplitPlan &sp, bool g0)
 {
     Comm *cm = h->comm;
     constexpr int64_t bb = 256;
@@ -1007,12 +1011,18 @@ static int dist_solve_wf16(lz_handle *h, int form, HaloPlan *hp, int64_t n, int6
         return hp ? halo_exchange(h, *hp, X, rowb, s) : LZ_OK;
     };
     const int64_t lcl = (lc >= 0 && lc < n) ? lc : -1;
-    // ---- beta_0 from the global Gram of B; V_0 = B with its halo / in every slot
-    int np = 0;
-    LZ_TRY(gram_partials<double>(h, n, 16, B, B, 16, &np));
-    LZ_TRY(gram_finish<double>(h, 16, np, 0, slab));
-    LZ_TRY(allreduce(bb));
-    LZ_TRY(sqrtm_pair<double>(h, 16, nullptr, 1, beta, binv[0], nullptr, slab));
+    // ---- beta_0 from the global Gram of B: g0 (no rank on the wide shape,
+    // whose slots have no room for it), summed by the first launch's consumers
+    // and all-reduced with its S1; otherwise a Gram, its own all-reduce and
+    // sqrtm first.  V_0 = B with its halo / in every slot
+    LZ_ARG_CHECK(!g0 || wp.var != 200, "beta_0's Gram in the first launch: not on the wide shape (internal)");
+    if (!g0) {
+        int np = 0;
+        LZ_TRY(gram_partials<double>(h, n, 16, B, B, 16, &np));
+        LZ_TRY(gram_finish<double>(h, 16, np, 0, slab));
+        LZ_TRY(allreduce(bb));
+        LZ_TRY(sqrtm_pair<double>(h, 16, nullptr, 1, beta, binv[0], nullptr, slab));
+    }
     if (ag) {
         if (cm) LZ_TRY(cm->allgather(B, X0, (size_t)n_pad * rowb, h->stream));
         else LZ_HIP_TRY(hipMemcpyAsync(slot, B, (size_t)n * rowb, hipMemcpyDeviceToDevice, h->stream));
@@ -1021,17 +1031,29 @@ static int dist_solve_wf16(lz_handle *h, int form, HaloPlan *hp, int64_t n, int6
         LZ_TRY(exchange(X0, h->stream));
     }
     LZ_TRY(wf_reset16(h, n, wp));
-    // ---- Y_0 = A V_0 (pass 1 only, every tile), alpha_0
+    // ---- Y_0 = A V_0 (pass 1 only, every tile; g0: and G_0), alpha_0
     int G = 0;
-    LZ_TRY(wf_step16(h, n, rp, col, wp.col16, val, pairs, wp, nullptr, nullptr, nullptr, nullptr, nullptr, nullptr,
-                     nullptr, X0, Y, 0, &G, nx, 0, T, h->partials2));
+    LZ_TRY(wf_step16(h, n, rp, col, wp.col16, val, pairs, wp, nullptr, nullptr, g0 ? X0 : nullptr, nullptr, nullptr,
+                     nullptr, nullptr, X0, Y, 0, &G, nx, 0, T, h->partials2));
     {
         WfSlabs sl;
         sl.add(h->partials2, G);
         LZ_TRY(wf_fold16(h, sl, slab));
     }
     LZ_TRY(allreduce(3 * bb));
-    LZ_TRY(alpha_wf16(h, slab, 1, binv[0], nullptr, alpha, P2, ag ? slot : X0, lcl, n, q));
+    if (g0) {  // beta_0, its inverse, alpha_0, P2 and q_0 in one kernel
+        WfAlpha wa;
+        wa.part = slab;
+        wa.P = 1;
+        wa.alpha = alpha;
+        wa.P2 = P2;
+        wa.V = ag ? slot : X0;
+        wa.lc = lcl;
+        wa.qrow = q;
+        LZ_TRY(sqrtm_pair<double>(h, 16, nullptr, 1, beta, binv[0], nullptr, slab + 2 * bb, nullptr, nullptr, &wa));
+    } else {
+        LZ_TRY(alpha_wf16(h, slab, 1, binv[0], nullptr, alpha, P2, ag ? slot : X0, lcl, n, q));
+    }
     const double *Vm1 = nullptr, *V0 = ag ? slot : X0;
     // all-gather form at N > 1: V_{j+1} into the slot over V_j, V_j into X1 (=
     // W) over V_{j-1}, so the slot can be all-gathered in place.  At one rank
