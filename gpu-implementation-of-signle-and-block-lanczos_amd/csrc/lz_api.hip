@@ -566,11 +566,13 @@ int attach_comm(lz_handle *h, Comm *c)
     // the exchange stream and its events first; the communicator is attached
     // last, so a failure leaves the handle detached (and c deleted)
     hipStream_t xs = nullptr;
-    hipEvent_t e1 = nullptr, e2 = nullptr;
+    hipEvent_t e1 = nullptr, e2 = nullptr, e3 = nullptr;
     hipError_t e = hipStreamCreateWithFlags(&xs, hipStreamNonBlocking);
     if (e == hipSuccess) e = hipEventCreateWithFlags(&e1, hipEventDisableTiming);
     if (e == hipSuccess) e = hipEventCreateWithFlags(&e2, hipEventDisableTiming);
+    if (e == hipSuccess) e = hipEventCreateWithFlags(&e3, hipEventDisableTiming);
     if (e != hipSuccess) {
+        if (e3) (void)hipEventDestroy(e3);
         if (e2) (void)hipEventDestroy(e2);
         if (e1) (void)hipEventDestroy(e1);
         if (xs) (void)hipStreamDestroy(xs);
@@ -581,6 +583,7 @@ int attach_comm(lz_handle *h, Comm *c)
     h->xstream = xs;
     h->ev_cx = e1;
     h->ev_xd = e2;
+    h->ev_bd = e3;
     h->nranks = c->nranks;
     h->rank = c->rank;
     h->comm = c;
@@ -619,8 +622,9 @@ static void detach_comm(lz_handle *h)
     h->comm = nullptr;
     if (h->ev_cx) (void)hipEventDestroy(h->ev_cx);
     if (h->ev_xd) (void)hipEventDestroy(h->ev_xd);
+    if (h->ev_bd) (void)hipEventDestroy(h->ev_bd);
     if (h->xstream) (void)hipStreamDestroy(h->xstream);
-    h->ev_cx = h->ev_xd = nullptr;
+    h->ev_cx = h->ev_xd = h->ev_bd = nullptr;
     h->xstream = nullptr;
     h->nranks = 1;
     h->rank = 0;
@@ -1086,15 +1090,32 @@ static int dist_solve_wf16(lz_handle *h, int form, HaloPlan *hp, int64_t n, int6
         sl.add(part, Gk);
         part += 3 * (int64_t)Gk * 256;
         if (exch) {
-            // V_{j+1}'s halo rows / peers' slots, then pass 1 of the boundary tiles
+            // V_{j+1}'s halo rows / peers' slots, then pass 1 of the boundary
+            // tiles: [0, t0) on the handle's stream and [t1, T) beside it on the
+            // exchange stream (two short launches of a few dozen blocks each,
+            // with no waits inside: run one after the other they cost a launch
+            // ramp and tail more per step)
             if (pre) LZ_HIP_TRY(hipStreamWaitEvent(h->stream, h->ev_xd, 0));
             else LZ_TRY(exchange(Vn, h->stream));
+            const bool two = t0 > 0 && t1 < T;
+            if (two) LZ_HIP_TRY(hipEventRecord(h->ev_cx, h->stream));
             LZ_TRY(wf_step16(h, n, rp, col, wp.col16, val, pairs, wp, nullptr, nullptr, nullptr, nullptr, nullptr,
                              nullptr, nullptr, Vg, Y, 0, &G1, nx, 0, t0, part));
             sl.add(part, G1);
             part += 3 * (int64_t)G1 * 256;
-            LZ_TRY(wf_step16(h, n, rp, col, wp.col16, val, pairs, wp, nullptr, nullptr, nullptr, nullptr, nullptr,
-                             nullptr, nullptr, Vg, Y, 0, &G2, nx, t1, T, part));
+            if (two) {
+                LZ_HIP_TRY(hipStreamWaitEvent(h->xstream, h->ev_cx, 0));
+                std::swap(h->stream, h->xstream);  // wf_step16 launches on h->stream
+                const int rc = wf_step16(h, n, rp, col, wp.col16, val, pairs, wp, nullptr, nullptr, nullptr, nullptr,
+                                         nullptr, nullptr, nullptr, Vg, Y, 0, &G2, nx, t1, T, part);
+                std::swap(h->stream, h->xstream);
+                LZ_TRY(rc);
+                LZ_HIP_TRY(hipEventRecord(h->ev_bd, h->xstream));
+                LZ_HIP_TRY(hipStreamWaitEvent(h->stream, h->ev_bd, 0));
+            } else {
+                LZ_TRY(wf_step16(h, n, rp, col, wp.col16, val, pairs, wp, nullptr, nullptr, nullptr, nullptr, nullptr,
+                                 nullptr, nullptr, Vg, Y, 0, &G2, nx, t1, T, part));
+            }
             sl.add(part, G2);
         }
         LZ_TRY(wf_fold16(h, sl, slab));

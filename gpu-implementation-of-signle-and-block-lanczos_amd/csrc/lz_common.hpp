@@ -81,6 +81,7 @@ struct lz_handle {
     // ev_xd: exchange done -> main)
     hipStream_t xstream = nullptr;
     hipEvent_t ev_cx = nullptr, ev_xd = nullptr;
+    hipEvent_t ev_bd = nullptr;  // the wavefront step's second boundary launch (exchange stream) -> main
     int64_t last_split[2] = {-1, -1};  // lz_debug_last_split
     int last_wf = 0, last_wf_pre = 0;  // lz_debug_last_wf: wavefront step, pass-2-first overlap
     // lz_block_lanczos leaves Q0 = Q1 = Q_{m-1}, W = W_m as the reference does
