@@ -90,19 +90,20 @@ PASS2_MFMA_FLOP_PER_ROW = 8 * 2048 // 16
 def wf_kernel(n, hw, nnz=None, one_gpu=True):
     """(full name, PMC short name) of the wavefront-step kernel (lz_wf.hip wf_step16):
     <consumers, stage entries, stages, loaders, updaters, strip slots - 1, 16-bit columns,
-    SW = false (the all-gather save-V_j form runs only at N > 1), GEN> -- GEN false for
-    the one-GPU solve's launches of the default shapes (the specialised form, round 5)."""
+    SW = false (the all-gather save-V_j form runs only at N > 1), GEN, QO = false> -- GEN
+    false for the one-GPU solve's launches of the default shapes (the specialised form,
+    round 5); QO true only in the post-call state launch, which is not a step."""
     c16 = col_bytes(n, hw) == 2
     sh = os.environ.get("LZ_WF_SHAPE", "111")
     tf = 'true' if c16 else 'false'
     gen = 'false' if one_gpu else 'true'
     if nnz is not None and nnz > 10.2 * n:  # the wide shape (C4's density)
-        return f"k_wf16<10,4400,2,1,{3 if c16 else 2},1,{tf},false,{gen}>", "k_wf16"
+        return f"k_wf16<10,4400,2,1,{3 if c16 else 2},1,{tf},false,{gen},false>", "k_wf16"
     if sh not in ("10", "11", "12"):  # default: 1 loader + 11 consumers + 4 updaters
-        return f"k_wf16<11,{11 * 16 * 11},3,1,4,1,{tf},false,{gen}>", "k_wf16"
+        return f"k_wf16<11,{11 * 16 * 11},3,1,4,1,{tf},false,{gen},false>", "k_wf16"
     nc = int(sh)
     du = {10: 2 if c16 else 1, 11: 2, 12: 3 if c16 else 2}[nc]
-    return f"k_wf16<{nc},{nc * 16 * 11},3,2,{14 - nc},{du},{tf},false,true>", "k_wf16"
+    return f"k_wf16<{nc},{nc * 16 * 11},3,2,{14 - nc},{du},{tf},false,true,false>", "k_wf16"
 
 
 # MFMA work of the wavefront step per row: updaters 12 (V_{j+1}) + 4 (G) + 4 (S2),

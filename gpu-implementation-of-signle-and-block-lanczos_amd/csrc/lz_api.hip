@@ -281,10 +281,20 @@ static int block_lanczos_wf16(lz_handle *h, int64_t n, int64_t nnz, const int64_
                               h->stream));
     // the reference's post-call state: W_m = Y_{m-1} beta^-1 - V_{m-2} P1 -
     // V_{m-1} P2 (the pass 2 a further step would run), Q0 = Q1 = V_{m-1} beta^-1
-    // (Q1 untouched at m = 1, as the reference's)
-    if (h->final_state)
-        LZ_TRY(final_state<double>(h, n, 16, Q0, Vm1, V0, nullptr, binv[(m - 1) & 1], Vm1 ? P1 : nullptr, P2, W, Q0,
-                                   m >= 2 ? Q1 : nullptr));
+    // (Q1 untouched at m = 1, as the reference's).  The default shape: one
+    // pass-2-only step launch whose updaters also store Q (QO; the LDS-DMA
+    // streams of pass 2, 4 waves per CU); otherwise the MFMA strip kernel
+    if (h->final_state) {
+        if (wp.var == 111) {
+            int Pq = 0;
+            LZ_TRY(wf_step16(h, n, rp, col, pl.col16, val, pl.pairs, wp, Q0, Vm1, V0, W, binv[(m - 1) & 1],
+                             Vm1 ? P1 : nullptr, P2, W, m >= 2 ? Q1 : nullptr, m, &Pq, -1, 0, 0, nullptr, nullptr,
+                             Q0, true));
+        } else {
+            LZ_TRY(final_state<double>(h, n, 16, Q0, Vm1, V0, nullptr, binv[(m - 1) & 1], Vm1 ? P1 : nullptr, P2, W,
+                                       Q0, m >= 2 ? Q1 : nullptr));
+        }
+    }
     return LZ_OK;
 }
 

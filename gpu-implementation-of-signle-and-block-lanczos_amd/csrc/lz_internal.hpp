@@ -128,7 +128,11 @@ int wf_step16(lz_handle *h, int64_t n, const int64_t *rp, const int32_t *col, co
               const double *val, const uint64_t *pairs, const WfPlan &pl, const double *Yj, const double *Vprev,
               const double *Vj, double *Vout, const double *binv, const double *P1, const double *P2,
               const double *Vg, double *Yo, int epoch, int *nparts, int64_t nx = -1, int64_t p1a = 0,
-              int64_t p1b = -1, double *part = nullptr, const int64_t *q = nullptr, double *Vsave = nullptr);
+              int64_t p1b = -1, double *part = nullptr, const int64_t *q = nullptr, double *Vsave = nullptr,
+              bool qo = false);
+// (qo: the one-GPU solve's post-call state -- a pass-2-only launch, Q =
+// V_j beta^-1 also stored into Vsave and, when not null, Yo; the default shape
+// only, else LZ_E_ARG)
 // (nx: rows of Vg, default n; pass 1 over tiles [p1a, p1b), default all; slabs
 // at part, default h->partials2; q: pass-2 tiles [q[0], q[1]) u [q[2], q[3]),
 // default all -- two ranges only without pass-1 tiles; Vout = Vg + 16 xoff;

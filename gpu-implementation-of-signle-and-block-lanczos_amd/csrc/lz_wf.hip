@@ -178,7 +178,11 @@ __device__ __forceinline__ double dpp_swap1(double x)
 // GEN: the general form above; false: the one-GPU solve's launch (pass 2 over
 // every tile, xoff = 0, the whole gather source below 2^24 rows, no SW), whose
 // range arithmetic then folds away at compile time.
-template <int NC, int CAP, int K, int NL, int NU, int DU, bool C16, bool SW = false, bool GEN = true>
+// QO (the one-GPU solve's post-call state, a pass-2-only launch): pass 2 also
+// stores Q = V_j beta^-1 into Vsave and (when not null) Yo -- the reference's
+// Q0 = Q1 = Q_{m-1} -- beside V_{m} = W_m into Vout.
+template <int NC, int CAP, int K, int NL, int NU, int DU, bool C16, bool SW = false, bool GEN = true,
+          bool QO = false>
 __global__ __launch_bounds__(64 * (NC + NL + NU)) void k_wf16(
     int64_t n, const int64_t *__restrict__ rp, const int32_t *__restrict__ col, const int16_t *__restrict__ col16,
     const double *__restrict__ val, const uint64_t *__restrict__ pairs, const double *Yj, const double *Vprev,
@@ -215,6 +219,7 @@ __global__ __launch_bounds__(64 * (NC + NL + NU)) void k_wf16(
     __syncthreads();  // the only block barrier
     const int64_t T = ceil_div(n, (int64_t)TR);
     static_assert(GEN || !SW, "SW stores are a distributed form");
+    static_assert(!(SW && QO), "Vsave carries either V_j (SW) or Q (QO)");
     if constexpr (!GEN) {  // the host launches this form only for these values
         xoff = 0;
         q0 = 0;
@@ -362,7 +367,11 @@ __global__ __launch_bounds__(64 * (NC + NL + NU)) void k_wf16(
                                                   has_prev ? bytes : 0, 0x00020000),
                 __builtin_amdgcn_make_buffer_rsrc(const_cast<double *>(Vj), (short)0, bytes, 0x00020000)};
             const auto Or = __builtin_amdgcn_make_buffer_rsrc(Vout, (short)0, bytes, 0x00020000);
-            const auto Sr = __builtin_amdgcn_make_buffer_rsrc(SW ? Vsave : Vout, (short)0, SW ? bytes : 0, 0x00020000);
+            const auto Sr = __builtin_amdgcn_make_buffer_rsrc(SW || QO ? Vsave : Vout, (short)0, SW || QO ? bytes : 0,
+                                                              0x00020000);
+            // QO: the second Q output (Q1; out of range, so dropped, when null)
+            const auto Qr = __builtin_amdgcn_make_buffer_rsrc(QO && Yo ? Yo : Vout, (short)0, QO && Yo ? bytes : 0,
+                                                              0x00020000);
             auto strip_r0 = [&](int64_t s) { return ptile(ut0 + (s / NC) * ustep) * TR + 16 * (s % NC); };
             // this lane's DMA pieces: LDS piece q = 64 k + lane holds row q >> 3,
             // global piece (q & 7) ^ swizzle
@@ -434,7 +443,7 @@ __global__ __launch_bounds__(64 * (NC + NL + NU)) void k_wf16(
                 // strip s landed: DU younger strips' six DMAs each, and from the
                 // steady state on also DU strips' two (SW: four) stores, were
                 // issued after it
-                constexpr int ST = SW ? 4 : 2;
+                constexpr int ST = SW ? 4 : QO ? 6 : 2;
                 if (s < DU) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(6 * DU) : "memory");
                 else asm volatile("s_waitcnt vmcnt(%0)" ::"n"((6 + ST) * DU) : "memory");
                 if (s % NC == DU && s >= NC && lane == 0)
@@ -492,6 +501,21 @@ __global__ __launch_bounds__(64 * (NC + NL + NU)) void k_wf16(
                     const uint32_t off = r0b + (uint32_t)(row * 128 + (ev ? c : c - 1) * 8);
                     if (cpol & 8) __builtin_amdgcn_raw_buffer_store_b128(*reinterpret_cast<const v4u32_t *>(&v), Or, off, 0, SA | 2);
                     else __builtin_amdgcn_raw_buffer_store_b128(*reinterpret_cast<const v4u32_t *>(&v), Or, off, 0, SA);
+                }
+                if constexpr (QO) {  // Q = V_j beta^-1, the same pair swap, two outputs
+                    d4_t qa = {0.0, 0.0, 0.0, 0.0};
+#pragma unroll
+                    for (int kc = 0; kc < 4; ++kc) qa = mfma16(ja[kc], bq[0][kc], qa);
+#pragma unroll
+                    for (int h2 = 0; h2 < 2; ++h2) {
+                        const double a0 = qa[2 * h2], a1 = qa[2 * h2 + 1];
+                        const double y = dpp_swap1(ev ? a1 : a0);
+                        const double2 v = ev ? make_double2(a0, y) : make_double2(y, a1);
+                        const int row = 4 * (2 * h2 + (ev ? 0 : 1)) + g;
+                        const uint32_t off = r0b + (uint32_t)(row * 128 + (ev ? c : c - 1) * 8);
+                        __builtin_amdgcn_raw_buffer_store_b128(*reinterpret_cast<const v4u32_t *>(&v), Sr, off, 0, 0);
+                        __builtin_amdgcn_raw_buffer_store_b128(*reinterpret_cast<const v4u32_t *>(&v), Qr, off, 0, 0);
+                    }
                 }
                 if constexpr (SW) {
                     // V_j's strip (slot part 2, as the DMA laid it out) to Vsave:
@@ -816,7 +840,7 @@ int wf_step16(lz_handle *h, int64_t n, const int64_t *rp, const int32_t *col, co
               const double *val, const uint64_t *pairs, const WfPlan &pl, const double *Yj, const double *Vprev,
               const double *Vj, double *Vout, const double *binv, const double *P1, const double *P2,
               const double *Vg, double *Yo, int epoch, int *nparts, int64_t nx, int64_t p1a, int64_t p1b,
-              double *part, const int64_t *q, double *Vsave)
+              double *part, const int64_t *q, double *Vsave, bool qo)
 {
     const int64_t T = ceil_div(n, (int64_t)pl.tr);
     const int64_t xoff = pl.xoff;
@@ -831,7 +855,9 @@ int wf_step16(lz_handle *h, int64_t n, const int64_t *rp, const int32_t *col, co
     LZ_ARG_CHECK(pl.ok && n < (1 << 24), "wavefront step: wf_plan16 first");
     LZ_ARG_CHECK(pairs != nullptr, "strip row orders (strip_pairs) missing");
     LZ_ARG_CHECK(P2 == nullptr || (Yj && Vj && Vout && binv && Vout == Vg + 16 * xoff), "wavefront step buffers");
-    LZ_ARG_CHECK(Vsave == nullptr || (P2 && pl.var != 0), "wavefront step: SW stores (the 111 / wide shapes)");
+    LZ_ARG_CHECK(qo || Vsave == nullptr || (P2 && pl.var != 0), "wavefront step: SW stores (the 111 / wide shapes)");
+    LZ_ARG_CHECK(!qo || (P2 && Vsave && pl.var == 111 && p1a == p1b && xoff == 0 && (nx < 0 || nx == n) && !q),
+                 "wavefront post-call state: a one-GPU pass-2-only launch of the default shape");
     static_assert(12 <= kPairPad, "row orders must cover the last tile's strips");
     // pass 2 covers its tile ranges when it runs; a pass-1-only launch its range
     const int64_t nq = (q1 - q0) + (q3 - q2);
@@ -885,7 +911,9 @@ int wf_step16(lz_handle *h, int64_t n, const int64_t *rp, const int32_t *col, co
     // step; and the one process that used it ended in a segfault at exit,
     // DESIGN.md 5.)
     int rc = LZ_OK;
-    const int ev = prof_begin(h, PROF_SPMM_PASS);
+    // (the post-call state launch is not a step: no class of its own, as the
+    // strip kernel it replaces had none)
+    const int ev = qo ? -1 : prof_begin(h, PROF_SPMM_PASS);
     // (the block is 64 (NC + NL + NU) threads: the kernel refuses any other size)
     auto go = [&](auto kern, int waves) {
         // blocks per CU of this instantiation (per process: one device model;
@@ -922,7 +950,7 @@ int wf_step16(lz_handle *h, int64_t n, const int64_t *rp, const int32_t *col, co
     // LDS (<= 160 KB): strip slots per updater DU + 1, fewer with 32-bit columns
     constexpr int cap12 = 12 * 16 * kWfCapPerRow, cap11 = 11 * 16 * kWfCapPerRow, cap10 = 10 * 16 * kWfCapPerRow;
     // (the instantiation must match pl.tr: the tile count above is the host's)
-    const bool sw = Vsave != nullptr;
+    const bool sw = Vsave != nullptr && !qo;
     // the one-GPU solve's launches (every pass-2 tile, whole source, no SW) take
     // the specialised form (GEN = false) of the default shapes
     const bool one = !sw && xoff == 0 && nx == n && q0 == 0 && q1 == T && q2 == T && q3 == T;
@@ -932,7 +960,9 @@ int wf_step16(lz_handle *h, int64_t n, const int64_t *rp, const int32_t *col, co
 #else
     const bool spec = one;
 #endif
-    if (pl.var == 200 && col16 && sw) go(k_wf16<10, kWfWideCap, 2, 1, 3, 1, true, true>, 10 + 1 + 3);
+    if (qo && col16) go(k_wf16<11, cap11, kWfK, 1, 4, 1, true, false, false, true>, 11 + 1 + 4);
+    else if (qo) go(k_wf16<11, cap11, kWfK, 1, 4, 1, false, false, false, true>, 11 + 1 + 4);
+    else if (pl.var == 200 && col16 && sw) go(k_wf16<10, kWfWideCap, 2, 1, 3, 1, true, true>, 10 + 1 + 3);
     else if (pl.var == 200 && col16 && spec) go(k_wf16<10, kWfWideCap, 2, 1, 3, 1, true, false, false>, 10 + 1 + 3);
     else if (pl.var == 200 && col16) go(k_wf16<10, kWfWideCap, 2, 1, 3, 1, true>, 10 + 1 + 3);
     else if (pl.var == 200 && sw) go(k_wf16<10, kWfWideCap, 2, 1, 2, 1, false, true>, 10 + 1 + 2);
