@@ -404,7 +404,12 @@ static int block_lanczos_b2_32(lz_handle *h, int64_t n, int64_t nnz, const int64
         // the one-workgroup kernels read 32 folded slabs, not the passes' 1024
         const int nf = fold_slabs_g(h, h->partials, np, (int)bb, 32);
         LZ_TRY(alpha_b2(h, h->partials2, nf, bi, alpha + j * bb, P2, in, lc, n, q + (int64_t)j * b));
-        LZ_TRY(fused_ub32(h, n, U, in, bi, P2, out, &np));
+        // the last step's pass UB also leaves the post-call Q0 = Q1 = W_j beta_j^-1
+        // (from the W_j rows it holds; Q0 over U, Q1 over W_j, row by row): the
+        // separate Q pass cost 0.89 ms a solve, this 0.65 (C5 step 4.289-4.294
+        // -> 4.256-4.282 ms, profiles/r05zn_c5_ub_q_ab.log)
+        const bool qlast = j + 1 == m && h->final_state;
+        LZ_TRY(fused_ub32(h, n, U, in, bi, P2, out, &np, qlast ? Q0 : nullptr, qlast && m >= 2 ? Q1 : nullptr));
         if (j + 1 < m) {
             const int ng = fold_slabs_g(h, h->partials, np, (int)bb, 32);
             LZ_TRY(m_b2(h, h->partials2, ng, bi, M));  // M_{j+1} = beta_j^-1 G_{j+1}
@@ -424,9 +429,8 @@ static int block_lanczos_b2_32(lz_handle *h, int64_t n, int64_t nnz, const int64
         in = out;
     }
     LZ_HIP_TRY(hipMemcpyAsync(beta + m * bb, binv[(m - 1) & 1], sizeof(float) * bb, hipMemcpyDeviceToDevice, h->stream));
-    if (h->final_state)  // W = W_m (in), Q0 = Q1 = W_{m-1} beta^-1 (prev)
-        LZ_TRY(final_state<float>(h, n, b, nullptr, nullptr, prev, in, binv[(m - 1) & 1], nullptr, nullptr, W, Q0,
-                                  m >= 2 ? Q1 : nullptr));
+    // (the post-call state: W = W_m is the last pass UB's output, in W by the
+    // residual order, and that pass also wrote Q0 = Q1 = W_{m-1} beta^-1)
     return LZ_OK;
 }
 

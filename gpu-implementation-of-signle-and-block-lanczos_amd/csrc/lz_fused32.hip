@@ -198,11 +198,15 @@ __global__ __launch_bounds__(64 * kF32Waves) void k_fused_el32(int64_t n, const 
     block_slab32<kF32Waves>(red, g, lane, w, part);
 }
 
-__global__ __launch_bounds__(64 * kF32Waves) void k_fused_ub32(int64_t n, const float *__restrict__ U,
-                                                               const float *__restrict__ Wj,
+// QO (the solve's last step): also Q = W_j beta^-1 into Qa and (when not
+// null) Qb -- the reference's post-call Q0 = Q1 = Q_{m-1} -- from the W_j rows
+// the wave already holds; Qa / Qb may alias U / W_j (a unit's rows are loaded
+// by the wave that stores them, before it stores them).
+template <bool QO>
+__global__ __launch_bounds__(64 * kF32Waves) void k_fused_ub32(int64_t n, const float *U, const float *Wj,
                                                                const float *__restrict__ binv,
                                                                const float *__restrict__ P2, float *__restrict__ Wn,
-                                                               double *__restrict__ part)
+                                                               double *__restrict__ part, float *Qa, float *Qb)
 {
     __shared__ double red[kF32Waves][1024];
     const int lane = threadIdx.x & 63, w = threadIdx.x >> 6, hh = lane >> 5, jr = lane & 31;
@@ -234,6 +238,21 @@ __global__ __launch_bounds__(64 * kF32Waves) void k_fused_ub32(int64_t n, const 
         for (int v = 0; v < 16; ++v) {
             const int64_t rr = r0 + (v & 3) + 8 * (v >> 2) + 4 * hh;
             if (rr < n) Wn[rr * 32 + jr] = acc[v];
+        }
+        if constexpr (QO) {
+            f16v_t q;
+#pragma unroll
+            for (int v = 0; v < 16; ++v) q[v] = 0.0f;
+#pragma unroll
+            for (int s2 = 0; s2 < 16; ++s2) q = mfma32(wa[s2], bo[s2], q);  // W_j beta^-1
+#pragma unroll
+            for (int v = 0; v < 16; ++v) {
+                const int64_t rr = r0 + (v & 3) + 8 * (v >> 2) + 4 * hh;
+                if (rr < n) {
+                    Qa[rr * 32 + jr] = q[v];
+                    if (Qb) Qb[rr * 32 + jr] = q[v];
+                }
+            }
         }
 #pragma unroll
         for (int v = 0; v < 16; ++v) g = mfma32(acc[v], acc[v], g);  // rows past n: 0
@@ -275,14 +294,18 @@ int fused_el32(lz_handle *h, int64_t n, const float *Wj, const float *U, int *np
 }
 
 int fused_ub32(lz_handle *h, int64_t n, const float *U, const float *Wj, const float *binv, const float *P2,
-               float *Wn, int *nparts)
+               float *Wn, int *nparts, float *Qa, float *Qb)
 {
     // 2 blocks per CU: 4.25 ms per C5 step against 4.40 at 4, 4.37 at 3, 4.38 at 1 and 8
     const int grid = f32_grid(h, n, 2);
     LZ_TRY(ensure_partials(h, (size_t)grid * 1024));
     const int ev = prof_begin(h, PROF_UPDATE_PASS);
-    hipLaunchKernelGGL(k_fused_ub32, dim3(grid), dim3(64 * kF32Waves), 0, h->stream, n, U, Wj, binv, P2, Wn,
-                       h->partials);
+    if (Qa)
+        hipLaunchKernelGGL(k_fused_ub32<true>, dim3(grid), dim3(64 * kF32Waves), 0, h->stream, n, U, Wj, binv, P2, Wn,
+                           h->partials, Qa, Qb);
+    else
+        hipLaunchKernelGGL(k_fused_ub32<false>, dim3(grid), dim3(64 * kF32Waves), 0, h->stream, n, U, Wj, binv, P2,
+                           Wn, h->partials, nullptr, nullptr);
     prof_end(h, ev);
     LZ_LAUNCH_CHECK();
     *nparts = grid;

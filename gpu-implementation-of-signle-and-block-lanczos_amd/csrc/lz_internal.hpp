@@ -169,7 +169,8 @@ int fused_u32(lz_handle *h, int64_t n, float *Wn, const float *Wj, const float *
 // C5 beta^2 step (lz_fused32.hip, lz_dense.hip, lz_spmm.hip)
 int fused_el32(lz_handle *h, int64_t n, const float *Wj, const float *U, int *nparts);
 int fused_ub32(lz_handle *h, int64_t n, const float *U, const float *Wj, const float *binv, const float *P2,
-               float *Wn, int *nparts);
+               float *Wn, int *nparts, float *Qa = nullptr,
+               float *Qb = nullptr);
 int alpha_b2(lz_handle *h, const double *part, int P, const float *binv, float *alpha, float *P2, const float *Wj,
              int64_t lc, int64_t n, float *qrow);
 int m_b2(lz_handle *h, const double *part, int P, const float *binv, float *M);
