@@ -90,20 +90,27 @@ PASS2_MFMA_FLOP_PER_ROW = 8 * 2048 // 16
 def wf_kernel(n, hw, nnz=None, one_gpu=True):
     """(full name, PMC short name) of the wavefront-step kernel (lz_wf.hip wf_step16):
     <consumers, stage entries, stages, loaders, updaters, strip slots - 1, 16-bit columns,
-    SW = false (the all-gather save-V_j form runs only at N > 1), GEN, QO = false> -- GEN
+    SW = false (the all-gather save-V_j form runs only at N > 1), GEN, XO = 0> -- GEN
     false for the one-GPU solve's launches of the default shapes (the specialised form,
-    round 5); QO true only in the post-call state launch, which is not a step."""
+    round 5); XO 1 is the default shape's first launch of a solve (beta_0's Gram, its own
+    instantiation: wf_first_kernel), XO 2 the post-call state launch, not a step."""
     c16 = col_bytes(n, hw) == 2
     sh = os.environ.get("LZ_WF_SHAPE", "111")
     tf = 'true' if c16 else 'false'
     gen = 'false' if one_gpu else 'true'
     if nnz is not None and nnz > 10.2 * n:  # the wide shape (C4's density)
-        return f"k_wf16<10,4400,2,1,{3 if c16 else 2},1,{tf},false,{gen},false>", "k_wf16"
+        return f"k_wf16<10,4400,2,1,{3 if c16 else 2},1,{tf},false,{gen},0>", "k_wf16"
     if sh not in ("10", "11", "12"):  # default: 1 loader + 11 consumers + 4 updaters
-        return f"k_wf16<11,{11 * 16 * 11},3,1,4,1,{tf},false,{gen},false>", "k_wf16"
+        return f"k_wf16<11,{11 * 16 * 11},3,1,4,1,{tf},false,{gen},0>", "k_wf16"
     nc = int(sh)
     du = {10: 2 if c16 else 1, 11: 2, 12: 3 if c16 else 2}[nc]
-    return f"k_wf16<{nc},{nc * 16 * 11},3,2,{14 - nc},{du},{tf},false,true,false>", "k_wf16"
+    return f"k_wf16<{nc},{nc * 16 * 11},3,2,{14 - nc},{du},{tf},false,true,0>", "k_wf16"
+
+
+def wf_first_kernel(name):
+    """The first launch of a solve for the default shape: the same kernel with XO = 1
+    (None for the other shapes, whose first launch is the step kernel itself)."""
+    return name[:-2] + "1>" if name.startswith("k_wf16<11,") and name.endswith(",0>") else None
 
 
 # MFMA work of the wavefront step per row: updaters 12 (V_{j+1}) + 4 (G) + 4 (S2),
@@ -760,7 +767,8 @@ def main():
                 # the solve's bytes spread over its launches, as bytes_per_launch (at N > 1 a step is
                 # several launches over the same rows: the requested tiles' pass 2, the step, the boundary)
                 traffic = round((d["hbm_bytes_first_launch"] + (K - 1) * d["hbm_bytes_per_launch"]) / spmm_cnt)
-            roof = {"bound": "hbm", "kernel": kname, "achieved": round(ach, 1),
+            roof = {"bound": "hbm", "kernel": kname, "first_launch_kernel": wf_first_kernel(kname),
+                    "achieved": round(ach, 1),
                     "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": round(ach / HBM_PEAK_GBS, 4),
                     "traffic": traffic, "traffic_unit": "bytes/launch (mean over the profiled solve's launches)",
                     "traffic_source": tsrc, "avg_ms": round(t_pass * 1e3, 4),

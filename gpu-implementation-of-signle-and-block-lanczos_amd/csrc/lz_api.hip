@@ -327,8 +327,8 @@ static int block_lanczos_fused16(lz_handle *h, int64_t n, int64_t nnz, const int
             LZ_TRY(strip_pairs(h, n, rp, &pl.pairs));
             pl.col16 = wp.col16;
             if (!g0) LZ_HIP_TRY(hipStreamWaitEvent(h->stream, h->ev_join, 0));
-            else if (wp.var == 200) LZ_TRY(gram_partials<double>(h, n, 16, B, B, 16, &P));  // (the wide shape)
-            const bool first = g0 && wp.var != 200;
+            else if (wp.var != 111) LZ_TRY(gram_partials<double>(h, n, 16, B, B, 16, &P));  // (another shape)
+            const bool first = g0 && wp.var == 111;
             return block_lanczos_wf16(h, n, nnz, rp, col, val, m, lc, B, q, alpha, beta, Q0, Q1, W, pl, wp,
                                       first ? -1 : P);
         }
@@ -833,9 +833,9 @@ static int dist_solve_impl(lz_handle *h, int form, HaloPlan *hp, int64_t n, int6
         if (f16 && (!ag || ag_wf)) {
             WfPlan wp;
             LZ_TRY(wf_plan16(h, n, nnz, rp, col, &wp, nx, own_off));
-            // beta_0's Gram from the first launch: every shape but the wide one
-            // (dist_solve_wf16); the ranks must agree, as on the form itself
-            bool g0 = wp.var != 200;
+            // beta_0's Gram from the first launch: the default shape (XO 1,
+            // dist_solve_wf16); the ranks must agree, as on the form itself
+            bool g0 = wp.var == 111;
             if (cm && h->nranks > 1) {  // every rank takes the same form (their collectives must match)
                 double v[2] = {wp.ok ? 1.0 : 0.0, g0 ? 1.0 : 0.0};
                 LZ_HIP_TRY(hipMemcpyAsync(slab, v, sizeof(v), hipMemcpyHostToDevice, h->stream));
@@ -1029,11 +1029,11 @@ static int dist_solve_wf16(lz_handle *h, int form, HaloPlan *hp, int64_t n, int6
         return hp ? halo_exchange(h, *hp, X, rowb, s) : LZ_OK;
     };
     const int64_t lcl = (lc >= 0 && lc < n) ? lc : -1;
-    // ---- beta_0 from the global Gram of B: g0 (no rank on the wide shape,
-    // whose slots have no room for it), summed by the first launch's consumers
+    // ---- beta_0 from the global Gram of B: g0 (every rank on the default
+    // shape), summed by the first launch's consumers
     // and all-reduced with its S1; otherwise a Gram, its own all-reduce and
     // sqrtm first.  V_0 = B with its halo / in every slot
-    LZ_ARG_CHECK(!g0 || wp.var != 200, "beta_0's Gram in the first launch: not on the wide shape (internal)");
+    LZ_ARG_CHECK(!g0 || wp.var == 111, "beta_0's Gram in the first launch: the default shape only (internal)");
     if (!g0) {
         int np = 0;
         LZ_TRY(gram_partials<double>(h, n, 16, B, B, 16, &np));

@@ -178,11 +178,13 @@ __device__ __forceinline__ double dpp_swap1(double x)
 // GEN: the general form above; false: the one-GPU solve's launch (pass 2 over
 // every tile, xoff = 0, the whole gather source below 2^24 rows, no SW), whose
 // range arithmetic then folds away at compile time.
-// QO (the one-GPU solve's post-call state, a pass-2-only launch): pass 2 also
-// stores Q = V_j beta^-1 into Vsave and (when not null) Yo -- the reference's
-// Q0 = Q1 = Q_{m-1} -- beside V_{m} = W_m into Vout.
-template <int NC, int CAP, int K, int NL, int NU, int DU, bool C16, bool SW = false, bool GEN = true,
-          bool QO = false>
+// XO, extra outputs (own instantiations, so the step launch carries none of
+// their registers): 1, a solve's first launch (pass 1 only, Vj != nullptr)
+// whose consumers also sum beta_0's Gram (see above); 2, the one-GPU solve's
+// post-call state (a pass-2-only launch): pass 2 also stores Q = V_j beta^-1
+// into Vsave and (when not null) Yo -- the reference's Q0 = Q1 = Q_{m-1} --
+// beside V_m = W_m into Vout.
+template <int NC, int CAP, int K, int NL, int NU, int DU, bool C16, bool SW = false, bool GEN = true, int XO = 0>
 __global__ __launch_bounds__(64 * (NC + NL + NU)) void k_wf16(
     int64_t n, const int64_t *__restrict__ rp, const int32_t *__restrict__ col, const int16_t *__restrict__ col16,
     const double *__restrict__ val, const uint64_t *__restrict__ pairs, const double *Yj, const double *Vprev,
@@ -205,7 +207,8 @@ __global__ __launch_bounds__(64 * (NC + NL + NU)) void k_wf16(
     const bool has_p2 = P2 != nullptr, has_prev = P1 != nullptr;
     // beta_0's Gram by the consumers (the first launch; their slabs parked in
     // the idle updaters' strip slots 1 .. DU)
-    constexpr bool kG0 = DU >= 1 && NU * DU * 3 >= NC;
+    constexpr bool kG0 = XO == 1 && DU >= 1 && NU * DU * 3 >= NC;
+    constexpr bool QO = XO == 2;
     const bool g0 = kG0 && !has_p2 && Vj != nullptr;
     if (threadIdx.x < K) {
         ready[threadIdx.x] = -1;
@@ -219,14 +222,14 @@ __global__ __launch_bounds__(64 * (NC + NL + NU)) void k_wf16(
     __syncthreads();  // the only block barrier
     const int64_t T = ceil_div(n, (int64_t)TR);
     static_assert(GEN || !SW, "SW stores are a distributed form");
-    static_assert(!(SW && QO), "Vsave carries either V_j (SW) or Q (QO)");
+    static_assert(!(SW && XO == 2), "Vsave carries either V_j (SW) or Q (XO 2)");
     if constexpr (!GEN) {  // the host launches this form only for these values
         xoff = 0;
         q0 = 0;
         q1 = q2 = q3 = T;
         nx = n;
     }
-    if (T != Th || blockDim.x != 64 * (NC + NL + NU) || (!kG0 && !has_p2 && Vj != nullptr)) {
+    if (T != Th || blockDim.x != 64 * (NC + NL + NU) || (kG0 != (!has_p2 && Vj != nullptr))) {
         // the host planned other tiles (flags, ranges) or launched another
         // block shape (waves past the roles would index past the tile), or asked
         // a shape without the slot room for beta_0's Gram: refuse loudly
@@ -757,13 +760,16 @@ __global__ __launch_bounds__(64 * (NC + NL + NU)) void k_wf16(
     }
 }
 
-// Whether wf_plan16 will most likely pick a one-GPU wavefront shape whose
-// first launch sums beta_0's Gram (every shape but the wide one): the solve
-// then skips the separate Gram (it would share the fabric with the plan).
+// Whether wf_plan16 will most likely pick the default wavefront shape, whose
+// first launch can sum beta_0's Gram (XO 1): the solve then skips the separate
+// Gram (it would share the fabric with the plan).
 bool wf_first_gram(int64_t n, int64_t nnz)
 {
     const char *e = getenv("LZ_PASS_WF");
-    return !(e && e[0] == '0') && n < (1 << 24) && !((double)nnz > 10.2 * (double)n);
+    const char *sh = getenv("LZ_WF_SHAPE");
+    const int want = sh ? atoi(sh) : 111;
+    return !(e && e[0] == '0') && n < (1 << 24) && !((double)nnz > 10.2 * (double)n) &&
+           !(want == 10 || want == 11 || want == 12);
 }
 
 int wf_plan16(lz_handle *h, int64_t n, int64_t nnz, const int64_t *rp, const int32_t *col, WfPlan *pl, int64_t nx,
@@ -960,8 +966,17 @@ int wf_step16(lz_handle *h, int64_t n, const int64_t *rp, const int32_t *col, co
 #else
     const bool spec = one;
 #endif
-    if (qo && col16) go(k_wf16<11, cap11, kWfK, 1, 4, 1, true, false, false, true>, 11 + 1 + 4);
-    else if (qo) go(k_wf16<11, cap11, kWfK, 1, 4, 1, false, false, false, true>, 11 + 1 + 4);
+    // (beta_0's Gram in a first launch: the default shape only, wf_first_gram)
+    const bool g0 = !P2 && Vj != nullptr;
+    if (g0 && pl.var != 111) {
+        set_error("wavefront first launch with beta_0's Gram: the default shape only (internal)");
+        rc = LZ_E_ARG;
+    } else if (qo && col16) go(k_wf16<11, cap11, kWfK, 1, 4, 1, true, false, false, 2>, 11 + 1 + 4);
+    else if (qo) go(k_wf16<11, cap11, kWfK, 1, 4, 1, false, false, false, 2>, 11 + 1 + 4);
+    else if (g0 && col16 && spec) go(k_wf16<11, cap11, kWfK, 1, 4, 1, true, false, false, 1>, 11 + 1 + 4);
+    else if (g0 && col16) go(k_wf16<11, cap11, kWfK, 1, 4, 1, true, false, true, 1>, 11 + 1 + 4);
+    else if (g0 && spec) go(k_wf16<11, cap11, kWfK, 1, 4, 1, false, false, false, 1>, 11 + 1 + 4);
+    else if (g0) go(k_wf16<11, cap11, kWfK, 1, 4, 1, false, false, true, 1>, 11 + 1 + 4);
     else if (pl.var == 200 && col16 && sw) go(k_wf16<10, kWfWideCap, 2, 1, 3, 1, true, true>, 10 + 1 + 3);
     else if (pl.var == 200 && col16 && spec) go(k_wf16<10, kWfWideCap, 2, 1, 3, 1, true, false, false>, 10 + 1 + 3);
     else if (pl.var == 200 && col16) go(k_wf16<10, kWfWideCap, 2, 1, 3, 1, true>, 10 + 1 + 3);

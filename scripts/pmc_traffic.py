@@ -2,7 +2,11 @@
 passes (FETCH_SIZE, WRITE_SIZE; KB per dispatch).  gfx950 FETCH_SIZE counts
 128-B reads at 64 B (MI355X_MICROARCH.md "HBM"), so it is doubled.
 
-    python scripts/pmc_traffic.py <fetch_dir> <write_dir> <kernel_full> <short> <n> <nnz> <hw> <out.json>
+    python scripts/pmc_traffic.py <fetch_dir> <write_dir> <kernel_full> <short> <n> <nnz> <hw> <out.json> [first]
+
+first (k_wf16 of the default shape): the instantiation of a solve's first launch (XO = 1,
+beta_0's Gram), summarised as hbm_bytes_first_launch; without it the first launches are
+told apart from the steady ones of the same instantiation by their writes.
 
 kernel_full: the instantiation as bench.py names it (e.g.
 "k_fused_pp16<14,2376,3,2,false>"), matched exactly against the demangled
@@ -20,24 +24,30 @@ sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 from bench import _norm, source_sha  # noqa: E402
 
 fd, wd, kfull, short, n, nnz, hw, out = sys.argv[1:9]
+kfirst = sys.argv[9] if len(sys.argv) > 9 else None
 
 
-def values(d, counter):
+def values(d, counter, kname=None):
+    kname = kname or kfull
     v, names = [], set()
     for f in glob.glob(f"{d}/**/*counter_collection.csv", recursive=True):
         for r in csv.DictReader(open(f)):
-            if _norm(r["Kernel_Name"]) == _norm(kfull) and r["Counter_Name"] == counter:
+            if _norm(r["Kernel_Name"]) == _norm(kname) and r["Counter_Name"] == counter:
                 v.append((int(r["Dispatch_Id"]), float(r["Counter_Value"])))
                 names.add(r["Kernel_Name"].split("(")[0])
     if not v:
-        sys.exit(f"{kfull}: no {counter} dispatches in {d}")
+        sys.exit(f"{kname}: no {counter} dispatches in {d}")
     return [x for _, x in sorted(v)], sorted(names)
 
 
 fv, names = values(fd, "FETCH_SIZE")
 wv, _ = values(wd, "WRITE_SIZE")
 first = None
-if short == "k_wf16" and len(fv) == len(wv):
+if kfirst:
+    f1, _ = values(fd, "FETCH_SIZE", kfirst)
+    w1, _ = values(wd, "WRITE_SIZE", kfirst)
+    first = int((2 * sum(f1) / len(f1) + sum(w1) / len(w1)) * 1024)
+elif short == "k_wf16" and len(fv) == len(wv):
     # the wavefront kernel's first launch of a solve is pass 1 only (it writes
     # Y alone, half the others' writes): steady-state launches summarised
     # apart, the two passes' dispatches paired in launch order
