@@ -34,8 +34,9 @@
 // every load of V_{j+1} is an sc1 load.  Results do not depend on placement;
 // liveness needs every block resident (one block per CU, grid <= CUs), and
 // every wait is bounded (a timeout sets the device error word).
-#include <atomic>
 #include <climits>
+#include <mutex>
+#include <unordered_map>
 
 #include "lz_internal.hpp"
 #include "lz_kernels.hpp"
@@ -899,7 +900,10 @@ int wf_step16(lz_handle *h, int64_t n, const int64_t *rp, const int32_t *col, co
     // C3 (lmin 4): shape 111 best at lmin + 3 = 7 (5: 3.07 ms, 6: 1.90, 7: 1.82,
     // 8: 1.84, 10: 1.87); the 2-loader shapes at lmin + 4; the wide shape flat
     // from lmin to lmin + 16 (profiles/r04_wide_lead_ab.log)
-    const int lead = lmin + (pl.var ? 3 : 4);
+#ifndef LZ_WF_LEAD_ADD  // (a measurement build may move the one-loader shapes' offset)
+#define LZ_WF_LEAD_ADD 3
+#endif
+    const int lead = lmin + (pl.var ? LZ_WF_LEAD_ADD : 4);
     // streaming (nt) hints: bit 0 the updaters' reads, bit 1 the CSR stages,
     // bit 2 the Y stores, bit 3 the V_{j+1} stores.  7: every stream touched
     // once is nt, so the V_{j+1} rows stay in L2 for the gathers (C3: 1.74-1.81
@@ -922,13 +926,21 @@ int wf_step16(lz_handle *h, int64_t n, const int64_t *rp, const int32_t *col, co
     const int ev = qo ? -1 : prof_begin(h, PROF_SPMM_PASS);
     // (the block is 64 (NC + NL + NU) threads: the kernel refuses any other size)
     auto go = [&](auto kern, int waves) {
-        // blocks per CU of this instantiation (per process: one device model;
-        // virtual ranks' threads may race here, each storing the same value)
-        static std::atomic<int> occ_cache{-1};
-        int occ = occ_cache.load(std::memory_order_relaxed);
-        if (occ < 0) {
-            if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&occ, kern, 64 * waves, 0) != hipSuccess) occ = 0;
-            occ_cache.store(occ, std::memory_order_relaxed);
+        // blocks per CU of this instantiation, cached per kernel (every
+        // instantiation has the same function type, so a static in this lambda
+        // would be one cache for all of them); per process: one device model
+        int occ = -1;
+        {
+            static std::mutex mu;
+            static std::unordered_map<const void *, int> occ_cache;
+            std::lock_guard<std::mutex> lk(mu);
+            const auto it = occ_cache.find(reinterpret_cast<const void *>(kern));
+            if (it != occ_cache.end()) {
+                occ = it->second;
+            } else {
+                if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&occ, kern, 64 * waves, 0) != hipSuccess) occ = 0;
+                occ_cache.emplace(reinterpret_cast<const void *>(kern), occ);
+            }
         }
         if ((int64_t)grid > (int64_t)occ * h->n_cu) {
             set_error("wavefront step: %d blocks of %d threads cannot all be resident (%d per CU x %d CUs)", grid,
