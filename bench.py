@@ -646,7 +646,7 @@ def main():
             # step 0 has no W_{j-1} term: A + 2 nbs, later steps A + 3 nbs
             sp5_b = k5p * (a5 + 2 * nbs5) + (k5p - 1) * nbs5
             t5 = sp5_ms * 1e-3
-            kn5 = "k_spmm_seg<float,32,48,768,false,0,false,true>"
+            kn5 = "k_spmm_seg<float,32,48,1024,false,0,false,true>"
             tr5, src5 = pmc_traffic("k_spmm_seg_c5", n5, A5.nnz, 0, kn5)
             c5["roofline"] = {"bound": "hbm", "kernel": kn5 + " (+ its long-tile pass, MODE 1)",
                               "bytes_per_launch": round(sp5_b / k5p), "avg_ms": round(t5 / k5p * 1e3, 4),

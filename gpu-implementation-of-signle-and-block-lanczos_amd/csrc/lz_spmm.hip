@@ -1279,8 +1279,13 @@ int spmm_rm_b2(lz_handle *h, int64_t n, int64_t nnz, const int64_t *rp, const in
     LZ_ARG_CHECK(spmm_b2_ok(n, nnz, nx), "beta^2 SpMM epilogue: shape not covered");
     if (n <= 0) return LZ_OK;
     const int ev = prof_begin(h, PROF_SPMM);
-    const int rc = launch_seg<float, 32, 48, 768, false, false, true>(h, n, rp, col, val, X, 32, nx, Y, 32, Wp, Mm,
-                                                                      plan_slot, slot_out);
+    // a 1024-entry stage (not the plain SpMM's 768): fewer power-law tiles
+    // overflow to the long-tile pass, at 6 blocks per CU instead of 7.  C5
+    // SpMM 2.894-2.901 -> 2.828-2.833 ms; stages of 896 / 1152 / 1280 (64-row
+    // tiles) / 1536: 2.874-2.877 / 2.939-2.942 / 2.833-2.845 / 2.924-2.929
+    // (profiles/r05zz6_c5_tile_shape_ab.log, alternating processes)
+    const int rc = launch_seg<float, 32, 48, 1024, false, false, true>(h, n, rp, col, val, X, 32, nx, Y, 32, Wp, Mm,
+                                                                       plan_slot, slot_out);
     prof_end(h, ev);
     LZ_TRY(rc);
     LZ_LAUNCH_CHECK();
