@@ -138,8 +138,8 @@ PASS2_KERNEL = "k_fused_update16<true,8,false>"  # the single-GPU pass 2 (lz_fus
 
 def spmm_kernel(nnz, n):
     """The plain SpMM kernel lz_csr_spmm launches for b = 16 fp64 (lz_spmm.hip launch_spmm_rm)."""
+    cap = 1536 if nnz > 13.0 * n else 768
     win = n >= (1 << 24)
-    cap = 1536 if nnz > 13.0 * n else (768 if win else 896)
     return f"k_spmm_seg<double,16,48,{cap},{'true' if win else 'false'},0,false,false>"
 
 

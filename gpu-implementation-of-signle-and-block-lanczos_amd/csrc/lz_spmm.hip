@@ -1237,11 +1237,7 @@ static int launch_spmm_rm(lz_handle *h, int64_t n, int64_t nnz, const int64_t *r
             else if (buf_ok) rc = launch_seg<T, B, 48, 1536, false, true>(h, n, rp, col, val, X, ldx, nx, Y, ldy);
             else if (!wide) rc = launch_seg<T, B, 48, 768, true, true>(h, n, rp, col, val, X, ldx, nx, Y, ldy);
             else rc = launch_seg<T, B, 48, 1536, true, true>(h, n, rp, col, val, X, ldx, nx, Y, ldy);
-        }
-        // (an 896-entry stage: C3 SpMM 1.224-1.227 -> 1.213-1.218 ms against 768;
-        // 640 / 1024 / 64 rows x 1024 / 32 x 512: 1.221-1.228 / 1.306-1.312 /
-        // 1.268-1.281 / 1.317-1.321, profiles/r05zza_spmm_tile_shape_ab.log)
-        else if (buf_ok && !wide) rc = launch_seg<T, B, 48, 896, false>(h, n, rp, col, val, X, ldx, nx, Y, ldy);
+        } else if (buf_ok && !wide) rc = launch_seg<T, B, 48, 768, false>(h, n, rp, col, val, X, ldx, nx, Y, ldy);
         else if (buf_ok) rc = launch_seg<T, B, 48, 1536, false>(h, n, rp, col, val, X, ldx, nx, Y, ldy);
         else if (!wide) rc = launch_seg<T, B, 48, 768, true>(h, n, rp, col, val, X, ldx, nx, Y, ldy);
         else rc = launch_seg<T, B, 48, 1536, true>(h, n, rp, col, val, X, ldx, nx, Y, ldy);
