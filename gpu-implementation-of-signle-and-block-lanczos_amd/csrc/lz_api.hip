@@ -386,7 +386,8 @@ static int block_lanczos_b2_32(lz_handle *h, int64_t n, int64_t nnz, const int64
     float *sc = reinterpret_cast<float *>(h->scratch + 4 * kMaxB * kMaxB);
     float *binv[2] = {sc, sc + bb}, *P2 = sc + 2 * bb, *M = sc + 3 * bb;
     float *U = Q0;
-    int np = 0;
+    int np = 0, cap = 768;
+    LZ_TRY(spmm_b2_stage(h, n, rp, &cap));  // (the solve's one host sync, before any of its work)
     LZ_TRY(gram_partials<float>(h, n, b, B, B, b, &np));
     LZ_TRY(sqrtm_pair<float>(h, b, nullptr, np, beta, binv[0], nullptr));
     const float *in = B, *prev = nullptr;
@@ -398,7 +399,8 @@ static int block_lanczos_b2_32(lz_handle *h, int64_t n, int64_t nnz, const int64
         // from step 1 on the long-tile pass runs beside the tile pass, over the
         // list step 0 queued (C5 step 4.401-4.411 -> 4.381-4.385 ms, each tile computed as before)
         const int plan = j > 0 ? lslot : -1;
-        LZ_TRY(spmm_rm_b2(h, n, nnz, rp, col, val, in, n, U, prev, j ? M : nullptr, plan, j == 0 ? &lslot : nullptr));
+        LZ_TRY(spmm_rm_b2(h, n, nnz, rp, col, val, in, n, U, prev, j ? M : nullptr, plan, j == 0 ? &lslot : nullptr,
+                          cap));
         if (j > 0) LZ_HIP_TRY(hipStreamWaitEvent(h->stream, h->ev_join, 0));
         LZ_TRY(fused_el32(h, n, in, U, &np));
         // the one-workgroup kernels read 32 folded slabs, not the passes' 1024

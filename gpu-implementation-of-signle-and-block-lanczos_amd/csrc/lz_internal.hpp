@@ -178,9 +178,12 @@ bool spmm_b2_ok(int64_t n, int64_t nnz, int64_t nx);
 int fold_slabs_g(lz_handle *h, const double *part, int64_t P, int bb, int G);  // -> slab count at h->partials2
 // plan_slot >= 0: the long-tile list an earlier call of the solve queued (its
 // *slot_out), the long-tile pass beside the main kernel (launch_seg)
+// cap: the CSR stage (768 or 1024 entries), one per solve (spmm_b2_stage):
+// a solve's planned calls must use the stage its first call queued with
 int spmm_rm_b2(lz_handle *h, int64_t n, int64_t nnz, const int64_t *rp, const int32_t *col, const float *val,
                const float *X, int64_t nx, float *Y, const float *Wp, const float *Mm, int plan_slot = -1,
-               int *slot_out = nullptr);
+               int *slot_out = nullptr, int cap = 768);
+int spmm_b2_stage(lz_handle *h, int64_t n, const int64_t *rp, int *cap);  // host sync
 // the same two passes at any b <= 32, fp64 or fp32 (b = 32 fp32: the MFMA kernels above;
 // otherwise VALU kernels); slabs of b x b doubles in h->partials
 template <typename T>

@@ -1273,19 +1273,52 @@ bool spmm_b2_ok(int64_t n, int64_t nnz, int64_t nx)
     return nx * 32 * (int64_t)sizeof(float) < (1LL << 31) && nx < (1 << 24) && (double)nnz <= 13.0 * (double)n;
 }
 
+// 48-row tiles whose CSR run exceeds `cap` entries (one thread a tile)
+__global__ __launch_bounds__(256) void k_tile_overflow(int64_t n, const int64_t *__restrict__ rp, int cap,
+                                                       int *__restrict__ count)
+{
+    const int64_t t = (int64_t)blockIdx.x * 256 + threadIdx.x, r0 = t * 48;
+    const bool over = r0 < n && rp[r0 + 48 < n ? r0 + 48 : n] - rp[r0] > cap;
+    const uint64_t b = __ballot(over);
+    if ((threadIdx.x & 63) == 0 && b) atomicAdd(count, __popcll(b));
+}
+
+int spmm_b2_stage(lz_handle *h, int64_t n, const int64_t *rp, int *cap)
+{
+    // The stage of the beta^2 SpMM, once per solve: 1024 entries where more
+    // than 1 % of the 48-row tiles hold over 1024 (a heavy tail of long rows,
+    // C5's power-law operator: 3.0 %; fewer tiles then go to the long-tile
+    // pass, at 6 blocks per CU instead of 7: SpMM 2.888-2.893 -> 2.821-2.824
+    // ms), 768 otherwise (1024 costs 7-8 % on banded and uniform-random
+    // operators, whose tiles stay under 1024: 0 %, even where 3 % exceed
+    // 768).  profiles/r05zz6_c5_tile_shape_ab.log, r05zzf_b2_stage_ab.log
+    *cap = 768;
+    if (n <= 0) return LZ_OK;
+    const int64_t tiles = ceil_div(n, (int64_t)48);
+    int *dcount = reinterpret_cast<int *>(h->scratch + 4 * kMaxB * kMaxB - 1);  // (one spare word)
+    LZ_HIP_TRY(hipMemsetAsync(dcount, 0, sizeof(int), h->stream));
+    hipLaunchKernelGGL(k_tile_overflow, dim3((unsigned)ceil_div(tiles, (int64_t)256)), dim3(256), 0, h->stream, n, rp,
+                       1024, dcount);
+    LZ_LAUNCH_CHECK();
+    int over = 0;
+    LZ_HIP_TRY(hipMemcpyAsync(&over, dcount, sizeof(int), hipMemcpyDeviceToHost, h->stream));
+    LZ_HIP_TRY(hipStreamSynchronize(h->stream));
+    if ((double)over > 0.01 * (double)tiles) *cap = 1024;
+    return LZ_OK;
+}
+
 int spmm_rm_b2(lz_handle *h, int64_t n, int64_t nnz, const int64_t *rp, const int32_t *col, const float *val,
-               const float *X, int64_t nx, float *Y, const float *Wp, const float *Mm, int plan_slot, int *slot_out)
+               const float *X, int64_t nx, float *Y, const float *Wp, const float *Mm, int plan_slot, int *slot_out,
+               int cap)
 {
     LZ_ARG_CHECK(spmm_b2_ok(n, nnz, nx), "beta^2 SpMM epilogue: shape not covered");
+    LZ_ARG_CHECK(cap == 768 || cap == 1024, "beta^2 SpMM stage: 768 or 1024 (spmm_b2_stage)");
     if (n <= 0) return LZ_OK;
     const int ev = prof_begin(h, PROF_SPMM);
-    // a 1024-entry stage (not the plain SpMM's 768): fewer power-law tiles
-    // overflow to the long-tile pass, at 6 blocks per CU instead of 7.  C5
-    // SpMM 2.894-2.901 -> 2.828-2.833 ms; stages of 896 / 1152 / 1280 (64-row
-    // tiles) / 1536: 2.874-2.877 / 2.939-2.942 / 2.833-2.845 / 2.924-2.929
-    // (profiles/r05zz6_c5_tile_shape_ab.log, alternating processes)
-    const int rc = launch_seg<float, 32, 48, 1024, false, false, true>(h, n, rp, col, val, X, 32, nx, Y, 32, Wp, Mm,
-                                                                       plan_slot, slot_out);
+    const int rc = cap == 1024 ? launch_seg<float, 32, 48, 1024, false, false, true>(h, n, rp, col, val, X, 32, nx, Y,
+                                                                                   32, Wp, Mm, plan_slot, slot_out)
+                               : launch_seg<float, 32, 48, 768, false, false, true>(h, n, rp, col, val, X, 32, nx, Y, 32,
+                                                                                  Wp, Mm, plan_slot, slot_out);
     prof_end(h, ev);
     LZ_TRY(rc);
     LZ_LAUNCH_CHECK();

@@ -22,11 +22,15 @@ def main():
     ap.add_argument("cfgs", nargs="+")
     ap.add_argument("--rounds", type=int, default=3)
     ap.add_argument("--steps", type=int, default=10)
+    ap.add_argument("--banded", type=int, default=0, help="a banded operator of this half width instead (10 nnz/row)")
     args = ap.parse_args()
     lz = ge.load_package()
     h = lz.Handle(0)
     n, b, m = 10_000_000, 32, args.steps
-    A = lz.gen_powerlaw(n, 10.0, 2.1, 100000, seed=20261015, dtype=np.float32)
+    if args.banded:
+        A = lz.gen_banded(n, 10.0, args.banded, 20261015, dtype=np.float32)
+    else:
+        A = lz.gen_powerlaw(n, 10.0, 2.1, 100000, seed=20261015, dtype=np.float32)
     Ad = lz.CsrDevice.from_host(A)
     B = torch.from_numpy(lz.uniform_B(n, b, 20261015, dtype=np.float32)).cuda()
     kw = dict(dtype=torch.float32, device="cuda")
