@@ -170,9 +170,11 @@ int lz_copy_row(lz_handle *h, int b, lz_dtype dtype, const void *Q, int64_t ld, 
  * That costs one row-local pass per call; lz_set_final_state(h, 0) skips it
  * for callers that never read the three blocks (they are then scratch).
  * Fused device-resident iteration: no host synchronisation inside the steps;
- * every output stays on the device.  At b = 16 fp64 the call ends with one
- * host synchronisation, to read the device error word of the step kernels
- * (LZ_E_DEVICE when one of them abandoned a bounded wait).
+ * every output stays on the device.  Before the first step one value is read
+ * back (one host synchronisation): the b = 16 fp64 wavefront step's plan, the
+ * b = 32 fp32 SpMM's stage choice.  At b = 16 fp64 the call also ends with
+ * one, to read the device error word of the step kernels (LZ_E_DEVICE when one
+ * of them abandoned a bounded wait).
  * The b = 16 fp64 step kernels keep one workgroup on every CU and their
  * workgroups wait on each other's progress: the launch is checked for
  * co-residency, and no kernel that itself waits on the solve's results may
