@@ -386,21 +386,27 @@ static int block_lanczos_b2_32(lz_handle *h, int64_t n, int64_t nnz, const int64
     float *sc = reinterpret_cast<float *>(h->scratch + 4 * kMaxB * kMaxB);
     float *binv[2] = {sc, sc + bb}, *P2 = sc + 2 * bb, *M = sc + 3 * bb;
     float *U = Q0;
-    int np = 0, cap = 768;
+    int np = 0, cap = 768, lslot = -1;
     LZ_TRY(spmm_b2_stage(h, n, rp, &cap));  // (the solve's one host sync, before any of its work)
+#ifndef LZ_B2_STEP0_QUEUES  // (measurement build: step 0 queues the list itself, as before round 5's end)
+    LZ_TRY(spmm_b2_plan(h, n, rp, cap, &lslot));
+#endif
     LZ_TRY(gram_partials<float>(h, n, b, B, B, b, &np));
     LZ_TRY(sqrtm_pair<float>(h, b, nullptr, np, beta, binv[0], nullptr));
     const float *in = B, *prev = nullptr;
     float *r0 = (m & 1) ? W : Q1, *r1 = (m & 1) ? Q1 : W;  // W_m lands in W (residual_order)
-    int lslot = -1;  // the long-tile list step 0's SpMM queued
     for (int j = 0; j < m; ++j) {
         float *out = j == 0 ? r0 : j == 1 ? r1 : const_cast<float *>(prev);
         const float *bi = binv[j & 1];
-        // from step 1 on the long-tile pass runs beside the tile pass, over the
-        // list step 0 queued (C5 step 4.401-4.411 -> 4.381-4.385 ms, each tile computed as before)
-        const int plan = j > 0 ? lslot : -1;
-        LZ_TRY(spmm_rm_b2(h, n, nnz, rp, col, val, in, n, U, prev, j ? M : nullptr, plan, j == 0 ? &lslot : nullptr,
-                          cap));
+        // the long-tile pass beside the tile pass, over the solve's list (from
+        // step 1 on: C5 step 4.401-4.411 -> 4.381-4.385 ms; step 0 too since
+        // the list is made up front; each tile computed as before)
+#ifndef LZ_B2_STEP0_QUEUES
+        LZ_TRY(spmm_rm_b2(h, n, nnz, rp, col, val, in, n, U, prev, j ? M : nullptr, lslot, nullptr, cap));
+#else
+        LZ_TRY(spmm_rm_b2(h, n, nnz, rp, col, val, in, n, U, prev, j ? M : nullptr, j ? lslot : -1,
+                          j ? nullptr : &lslot, cap));
+#endif
         if (j > 0) LZ_HIP_TRY(hipStreamWaitEvent(h->stream, h->ev_join, 0));
         LZ_TRY(fused_el32(h, n, in, U, &np));
         // the one-workgroup kernels read 32 folded slabs, not the passes' 1024

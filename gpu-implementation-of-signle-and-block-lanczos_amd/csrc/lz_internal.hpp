@@ -184,6 +184,9 @@ int spmm_rm_b2(lz_handle *h, int64_t n, int64_t nnz, const int64_t *rp, const in
                const float *X, int64_t nx, float *Y, const float *Wp, const float *Mm, int plan_slot = -1,
                int *slot_out = nullptr, int cap = 768);
 int spmm_b2_stage(lz_handle *h, int64_t n, const int64_t *rp, int *cap);  // host sync
+// the long-tile list for that stage, before the solve's first SpMM: every call
+// of the solve then runs planned (plan_slot = *slot)
+int spmm_b2_plan(lz_handle *h, int64_t n, const int64_t *rp, int cap, int *slot);
 // the same two passes at any b <= 32, fp64 or fp32 (b = 32 fp32: the MFMA kernels above;
 // otherwise VALU kernels); slabs of b x b doubles in h->partials
 template <typename T>

@@ -1142,18 +1142,9 @@ static int launch_fnz(lz_handle *h, int64_t nnz, const T *val, const T *X, int64
     return LZ_OK;
 }
 
-// nnz-split SpMM with the long-tile queue: the main kernel, then a persistent
-// kernel over the queued tiles (an empty queue costs one short launch).
-// plan_slot >= 0: the long tiles an earlier call on the same operator queued
-// (count slot plan_slot, *slot_out of that call) -- the long-tile pass runs
-// first, on its own stream, beside the main kernel, which then only skips them.
-template <typename T, int B, int TR, int CAP, bool WIN, bool YCM = false, bool EPI = false>
-static int launch_seg(lz_handle *h, int64_t n, const int64_t *rp, const int32_t *col, const T *val, const T *X,
-                      int64_t ldx, int64_t nx, T *Y, int64_t ldy, const T *Wp = nullptr, const T *Mm = nullptr,
-                      int plan_slot = -1, int *slot_out = nullptr)
+// the long-tile queue for st tiles: count slots longq[0..1], then the list
+static int ensure_longq(lz_handle *h, int64_t st)
 {
-    const int64_t st = ceil_div(n, (int64_t)TR);
-    LZ_ARG_CHECK(st < (1LL << 31), "too many row tiles");
     if ((size_t)st + 2 > h->longq_cap) {
         LZ_HIP_TRY(hipStreamSynchronize(h->stream));
         (void)hipFree(h->longq);
@@ -1168,6 +1159,23 @@ static int launch_seg(lz_handle *h, int64_t n, const int64_t *rp, const int32_t 
         h->longq_cap = (size_t)st + 2;
         h->longq_parity = 0;
     }
+    return LZ_OK;
+}
+
+// nnz-split SpMM with the long-tile queue: the main kernel, then a persistent
+// kernel over the queued tiles (an empty queue costs one short launch).
+// plan_slot >= 0: the long tiles an earlier call on the same operator queued
+// (count slot plan_slot, *slot_out of that call, or a list spmm_b2_plan made
+// up front) -- the long-tile pass runs
+// first, on its own stream, beside the main kernel, which then only skips them.
+template <typename T, int B, int TR, int CAP, bool WIN, bool YCM = false, bool EPI = false>
+static int launch_seg(lz_handle *h, int64_t n, const int64_t *rp, const int32_t *col, const T *val, const T *X,
+                      int64_t ldx, int64_t nx, T *Y, int64_t ldy, const T *Wp = nullptr, const T *Mm = nullptr,
+                      int plan_slot = -1, int *slot_out = nullptr)
+{
+    const int64_t st = ceil_div(n, (int64_t)TR);
+    LZ_ARG_CHECK(st < (1LL << 31), "too many row tiles");
+    LZ_TRY(ensure_longq(h, st));
     if (plan_slot >= 0) {
         LZ_ARG_CHECK(plan_slot <= 1 && (size_t)st + 2 <= h->longq_cap, "planned SpMM: no earlier queue");
         if (!h->lstream) {
@@ -1304,6 +1312,35 @@ int spmm_b2_stage(lz_handle *h, int64_t n, const int64_t *rp, int *cap)
     LZ_HIP_TRY(hipMemcpyAsync(&over, dcount, sizeof(int), hipMemcpyDeviceToHost, h->stream));
     LZ_HIP_TRY(hipStreamSynchronize(h->stream));
     if ((double)over > 0.01 * (double)tiles) *cap = 1024;
+    return LZ_OK;
+}
+
+// the long-tile list of the solve, before its first SpMM: every 48-row tile
+// whose run exceeds cap, so that the first step's long-tile pass can also run
+// beside its tile pass (the tile pass in planned mode only skips them; the
+// list order does not matter: each listed tile is computed by one block, in
+// chunk order)
+__global__ __launch_bounds__(256) void k_tile_list(int64_t n, const int64_t *__restrict__ rp, int cap,
+                                                   int *__restrict__ count, int *__restrict__ list)
+{
+    const int64_t t = (int64_t)blockIdx.x * 256 + threadIdx.x, r0 = t * 48;
+    if (r0 < n && rp[r0 + 48 < n ? r0 + 48 : n] - rp[r0] > cap) list[atomicAdd(count, 1)] = (int)t;
+}
+
+int spmm_b2_plan(lz_handle *h, int64_t n, const int64_t *rp, int cap, int *slot)
+{
+    const int64_t st = ceil_div(n, (int64_t)48);
+    LZ_ARG_CHECK(st < (1LL << 31), "too many row tiles");
+    LZ_TRY(ensure_longq(h, st));
+    *slot = h->longq_parity;
+    h->longq_parity ^= 1;
+    // both counts zeroed: this list's, and the next unplanned call's (which
+    // expects its slot at zero, as an unplanned call leaves the other one)
+    LZ_HIP_TRY(hipMemsetAsync(h->longq, 0, 2 * sizeof(int), h->stream));
+    if (n <= 0) return LZ_OK;
+    hipLaunchKernelGGL(k_tile_list, dim3((unsigned)ceil_div(st, (int64_t)256)), dim3(256), 0, h->stream, n, rp, cap,
+                       h->longq + *slot, h->longq + 2);
+    LZ_LAUNCH_CHECK();
     return LZ_OK;
 }
 
