@@ -386,6 +386,14 @@ static int block_lanczos_b2_32(lz_handle *h, int64_t n, int64_t nnz, const int64
     float *sc = reinterpret_cast<float *>(h->scratch + 4 * kMaxB * kMaxB);
     float *binv[2] = {sc, sc + bb}, *P2 = sc + 2 * bb, *M = sc + 3 * bb;
     float *U = Q0;
+    // every return leaves the handle's stream behind the side stream's sqrtm
+    // of the next step's G: an early error return too.  (beta_0's Gram and
+    // sqrtm beside step 0's SpMM measured a wash: the SpMM paid the Gram's
+    // bandwidth, profiles/r05zzs_c5_gram0_beside_ab.log)
+    struct JoinSide {
+        lz_handle *h;
+        ~JoinSide() { (void)hipStreamWaitEvent(h->stream, h->ev_join, 0); }
+    } join_side{h};
     int np = 0, cap = 768, lslot = -1;
     LZ_TRY(spmm_b2_stage(h, n, rp, &cap));  // (the solve's one host sync, before any of its work)
 #ifndef LZ_B2_STEP0_QUEUES  // (measurement build: step 0 queues the list itself, as before round 5's end)
