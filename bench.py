@@ -19,6 +19,10 @@ HBM.
 At N > 1 (either config) the line reports the `--exchange` form (halo by
 default) as `value` and times the other form (the north star's RCCL
 all-gather) beside it on the same partition (extra.other_exchange).
+`--gpus N` runs N ranks: under torch.distributed.run as given (WORLD_SIZE
+must equal N, else the run fails), or, with WORLD_SIZE unset and N > 1, by
+starting `python -m torch.distributed.run --nproc-per-node N ... bench.py`
+as a child process before anything touches the GPU and relaying its line.
 
 After the timed region the run checks itself: the device error word must be
 0 (no persistent kernel abandoned a bounded spin) and, on one GPU, the first
@@ -282,8 +286,58 @@ def parse_args():
     return args
 
 
+def world_plan(gpus: int, env) -> str:
+    """What `bench.py --gpus N` does in this environment, decided before anything
+    touches the GPU: "run" (this process is the job, or one rank of it: WORLD_SIZE
+    unset and N = 1, or WORLD_SIZE == N) or "launch" (WORLD_SIZE unset and N > 1:
+    start N local ranks under torch.distributed.run as a child process).  A
+    WORLD_SIZE that disagrees with --gpus is an error: a line for another N than
+    the one asked for is never printed."""
+    if gpus < 1:
+        raise SystemExit(f"bench.py: --gpus {gpus}: at least 1")
+    w = env.get("WORLD_SIZE")
+    if w is None or w == "":
+        return "launch" if gpus > 1 else "run"
+    if int(w) != gpus:
+        raise SystemExit(f"bench.py: --gpus {gpus} but WORLD_SIZE={w}: refusing to report a {w}-rank run "
+                         f"as {gpus} GPUs")
+    return "run"
+
+
+def free_port() -> int:
+    import socket
+    with socket.socket(socket.AF_INET, socket.SOCK_STREAM) as s:
+        s.bind(("127.0.0.1", 0))
+        return int(s.getsockname()[1])
+
+
+def launch_cmd(argv, gpus: int, port: int):
+    """The torch.distributed.run command that starts `gpus` ranks of this script
+    with the same arguments (one process per GPU, rendezvous on 127.0.0.1)."""
+    return [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={gpus}",
+            "--master-addr", "127.0.0.1", f"--master-port={port}", os.path.abspath(__file__)] + list(argv)
+
+
+def relay(cmd, out=None) -> int:
+    """Run cmd as a child process (this process has not touched the GPU, and
+    never execs); its stderr passes through, its stdout -- rank 0's one JSON
+    line -- is copied to ours.  Returns the child's exit status."""
+    import subprocess
+    out = out or sys.stdout
+    p = subprocess.run(cmd, stdout=subprocess.PIPE, stderr=None, text=True)
+    if p.stdout:
+        out.write(p.stdout)
+        out.flush()
+    return p.returncode
+
+
 def main():
     args = parse_args()
+    if args.config == "c4rank" and args.gpus != 1:
+        raise SystemExit("--config c4rank runs one rank's share on ONE GPU (the 8-GPU run is --config c4)")
+    if world_plan(args.gpus, os.environ) == "launch":
+        log(f"bench.py: --gpus {args.gpus} without WORLD_SIZE: starting {args.gpus} ranks under torch.distributed.run")
+        sys.exit(relay(launch_cmd(sys.argv[1:], args.gpus, free_port())))
     # Native libraries write to fd 1 (RCCL prints a version banner at communicator
     # init): route fd 1 to stderr and keep the real stdout for the one JSON line.
     sys.stdout.flush()
@@ -296,8 +350,7 @@ def main():
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
-    if world != args.gpus:
-        log(f"note: --gpus {args.gpus} but WORLD_SIZE={world}; using WORLD_SIZE")
+    assert world == args.gpus  # world_plan
     torch.cuda.set_device(local)
     if world > 1:
         dist.init_process_group("nccl", device_id=torch.device("cuda", local))

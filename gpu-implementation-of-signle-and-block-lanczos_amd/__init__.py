@@ -61,8 +61,7 @@ HIP_SYMBOLS = [
     ("lz_device_error", _c_int, [_c_vp, ctypes.POINTER(_c_int)]),
     ("lz_debug_poison_lds", _c_int, [_c_vp, ctypes.c_uint32]),
     ("lz_debug_set_device_error", _c_int, [_c_vp, _c_int]),
-    ("lz_debug_spmm_panel", _c_int, [_c_vp, _c_i64, _c_i64, _c_vp, _c_vp, _c_int, _c_vp, _c_vp, _c_vp, _c_vp,
-                                     _c_vp, _c_vp]),
+    ("lz_debug_fail_next_setup", _c_int, [_c_vp, _c_int]),
     ("lz_prof_enable", _c_int, [_c_vp, _c_int]),
     ("lz_prof_enable_mask", _c_int, [_c_vp, ctypes.c_uint]),
     ("lz_prof_read", _c_int, [_c_vp, _c_int, ctypes.POINTER(_c_dbl), ctypes.POINTER(_c_int)]),
@@ -444,87 +443,6 @@ class CsrDevice:
                          torch.from_numpy(A.val).to(device))
 
 
-# ------------------------------------------------ column-panel SpMM (candidate)
-PANEL_ROWS, PANEL_WIDTH, PANEL_MAX_ENTRIES, PANEL_GOFF = 2048, 512, 1536, 136
-
-
-@dataclass
-class PanelPlan:
-    """The column-panel SpMM's once-per-operator plan (lz_debug_spmm_panel, host
-    arrays): passes = (row block, 512-row X panel, up to 1536 entries)."""
-    n: int
-    nblocks: int
-    bp0: np.ndarray    # int32 [nblocks + 1]
-    px0: np.ndarray    # int32 [npass]
-    pe0: np.ndarray    # int32 [npass + 1]
-    goff: np.ndarray   # uint16 [npass * 136]
-    ev: np.ndarray     # float64 [pe0[-1]]
-    ex: np.ndarray     # uint16 [pe0[-1]]
-
-    def device(self, device="cuda"):
-        torch = _torch()
-        return {k: torch.from_numpy(getattr(self, k)).to(device) for k in ("bp0", "px0", "pe0", "goff", "ev", "ex")}
-
-
-def panel_plan(A: "CsrHost") -> PanelPlan:
-    """For every block of 2048 rows, its entries regrouped by the 512-row X panel
-    their column falls in (panels from the block's smallest column), CSR order
-    kept inside a panel (so by row, then column), a panel of more than 1536
-    entries split over several passes, each pass padded to 8 entries; entry
-    word = (row % 16) << 9 | (column - panel start); group offsets = where each
-    16-row group's entries start in the pass."""
-    R, W, E, GO = PANEL_ROWS, PANEL_WIDTH, PANEL_MAX_ENTRIES, PANEL_GOFF
-    n, rp, col = A.n, A.row_ptr.astype(np.int64), A.col
-    nb = (n + R - 1) // R
-    cnt = np.diff(rp)
-    rows = np.repeat(np.arange(n, dtype=np.int64), cnt)
-    blk = rows // R
-    starts = rp[np.minimum(np.arange(nb, dtype=np.int64) * R, n)]
-    has = np.diff(np.append(starts, rp[n])) > 0
-    base = np.zeros(nb, np.int64)
-    if has.any():  # (an empty block contributes no entries, so each segment ends at the next one's start)
-        base[has] = np.minimum.reduceat(col, starts[has])
-    rel = col.astype(np.int64) - base[blk]
-    p = rel // W
-    maxp = int(p.max()) + 1 if p.size else 1
-    key = blk * maxp + p
-    order = np.argsort(key, kind="stable")
-    key_s = key[order]
-    # segments (block, panel) and their split into passes of <= E entries
-    seg_start = np.flatnonzero(np.r_[True, key_s[1:] != key_s[:-1]]) if key_s.size else np.zeros(0, np.int64)
-    seg_len = np.diff(np.r_[seg_start, key_s.size])
-    seg_pass = (seg_len + E - 1) // E
-    pass_base = np.r_[0, np.cumsum(seg_pass)[:-1]]
-    npass = int(seg_pass.sum())
-    seg_of = np.repeat(np.arange(seg_start.size), seg_len)
-    idx_in_seg = np.arange(key_s.size) - seg_start[seg_of]
-    pid = pass_base[seg_of] + idx_in_seg // E
-    pass_cnt = np.bincount(pid, minlength=npass)
-    pad = (pass_cnt + 7) // 8 * 8
-    pe0 = np.r_[0, np.cumsum(pad)].astype(np.int64)
-    pass_first = np.r_[0, np.cumsum(pass_cnt)[:-1]]
-    dest = pe0[pid] + (np.arange(key_s.size) - pass_first[pid])
-    rows_s = rows[order]
-    ev = np.zeros(int(pe0[-1]), np.float64)
-    ex = np.zeros(int(pe0[-1]), np.uint16)
-    ev[dest] = A.val[order]
-    ex[dest] = (((rows_s % 16) << 9) | (rel[order] % W)).astype(np.uint16)
-    g = (rows_s % R) // 16
-    gc = np.bincount(pid * 128 + g, minlength=npass * 128).reshape(npass, 128) if npass else \
-        np.zeros((0, 128), np.int64)
-    goff = np.zeros((npass, GO), np.uint16)
-    goff[:, 1:129] = np.cumsum(gc, axis=1)
-    seg_blk = key_s[seg_start] // maxp
-    seg_p = key_s[seg_start] % maxp
-    pass_seg = np.repeat(np.arange(seg_start.size), seg_pass)
-    px0 = (base[seg_blk[pass_seg]] + seg_p[pass_seg] * W).astype(np.int32)
-    pass_blk = seg_blk[pass_seg]
-    bp0 = np.searchsorted(pass_blk, np.arange(nb + 1)).astype(np.int32)
-    if pe0[-1] >= 2 ** 31:
-        raise LanczosError("panel plan: more than 2^31 entries")
-    return PanelPlan(n, nb, bp0, px0, pe0.astype(np.int32), goff.reshape(-1), ev, ex)
-
-
 class Handle:
     """lz_handle on one device, bound to torch's current stream at each call."""
 
@@ -567,15 +485,6 @@ class Handle:
         ldx, ldy = _ld(X), _ld(Y)
         _check(self.L.lz_csr_spmm(self.ptr, A.n, A.n_cols, A.nnz, _ptr(A.row_ptr), _ptr(A.col),
                                   _ptr(A.val), A.dtype, b, _ptr(X), ldx, layout, _ptr(Y), ldy), "lz_csr_spmm")
-        return Y
-
-    def spmm_panel(self, plan_dev: dict, n: int, nblocks: int, X, Y):
-        """Y = A X by the column-panel candidate (lz_debug_spmm_panel) from a
-        PanelPlan's device arrays; X (nx, 16) and Y (n, 16) fp64 row-major."""
-        d = plan_dev
-        _check(self.L.lz_debug_spmm_panel(self.ptr, n, X.shape[0], _ptr(X), _ptr(Y), nblocks, _ptr(d["bp0"]),
-                                          _ptr(d["px0"]), _ptr(d["pe0"]), _ptr(d["goff"]), _ptr(d["ev"]),
-                                          _ptr(d["ex"])), "lz_debug_spmm_panel")
         return Y
 
     def to_row_major(self, Xcm, Y):
@@ -665,6 +574,11 @@ class Handle:
     def debug_set_device_error(self, code: int):
         """Store `code` into the device error word (test support)."""
         _check(self.L.lz_debug_set_device_error(self.ptr, code), "lz_debug_set_device_error")
+
+    def debug_fail_next_setup(self, code: int = 5):
+        """The next distributed solve on this handle fails its set-up with `code`
+        on this rank (test support: its peers must return, not wait)."""
+        _check(self.L.lz_debug_fail_next_setup(self._h, code), "lz_debug_fail_next_setup")
 
     def debug_poison_lds(self, pattern: int = 0xFFFFFFFF):
         """Fill every CU's LDS with `pattern` (test support: stale-LDS reads show as NaN)."""

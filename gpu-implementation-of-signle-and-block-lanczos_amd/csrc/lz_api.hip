@@ -828,44 +828,79 @@ static int dist_solve_impl(lz_handle *h, int form, HaloPlan *hp, int64_t n, int6
     T *sc = reinterpret_cast<T *>(h->scratch + 4 * kMaxB * kMaxB);
     T *binv[2] = {sc, sc + bb}, *P = sc + 2 * bb;
     T *own = X0 + own_off * b;  // allgather: this rank's slot of X_full
-    // ---- once per solve (before any step: these may synchronise)
+    // ---- once per solve (before any step: these may synchronise).  Every
+    // set-up step that can fail runs before the solve's first collective, the
+    // ranks' vote below: a rank whose set-up failed still joins it, with
+    // ok = 0, so every rank returns an error instead of its peers waiting in a
+    // collective this rank never issues.
+    int prc = h->dbg_setup_fail;  // lz_debug_fail_next_setup (test support), consumed here
+    h->dbg_setup_fail = 0;
+    if (prc != LZ_OK) set_error("set-up failure forced by lz_debug_fail_next_setup");
     T *Y = nullptr;
-    if (!f16) {
-        LZ_TRY(grow_ws(h, &h->ybuf, &h->ybuf_cap, (size_t)std::max<int64_t>(n, 1) * rowb));
+    if (prc == LZ_OK && !f16) {
+        prc = grow_ws(h, &h->ybuf, &h->ybuf_cap, (size_t)std::max<int64_t>(n, 1) * rowb);
         Y = static_cast<T *>(h->ybuf);
     }
-    if (!ag && hp && cm && h->nranks > 1)
-        LZ_TRY(grow_ws(h, &hp->sendbuf, &hp->send_cap, (size_t)std::max<int64_t>(hp->n_send, 1) * rowb));
-    if constexpr (std::is_same<T, double>::value) {
-        // the wavefront step when it applies (LZ_PASS_WF=0: the two passes).  The
-        // all-gather form takes it at one rank, where its exchange moves nothing:
-        // at N > 1 the all-gather (the whole block from every peer; ~4.2 ms at C4
-        // on 8 GPUs) outlasts the step's compute, and the two-pass
-        // step hides the interior rows' pass 1 under it where the wavefront step,
-        // which needs the exchange between its pass 2 and the boundary tiles'
-        // pass 1, could hide nothing.  LZ_AG_WF=1 / 0 forces it on / off (tests).
-        const char *agw = getenv("LZ_AG_WF");
-        const bool ag_wf = agw ? agw[0] == '1' : h->nranks == 1;
-        if (f16 && (!ag || ag_wf)) {
-            WfPlan wp;
-            LZ_TRY(wf_plan16(h, n, nnz, rp, col, &wp, nx, own_off));
-            // beta_0's Gram from the first launch: the default shape (XO 1,
-            // dist_solve_wf16); the ranks must agree, as on the form itself
-            bool g0 = wp.var == 111;
-            if (cm && h->nranks > 1) {  // every rank takes the same form (their collectives must match)
-                double v[2] = {wp.ok ? 1.0 : 0.0, g0 ? 1.0 : 0.0};
-                LZ_HIP_TRY(hipMemcpyAsync(slab, v, sizeof(v), hipMemcpyHostToDevice, h->stream));
-                LZ_TRY(cm->allreduce_sum(slab, 2, h->stream));
-                LZ_HIP_TRY(hipMemcpyAsync(v, slab, sizeof(v), hipMemcpyDeviceToHost, h->stream));
-                LZ_HIP_TRY(hipStreamSynchronize(h->stream));
-                wp.ok = v[0] == (double)h->nranks;
-                g0 = v[1] == (double)h->nranks;
+    if (prc == LZ_OK && !ag && hp && cm && h->nranks > 1)
+        prc = grow_ws(h, &hp->sendbuf, &hp->send_cap, (size_t)std::max<int64_t>(hp->n_send, 1) * rowb);
+    // the wavefront step when it applies (LZ_PASS_WF=0: the two passes).  The
+    // all-gather form takes it at one rank, where its exchange moves nothing:
+    // at N > 1 the all-gather (the whole block from every peer; ~4.2 ms at C4
+    // on 8 GPUs) outlasts the step's compute, and the two-pass
+    // step hides the interior rows' pass 1 under it where the wavefront step,
+    // which needs the exchange between its pass 2 and the boundary tiles'
+    // pass 1, could hide nothing.  LZ_AG_WF=1 / 0 forces it on / off (tests).
+    const char *agw = getenv("LZ_AG_WF");
+    const bool ag_wf = agw ? agw[0] == '1' : h->nranks == 1;
+    const bool try_wf = std::is_same<T, double>::value && f16 && (!ag || ag_wf);
+    WfPlan wp;
+    bool g0 = false;  // beta_0's Gram from the first launch: the default shape (XO 1, dist_solve_wf16)
+    if (prc == LZ_OK && try_wf) {
+        prc = wf_plan16(h, n, nnz, rp, col, &wp, nx, own_off);
+        g0 = wp.var == 111;
+    }
+    Pass1Plan pl;
+    SplitPlan sp;
+    // the plans of the step form this rank expects (the vote may still turn
+    // the wavefront form down: then the two-pass plan follows the vote)
+    auto plan_twopass = [&]() -> int {
+        if (f16) LZ_TRY(pass1_plan(h, n, nnz, rp, col, nx, own_off, &pl));
+        if (!f16 || fused16_direct(nx, pl.win)) LZ_TRY(split_plan(h, n, rp, col, own_off, own_off + n, &sp));
+        return LZ_OK;
+    };
+    bool planned_twopass = false;
+    if (prc == LZ_OK && try_wf && wp.ok) prc = split_plan(h, n, rp, col, own_off, own_off + n, &sp);
+    if (prc == LZ_OK && !(try_wf && wp.ok)) {
+        prc = plan_twopass();
+        planned_twopass = true;
+    }
+    // ---- the vote: set-up ok on every rank, and (b = 16 fp64) the wavefront
+    // form and the first-launch Gram only where every rank can take them
+    // (their collectives must match)
+    if (cm && h->nranks > 1) {
+        double v[3] = {prc == LZ_OK ? 1.0 : 0.0, wp.ok ? 1.0 : 0.0, g0 ? 1.0 : 0.0};
+        LZ_HIP_TRY(hipMemcpyAsync(slab, v, sizeof(v), hipMemcpyHostToDevice, h->stream));
+        LZ_TRY(cm->allreduce_sum(slab, 3, h->stream));
+        LZ_HIP_TRY(hipMemcpyAsync(v, slab, sizeof(v), hipMemcpyDeviceToHost, h->stream));
+        LZ_HIP_TRY(hipStreamSynchronize(h->stream));
+        if (v[0] != (double)h->nranks) {
+            if (prc == LZ_OK) {
+                set_error("a peer rank failed its set-up of this distributed solve (%d of %d ok)", (int)v[0],
+                          h->nranks);
+                prc = LZ_E_STATE;
             }
+            return prc;
+        }
+        wp.ok = v[1] == (double)h->nranks;
+        g0 = v[2] == (double)h->nranks;
+    } else if (prc != LZ_OK) {
+        return prc;
+    }
+    if constexpr (std::is_same<T, double>::value) {
+        if (try_wf) {
             h->last_wf = wp.ok ? 1 : 0;
             h->last_wf_pre = 0;
             if (wp.ok) {
-                SplitPlan sp;
-                LZ_TRY(split_plan(h, n, rp, col, own_off, own_off + n, &sp));
                 h->last_split[0] = sp.on ? sp.i0 : -1;
                 h->last_split[1] = sp.on ? sp.i1 : -1;
                 return dist_solve_wf16(h, form, hp, n, n_pad, nnz, rp, col, val, m, lc, B, q, alpha, beta, X0, X1,
@@ -874,10 +909,8 @@ static int dist_solve_impl(lz_handle *h, int form, HaloPlan *hp, int64_t n, int6
         }
     }
     h->last_wf = h->last_wf_pre = 0;
-    Pass1Plan pl;
-    if (f16) LZ_TRY(pass1_plan(h, n, nnz, rp, col, nx, own_off, &pl));
-    SplitPlan sp;
-    if (!f16 || fused16_direct(nx, pl.win)) LZ_TRY(split_plan(h, n, rp, col, own_off, own_off + n, &sp));
+    // (only where a peer turned the wavefront form down after this rank planned it)
+    if (!planned_twopass) LZ_TRY(plan_twopass());
     h->last_split[0] = sp.on ? sp.i0 : -1;
     h->last_split[1] = sp.on ? sp.i1 : -1;
     const bool reduce = cm && (ag || h->nranks > 1);
@@ -1196,7 +1229,10 @@ using namespace lz;
 // collective return only when they poll ncclCommGetAsyncError or abort
 // themselves, so a failure before the first collective (arguments, workspace
 // growth, the plans) leaves the communicator usable, and the caller fails every
-// rank alike or calls lz_comm_abort.
+// rank alike or calls lz_comm_abort.  (Inside the solve, a set-up failure
+// joins the ranks' vote -- the solve's first collective -- with ok = 0, so its
+// peers return LZ_E_STATE rather than wait; dist_solve_impl.  Argument errors
+// the wrappers report before any work are the caller's to make rank-uniform.)
 // (LZ_E_DEVICE comes from the status read after the solve's closing fence: no
 // peer waits on this rank then, and the communicator stays usable.)
 static int dist_fail(lz_handle *h, int rc, uint64_t issued0)
@@ -1311,6 +1347,14 @@ int lz_finalize(lz_handle *h)
     if (h->ev_ljoin) (void)hipEventDestroy(h->ev_ljoin);
     if (h->lstream) (void)hipStreamDestroy(h->lstream);
     if (h->side) (void)hipStreamDestroy(h->side);
+    for (hipStream_t s : {h->pf_sg, h->pf_sp})
+        if (s) {
+            (void)hipStreamSynchronize(s);
+            (void)hipStreamDestroy(s);
+        }
+    for (hipEvent_t e : {h->ev_pff, h->ev_pfg, h->ev_pfp})
+        if (e) (void)hipEventDestroy(e);
+    (void)hipFree(h->pf_ctl);
     delete h;
     return LZ_OK;
 }
@@ -1330,6 +1374,13 @@ int lz_debug_set_device_error(lz_handle *h, int code)
 {
     LZ_HANDLE_CHECK(h);
     LZ_HIP_TRY(hipMemsetD32Async(reinterpret_cast<hipDeviceptr_t>(h->err_flag), code, 1, h->stream));
+    return LZ_OK;
+}
+
+int lz_debug_fail_next_setup(lz_handle *h, int code)
+{
+    LZ_HANDLE_CHECK(h);
+    h->dbg_setup_fail = code;
     return LZ_OK;
 }
 

@@ -87,6 +87,7 @@ struct lz_handle {
     // lz_block_lanczos leaves Q0 = Q1 = Q_{m-1}, W = W_m as the reference does
     // (one row-local pass per solve); lz_set_final_state(h, 0) skips that pass
     int final_state = 1;
+    int dbg_setup_fail = 0;       // lz_debug_fail_next_setup: the next distributed set-up's forced status
     // fixed-nnz SpMM format (experiment, lz_spmm.hip fnz_prepare): the operator's
     // columns with row-end flags and each tile's first row, keyed by the operator
     void *c16buf = nullptr;       // pass 1's 16-bit columns (col16_plan), nnz int16
@@ -110,6 +111,13 @@ struct lz_handle {
     // same solve queued) runs on its own stream beside the tile pass
     hipStream_t lstream = nullptr;
     hipEvent_t ev_lfork = nullptr, ev_ljoin = nullptr;
+    // CU-partitioned SpMM (LZ_SPMM_PF, lz_spmm.hip launch_seg_pf): the tile
+    // kernel's and the prefetch kernel's CU-masked streams, their fork / join
+    // events, the control words, the mask split they were made for
+    hipStream_t pf_sg = nullptr, pf_sp = nullptr;
+    hipEvent_t ev_pff = nullptr, ev_pfg = nullptr, ev_pfp = nullptr;
+    int *pf_ctl = nullptr;
+    int pf_key = -1;
     size_t pairs_cap = 0;         // entries
     void *cm_buf = nullptr;       // column-major SpMM: row-major copies of X and Y
     size_t cm_cap = 0;            // bytes

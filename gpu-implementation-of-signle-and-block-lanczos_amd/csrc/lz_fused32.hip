@@ -260,6 +260,135 @@ __global__ __launch_bounds__(64 * kF32Waves) void k_fused_ub32(int64_t n, const 
     block_slab32<kF32Waves>(red, g, lane, w, part);
 }
 
+// Pass UB with coalesced operand loads (round 6; LZ_UB_DMA=0 selects
+// k_fused_ub32 above).  aop32 has each lane read its own row's half, so one
+// load instruction touches 32 different 128-B lines (32 B of each) and the
+// next three touch them again: pass UB moved its 3 n b s at 4.1 TB/s where
+// pass EL, whose instructions read whole rows, reached 5.7.  Here each wave
+// pulls its 32-row strip of U and of W_j into LDS by LDS-DMA, 16 B per lane,
+// 1 KB (8 whole rows) per instruction, one strip ahead of the one it
+// computes; each lane's global piece is chosen so the strip lands XOR-swizzled
+// (row r's 16-B chunk c at position 8 r + (c ^ (r & 7))), and the MFMA
+// A-operands -- a lane's 64 contiguous bytes of its row -- come back as four
+// conflict-free ds_read_b128.  The products, their order and the stores are
+// k_fused_ub32's, so the results are the same bits.
+__device__ __forceinline__ __amdgpu_buffer_rsrc_t ub_rsrc(const float *p, int64_t rows)
+{
+    return __builtin_amdgcn_make_buffer_rsrc(const_cast<float *>(p), (short)0, (int)(rows * 128), 0x00020000);
+}
+
+template <bool QO>
+__global__ __launch_bounds__(64 * kF32Waves) void k_fused_ub32d(int64_t n, const float *U, const float *Wj,
+                                                                const float *__restrict__ binv,
+                                                                const float *__restrict__ P2, float *__restrict__ Wn,
+                                                                double *__restrict__ part, float *Qa, float *Qb)
+{
+    // per wave: two slots x (U strip, W_j strip) of 4 KB; the block slab's
+    // reduction reuses the same memory after the loop
+    __shared__ __attribute__((aligned(16))) float ust[kF32Waves][2][2][1024];
+    const int lane = threadIdx.x & 63, w = threadIdx.x >> 6, hh = lane >> 5, jr = lane & 31;
+    float bo[16], po[16];
+    bop32(binv, 1.0f, hh, jr, bo);
+    bop32(P2, -1.0f, hh, jr, po);
+    f16v_t g;
+#pragma unroll
+    for (int v = 0; v < 16; ++v) g[v] = 0.0f;
+    XcdSched sch(ceil_div(n, (int64_t)(32 * kF32Waves)));
+    const int64_t nst = sch.end > sch.begin ? (sch.end - sch.begin + sch.step - 1) / sch.step : 0;
+    // DMA piece of this lane: LDS position 64 k + lane holds row 8 k + lane / 8,
+    // chunk (lane & 7) ^ ((lane >> 3) & 7) of the strip
+    const uint32_t goff = (uint32_t)((lane >> 3) * 128 + 16 * ((lane & 7) ^ ((lane >> 3) & 7)));
+    // this lane's A-operand chunks 4 hh + cc of row jr
+    const uint32_t rbase = (uint32_t)(jr * 128);
+    auto dma = [&](int64_t s) {
+        const int slot = (int)(s & 1);
+        const int64_t r0 = (sch.begin + s * sch.step) * (32 * kF32Waves) + 32 * w;
+        const int64_t rows = s < nst && r0 < n ? (n - r0 < 32 ? n - r0 : 32) : 0;
+        const __amdgpu_buffer_rsrc_t ur = ub_rsrc(U + (rows ? r0 * 32 : 0), rows);
+        const __amdgpu_buffer_rsrc_t wr = ub_rsrc(Wj + (rows ? r0 * 32 : 0), rows);
+#pragma unroll
+        for (int k = 0; k < 4; ++k) {  // rows past the strip's end: out of range, land as zeros
+            __builtin_amdgcn_raw_ptr_buffer_load_lds(ur, (ws_lds_t *)&ust[w][slot][0][256 * k], 16, goff + 1024 * k, 0, 0, 0);
+            __builtin_amdgcn_raw_ptr_buffer_load_lds(wr, (ws_lds_t *)&ust[w][slot][1][256 * k], 16, goff + 1024 * k, 0, 0, 0);
+        }
+    };
+    constexpr int ST = QO ? 48 : 16;  // store instructions per strip
+    dma(0);
+    for (int64_t s = 0; s < nst; ++s) {
+        dma(s + 1);
+        // strip s landed: strip s + 1's 8 DMAs, and from s = 1 on strip s - 1's
+        // stores, were issued after it
+        if (s == 0) asm volatile("s_waitcnt vmcnt(8)" ::: "memory");
+        else asm volatile("s_waitcnt vmcnt(%0)" ::"n"(8 + ST) : "memory");
+        const uint32_t sb = ws_lds_addr(reinterpret_cast<int *>(&ust[w][(int)(s & 1)][0][0]));
+        float4 u4[4], w4[4];
+        const uint32_t o0 = sb + rbase + 16u * (uint32_t)((4 * hh + 0) ^ (jr & 7)),
+                       o1 = sb + rbase + 16u * (uint32_t)((4 * hh + 1) ^ (jr & 7)),
+                       o2 = sb + rbase + 16u * (uint32_t)((4 * hh + 2) ^ (jr & 7)),
+                       o3 = sb + rbase + 16u * (uint32_t)((4 * hh + 3) ^ (jr & 7));
+        asm volatile(
+            "ds_read_b128 %0, %8\n\t"
+            "ds_read_b128 %1, %9\n\t"
+            "ds_read_b128 %2, %10\n\t"
+            "ds_read_b128 %3, %11\n\t"
+            "ds_read_b128 %4, %8 offset:4096\n\t"
+            "ds_read_b128 %5, %9 offset:4096\n\t"
+            "ds_read_b128 %6, %10 offset:4096\n\t"
+            "ds_read_b128 %7, %11 offset:4096\n\t"
+            "s_waitcnt lgkmcnt(0)"
+            : "=&v"(u4[0]), "=&v"(u4[1]), "=&v"(u4[2]), "=&v"(u4[3]), "=&v"(w4[0]), "=&v"(w4[1]), "=&v"(w4[2]),
+              "=&v"(w4[3])
+            : "v"(o0), "v"(o1), "v"(o2), "v"(o3)
+            : "memory");
+        float ua[16], wa[16];
+#pragma unroll
+        for (int c = 0; c < 4; ++c) {
+            ua[4 * c] = u4[c].x; ua[4 * c + 1] = u4[c].y; ua[4 * c + 2] = u4[c].z; ua[4 * c + 3] = u4[c].w;
+            wa[4 * c] = w4[c].x; wa[4 * c + 1] = w4[c].y; wa[4 * c + 2] = w4[c].z; wa[4 * c + 3] = w4[c].w;
+        }
+        const int64_t r0 = (sch.begin + s * sch.step) * (32 * kF32Waves) + 32 * w;
+        f16v_t acc, acc2;  // two independent chains (each MFMA waits on its predecessor)
+#pragma unroll
+        for (int v = 0; v < 16; ++v) acc[v] = acc2[v] = 0.0f;
+#pragma unroll
+        for (int s2 = 0; s2 < 16; ++s2) {
+            acc = mfma32(ua[s2], bo[s2], acc);    // U beta^-1
+            acc2 = mfma32(wa[s2], po[s2], acc2);  // - W_j P2
+        }
+#pragma unroll
+        for (int v = 0; v < 16; ++v) acc[v] += acc2[v];
+        // (every strip issues exactly ST stores, rows past n to an out-of-range
+        // offset, so the vmcnt arithmetic above holds for the last strip too)
+        const __amdgpu_buffer_rsrc_t nr = ub_rsrc(Wn + (r0 < n ? r0 * 32 : 0), r0 < n ? (n - r0 < 32 ? n - r0 : 32) : 0);
+#pragma unroll
+        for (int v = 0; v < 16; ++v) {
+            const uint32_t rr = (uint32_t)((v & 3) + 8 * (v >> 2) + 4 * hh);
+            __builtin_amdgcn_raw_buffer_store_b32(__builtin_bit_cast(uint32_t, acc[v]), nr, rr * 128 + 4 * jr, 0, 0);
+        }
+        if constexpr (QO) {
+            f16v_t q;
+#pragma unroll
+            for (int v = 0; v < 16; ++v) q[v] = 0.0f;
+#pragma unroll
+            for (int s2 = 0; s2 < 16; ++s2) q = mfma32(wa[s2], bo[s2], q);  // W_j beta^-1
+            const int64_t nrow = r0 < n ? (n - r0 < 32 ? n - r0 : 32) : 0;
+            const __amdgpu_buffer_rsrc_t qa = ub_rsrc(Qa + (nrow ? r0 * 32 : 0), nrow);
+            const __amdgpu_buffer_rsrc_t qb = ub_rsrc((Qb ? Qb : Qa) + (nrow ? r0 * 32 : 0), Qb ? nrow : 0);
+#pragma unroll
+            for (int v = 0; v < 16; ++v) {
+                const uint32_t rr = (uint32_t)((v & 3) + 8 * (v >> 2) + 4 * hh);
+                __builtin_amdgcn_raw_buffer_store_b32(__builtin_bit_cast(uint32_t, q[v]), qa, rr * 128 + 4 * jr, 0, 0);
+                __builtin_amdgcn_raw_buffer_store_b32(__builtin_bit_cast(uint32_t, q[v]), qb, rr * 128 + 4 * jr, 0, 0);
+            }
+        }
+#pragma unroll
+        for (int v = 0; v < 16; ++v) g = mfma32(acc[v], acc[v], g);  // rows past n: 0
+    }
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();  // every wave is done with its slots: the reduction reuses them
+    block_slab32<kF32Waves>(reinterpret_cast<double (*)[1024]>(&ust[0][0][0][0]), g, lane, w, part);
+}
+
 // blocks per CU: pass E (190 registers: 2 waves per SIMD) 2; pass U 4.
 // Measured at C5 (ms, E / U): grid 1x 1.12 / 0.91, 2x 0.96 / 0.78, 3x 1.20 / 0.78, 4x - / 0.76.
 static int f32_grid(lz_handle *h, int64_t n, int mult)
@@ -300,7 +429,15 @@ int fused_ub32(lz_handle *h, int64_t n, const float *U, const float *Wj, const f
     const int grid = f32_grid(h, n, 2);
     LZ_TRY(ensure_partials(h, (size_t)grid * 1024));
     const int ev = prof_begin(h, PROF_UPDATE_PASS);
-    if (Qa)
+    const char *ud = getenv("LZ_UB_DMA");  // "0": the register-operand form (A/B; read per call)
+    const bool dma = !(ud && ud[0] == '0');
+    if (dma && Qa)
+        hipLaunchKernelGGL(k_fused_ub32d<true>, dim3(grid), dim3(64 * kF32Waves), 0, h->stream, n, U, Wj, binv, P2, Wn,
+                           h->partials, Qa, Qb);
+    else if (dma)
+        hipLaunchKernelGGL(k_fused_ub32d<false>, dim3(grid), dim3(64 * kF32Waves), 0, h->stream, n, U, Wj, binv, P2,
+                           Wn, h->partials, nullptr, nullptr);
+    else if (Qa)
         hipLaunchKernelGGL(k_fused_ub32<true>, dim3(grid), dim3(64 * kF32Waves), 0, h->stream, n, U, Wj, binv, P2, Wn,
                            h->partials, Qa, Qb);
     else

@@ -35,6 +35,7 @@
 // current pass computes and written to the other LDS buffers after it, then
 // ONE barrier per pass.
 #include "lz_common.hpp"
+#include "lz_diag.h"
 #include "lz_internal.hpp"
 #include "lz_kernels.hpp"
 

@@ -386,14 +386,34 @@ __device__ __forceinline__ Vec<T, VEC> epi_piece(Vec<T, VEC> y, const T *__restr
     return y;
 }
 
-template <typename T, int B, int TR, int CAP, bool WIN, int MODE, bool YCM = false, bool EPI = false>
+// ---- CU-partitioned SpMM (LZ_SPMM_PF; DESIGN.md 4 SpMM "Round 6") ----
+// The tile kernel runs on a stream masked to most of each XCD's CUs; a
+// prefetch kernel on the rest pulls the CSR runs, row pointers and the X rows
+// the XCD's next tiles touch first into that XCD's L2, paced by the number of
+// tile blocks the XCD has started.  Control words: one 128-B line per XCC
+// (only that XCD's CUs touch it, so workgroup-scope atomics -- performed in
+// the XCD's own L2, not at memory like agent-scope ones on a multi-XCD chip
+// -- are enough; round 6's first version used agent scope and its contended
+// memory-side atomics took the launch from 1.2 to 6.5-17.6 ms):
+//   [32 x + 0]  tile blocks started on XCC x        (tile kernel)
+//   [32 x + 1]  XCC x's block group blockIdx % 8    (tile kernel; -1 until known)
+//   [32 x + 2]  prefetch chunk ticket
+//   [32 x + 3]  highest X row prefetched (-1 at the start)
+constexpr int kPfCtl = 256;
+
+__device__ __forceinline__ int xcc_id()
+{
+    return (int)(__builtin_amdgcn_s_getreg(20 | (0 << 6) | (3 << 11)) & 7u);  // HW_REG_XCC_ID
+}
+
+template <typename T, int B, int TR, int CAP, bool WIN, int MODE, bool YCM = false, bool EPI = false, bool PF = false>
 __global__ __launch_bounds__(256) void k_spmm_seg(int64_t n, const int64_t *__restrict__ rp,
                                                   const int32_t *__restrict__ col,
                                                   const T *__restrict__ val,
                                                   const T *__restrict__ X, int64_t ldx, int64_t nx,
                                                   T *__restrict__ Y, int64_t ldy, int *__restrict__ longq,
                                                   int parity, const T *__restrict__ Wp, const T *__restrict__ Mm,
-                                                  int diag)
+                                                  int diag, int *__restrict__ pfc)
 {
     // MODE 0: tiles whose run exceeds the stage (or, WIN, whose columns exceed
     //         the window) are queued (longq[0] = count, longq[1..] = tile ids)
@@ -573,6 +593,15 @@ __global__ __launch_bounds__(256) void k_spmm_seg(int64_t n, const int64_t *__re
         return;
     }
     const int N = (int)N64;
+    if constexpr (PF) {  // publish this block's start to the XCD's prefetcher
+        if (tid == 0) {
+            const int x = xcc_id();
+            __hip_atomic_fetch_add(&pfc[32 * x], 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+            if ((blockIdx.x >> 3) < 8)
+                __hip_atomic_exchange(&pfc[32 * x + 1], (int)(blockIdx.x & 7), __ATOMIC_RELAXED,
+                                      __HIP_MEMORY_SCOPE_WORKGROUP);
+        }
+    }
     {  // stage the run with 16-B loads (aligned down; a piece reaching past nnz,
        // last tile only, element-wise), then the row id of every entry
         constexpr int EPV = 16 / (int)sizeof(T);
@@ -749,6 +778,128 @@ __global__ __launch_bounds__(256) void k_spmm_seg(int64_t n, const int64_t *__re
         }
     }
     }  // MODE 0
+}
+
+// The prefetch side of the CU-partitioned SpMM.  Persistent blocks, each on
+// the XCD it reads from HW_REG_XCC_ID: the XCD's tiles (xcd_remap's range for
+// its block group) are cut into chunks of C tiles, claimed in order by ticket;
+// chunk c waits until the XCD has started c*C - D tile blocks (never more than
+// D tiles ahead of the dispatch front), skips itself when the front has
+// passed it, and otherwise loads its row pointers, CSR run (every column, for
+// the chunk's column range; values one 4-B load per 64 B) and the X rows
+// above the XCD's frontier that its columns reach (at most maxspan rows: a
+// band, not a random operator).  The loaded data is dropped: it only has to
+// sit in the XCD's L2 when the tile blocks read it.  Every wait is bounded,
+// and nothing here affects results.
+template <int TR>
+__global__ __launch_bounds__(256) void k_spmm_pf(int64_t n, int64_t ntiles, const int64_t *__restrict__ rp,
+                                                 const int32_t *__restrict__ col, const char *__restrict__ val,
+                                                 int vsz, const char *__restrict__ X, int rowb,
+                                                 int *__restrict__ ctl, int C, int D, int maxspan,
+                                                 uint32_t *__restrict__ sink)
+{
+    __shared__ int s_g, s_min, s_max, s_lo;
+    __shared__ int64_t s_c;
+    const int tid = threadIdx.x, x = xcc_id();
+    if (tid == 0) {
+        int g = -1;
+        for (int it = 0; it < (1 << 20); ++it) {
+            g = __hip_atomic_fetch_add(&ctl[32 * x + 1], 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+            if (g >= 0) break;
+            __builtin_amdgcn_s_sleep(8);
+        }
+        s_g = g;
+    }
+    __syncthreads();
+    const int g = s_g;
+    if (g < 0) return;  // the XCD ran no tile block in time (bounded wait)
+    const int64_t q = ntiles >> 3, r8 = ntiles & 7;
+    const int64_t t0 = g < r8 ? g * (q + 1) : r8 * (q + 1) + (g - r8) * q, len = q + (g < r8 ? 1 : 0);
+    const int64_t nch = (len + C - 1) / C;
+    uint32_t acc = 0;
+    for (;;) {
+        if (tid == 0) {
+            s_c = __hip_atomic_fetch_add(&ctl[32 * x + 2], 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+            s_min = 0x7fffffff;
+            s_max = -1;
+            const int64_t need = s_c * C - D;
+            bool ok = s_c >= nch;
+            for (int it = 0; it < (1 << 18) && !ok; ++it) {
+                ok = __hip_atomic_fetch_add(&ctl[32 * x], 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP) >= need;
+                if (!ok) __builtin_amdgcn_s_sleep(2);
+            }
+            if (!ok) s_c = nch;  // the tile blocks stopped advancing: give up (bounded)
+            // the front has passed the whole chunk: nothing left to pull ahead
+            if (s_c < nch &&
+                __hip_atomic_fetch_add(&ctl[32 * x], 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP) >= (s_c + 1) * C)
+                s_c = -1 - s_c;
+        }
+        __syncthreads();
+        const int64_t c = s_c;
+        if (c >= nch) break;
+        if (c >= 0) {
+            const int64_t ta = t0 + c * C, tb = (c + 1) * C < len ? ta + C : t0 + len;
+            const int64_t ra = ta * TR, rb = tb * TR < n ? tb * TR : n;
+            const int64_t ka = rp[ra], kb = rp[rb];
+            // row pointers: one 4-B load per 64 B
+            for (int64_t o = ((ra * 8) & ~(int64_t)63) + 64 * tid; o < (rb + 1) * 8; o += 64 * 256)
+                acc ^= *reinterpret_cast<const uint32_t *>(reinterpret_cast<const char *>(rp) + o);
+            // values: one 4-B load per 64 B
+            for (int64_t o = ((ka * vsz) & ~(int64_t)63) + 64 * tid; o < kb * vsz; o += 64 * 256)
+                acc ^= *reinterpret_cast<const uint32_t *>(val + o);
+            // columns: all of them, 16 B per lane (their range sets the X rows)
+            int lmin = 0x7fffffff, lmax = -1;
+            const int64_t a4 = ka & ~(int64_t)3;
+            for (int64_t k = a4 + 4 * tid; k < kb; k += 4 * 256) {
+                int cv[4] = {0, 0, 0, 0};
+                if (k + 4 <= kb) {
+                    const int4 v = *reinterpret_cast<const int4 *>(col + k);
+                    cv[0] = v.x; cv[1] = v.y; cv[2] = v.z; cv[3] = v.w;
+                } else {
+                    for (int e = 0; e < 4 && k + e < kb; ++e) cv[e] = col[k + e];
+                }
+#pragma unroll
+                for (int e = 0; e < 4; ++e)
+                    if (k + e >= ka && k + e < kb) {
+                        lmin = cv[e] < lmin ? cv[e] : lmin;
+                        lmax = cv[e] > lmax ? cv[e] : lmax;
+                    }
+            }
+#pragma unroll
+            for (int o = 32; o > 0; o >>= 1) {
+                const int a = __shfl_xor(lmin, o, 64), b2 = __shfl_xor(lmax, o, 64);
+                lmin = a < lmin ? a : lmin;
+                lmax = b2 > lmax ? b2 : lmax;
+            }
+            if ((tid & 63) == 0) {
+                atomicMin(&s_min, lmin);
+                atomicMax(&s_max, lmax);
+            }
+            __syncthreads();
+            if (tid == 0) {
+                int lo = -1;
+                if (s_max >= 0) {
+                    const int old =
+                        __hip_atomic_fetch_max(&ctl[32 * x + 3], s_max, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+                    lo = old + 1 > s_min ? old + 1 : s_min;
+                    if (s_max - lo >= maxspan) lo = -1;  // not a band: leave X alone
+                }
+                s_lo = lo;
+            }
+            __syncthreads();
+            if (s_lo >= 0 && s_lo <= s_max)
+                for (int64_t o = (int64_t)s_lo * rowb + 64 * tid; o < ((int64_t)s_max + 1) * rowb; o += 64 * 256)
+                    acc ^= *reinterpret_cast<const uint32_t *>(X + o);
+        }
+        __syncthreads();  // s_c / s_min / s_max / s_lo are rewritten by the next claim
+    }
+    if (acc == 0x9e3779b9u) sink[tid] = acc;  // (keeps the loads)
+}
+
+__global__ void k_pf_init(int *ctl)
+{
+    const int i = threadIdx.x;
+    if (i < kPfCtl) ctl[i] = (i % 32 == 1 || i % 32 == 3) ? -1 : 0;
 }
 
 // Row-major SpMM at a block width off the tuned set (b not a power of two):
@@ -1162,6 +1313,81 @@ static int ensure_longq(lz_handle *h, int64_t st)
     return LZ_OK;
 }
 
+// LZ_SPMM_PF = "k[,C[,D[,span]]]" (read per call): the CU-partitioned SpMM with k
+// of every 8 CUs of each XCD prefetching (0: off), chunks of C tiles, at most
+// D tiles ahead of the XCD's dispatch front, X rows only for column spans
+// under `span` rows.  LZ_SPMM_PF_MAP selects which mask bits are an XCD's
+// CUs (0: bit i is CU i / 8 of XCC i % 8).
+static bool pf_config(int *k, int *C, int *D, int *span)
+{
+    const char *e = getenv("LZ_SPMM_PF");
+    if (!e || !*e) return false;
+    int v[4] = {0, *C, *D, *span};
+    const int got = sscanf(e, "%d,%d,%d,%d", &v[0], &v[1], &v[2], &v[3]);
+    if (got < 1 || v[0] < 0 || v[0] > 7 || v[1] < 1 || v[2] < 0 || v[3] < 1) return false;
+    *k = v[0];
+    *C = v[1];
+    *D = v[2];
+    *span = v[3];
+    return true;
+}
+
+static int pf_setup(lz_handle *h, int k)
+{
+    const char *mp = getenv("LZ_SPMM_PF_MAP");
+    const int map = mp ? atoi(mp) : 0;
+    const int key = k * 16 + map;
+    if (h->pf_key == key) return LZ_OK;
+    for (hipStream_t *s : {&h->pf_sg, &h->pf_sp})
+        if (*s) {
+            LZ_HIP_TRY(hipStreamSynchronize(*s));
+            LZ_HIP_TRY(hipStreamDestroy(*s));
+            *s = nullptr;
+        }
+    uint32_t mg[8] = {}, mpf[8] = {};
+    for (int i = 0; i < 256; ++i) {
+        // map 0: bit i -> CU i / 8 of XCC i % 8; map 1: bit i -> CU i % 32 of XCC i / 32
+        const int j = map == 0 ? i / 8 : i % 32;
+        (j % 8 < k ? mpf : mg)[i / 32] |= 1u << (i % 32);
+    }
+    LZ_HIP_TRY(hipExtStreamCreateWithCUMask(&h->pf_sg, 8, mg));
+    LZ_HIP_TRY(hipExtStreamCreateWithCUMask(&h->pf_sp, 8, mpf));
+    for (hipEvent_t *e : {&h->ev_pff, &h->ev_pfg, &h->ev_pfp})
+        if (!*e) LZ_HIP_TRY(hipEventCreateWithFlags(e, hipEventDisableTiming));
+    if (!h->pf_ctl) LZ_HIP_TRY(hipMalloc(&h->pf_ctl, sizeof(int) * (kPfCtl + 256)));
+    h->pf_key = key;
+    return LZ_OK;
+}
+
+template <typename T, int B, int TR, int CAP>
+static int launch_seg_pf(lz_handle *h, int64_t n, const int64_t *rp, const int32_t *col, const T *val, const T *X,
+                         int64_t ldx, int64_t nx, T *Y, int64_t ldy, int k, int C, int D, int span)
+{
+    const int64_t st = ceil_div(n, (int64_t)TR);
+    LZ_TRY(pf_setup(h, k));
+    const int parity = h->longq_parity;
+    h->longq_parity ^= 1;
+    hipLaunchKernelGGL(k_pf_init, dim3(1), dim3(kPfCtl), 0, h->stream, h->pf_ctl);
+    LZ_HIP_TRY(hipEventRecord(h->ev_pff, h->stream));
+    LZ_HIP_TRY(hipStreamWaitEvent(h->pf_sg, h->ev_pff, 0));
+    LZ_HIP_TRY(hipStreamWaitEvent(h->pf_sp, h->ev_pff, 0));
+    // 4 blocks per prefetching CU (4 k CUs per XCD)
+    const int gp = 8 * 4 * k * 4;
+    hipLaunchKernelGGL((k_spmm_pf<TR>), dim3(gp), dim3(256), 0, h->pf_sp, n, st, rp, col,
+                       reinterpret_cast<const char *>(val), (int)sizeof(T), reinterpret_cast<const char *>(X),
+                       (int)(ldx * sizeof(T)), h->pf_ctl, C, D, span, reinterpret_cast<uint32_t *>(h->pf_ctl + kPfCtl));
+    hipLaunchKernelGGL((k_spmm_seg<T, B, TR, CAP, false, 0, false, false, true>), dim3((unsigned)st), dim3(256), 0,
+                       h->pf_sg, n, rp, col, val, X, ldx, nx, Y, ldy, h->longq, parity, nullptr, nullptr, 0, h->pf_ctl);
+    const int g2 = (int)std::max<int64_t>(1, std::min<int64_t>(st, (int64_t)h->n_cu * 4));
+    hipLaunchKernelGGL((k_spmm_seg<T, B, TR, CAP, false, 1>), dim3(g2), dim3(256), 0, h->pf_sg, n, rp, col, val, X, ldx,
+                       nx, Y, ldy, h->longq, parity, nullptr, nullptr, 0, nullptr);
+    LZ_HIP_TRY(hipEventRecord(h->ev_pfg, h->pf_sg));
+    LZ_HIP_TRY(hipEventRecord(h->ev_pfp, h->pf_sp));
+    LZ_HIP_TRY(hipStreamWaitEvent(h->stream, h->ev_pfg, 0));
+    LZ_HIP_TRY(hipStreamWaitEvent(h->stream, h->ev_pfp, 0));
+    return LZ_OK;
+}
+
 // nnz-split SpMM with the long-tile queue: the main kernel, then a persistent
 // kernel over the queued tiles (an empty queue costs one short launch).
 // plan_slot >= 0: the long tiles an earlier call on the same operator queued
@@ -1187,12 +1413,16 @@ static int launch_seg(lz_handle *h, int64_t n, const int64_t *rp, const int32_t 
         LZ_HIP_TRY(hipEventRecord(h->ev_lfork, h->stream));
         LZ_HIP_TRY(hipStreamWaitEvent(h->lstream, h->ev_lfork, 0));
         hipLaunchKernelGGL((k_spmm_seg<T, B, TR, CAP, WIN, 1, YCM, EPI>), dim3(g2), dim3(256), 0, h->lstream, n, rp,
-                           col, val, X, ldx, nx, Y, ldy, h->longq, 2 + plan_slot, Wp, Mm, 0);
+                           col, val, X, ldx, nx, Y, ldy, h->longq, 2 + plan_slot, Wp, Mm, 0, nullptr);
         LZ_HIP_TRY(hipEventRecord(h->ev_ljoin, h->lstream));
         hipLaunchKernelGGL((k_spmm_seg<T, B, TR, CAP, WIN, 0, YCM, EPI>), dim3((unsigned)st), dim3(256), 0, h->stream,
-                           n, rp, col, val, X, ldx, nx, Y, ldy, h->longq, 2 + plan_slot, Wp, Mm, 0);
+                           n, rp, col, val, X, ldx, nx, Y, ldy, h->longq, 2 + plan_slot, Wp, Mm, 0, nullptr);
         LZ_HIP_TRY(hipStreamWaitEvent(h->stream, h->ev_ljoin, 0));
         return LZ_OK;
+    }
+    if constexpr (!WIN && !YCM && !EPI) {
+        int k = 0, C = 8, D = 96, span = 65536;
+        if (pf_config(&k, &C, &D, &span) && k > 0) return launch_seg_pf<T, B, TR, CAP>(h, n, rp, col, val, X, ldx, nx, Y, ldy, k, C, D, span);
     }
     const int parity = h->longq_parity;
     h->longq_parity ^= 1;
@@ -1209,10 +1439,10 @@ static int launch_seg(lz_handle *h, int64_t n, const int64_t *rp, const int32_t 
     constexpr int diag = 0;
 #endif
     hipLaunchKernelGGL((k_spmm_seg<T, B, TR, CAP, WIN, 0, YCM, EPI>), dim3((unsigned)st), dim3(256), 0, h->stream, n, rp,
-                       col, val, X, ldx, nx, Y, ldy, h->longq, parity, Wp, Mm, diag);
+                       col, val, X, ldx, nx, Y, ldy, h->longq, parity, Wp, Mm, diag, nullptr);
     const int g2 = (int)std::max<int64_t>(1, std::min<int64_t>(st, (int64_t)h->n_cu * 4));
     hipLaunchKernelGGL((k_spmm_seg<T, B, TR, CAP, WIN, 1, YCM, EPI>), dim3(g2), dim3(256), 0, h->stream, n, rp, col, val,
-                       X, ldx, nx, Y, ldy, h->longq, parity, Wp, Mm, 0);
+                       X, ldx, nx, Y, ldy, h->longq, parity, Wp, Mm, 0, nullptr);
     return LZ_OK;
 }
 

@@ -78,6 +78,11 @@ int lz_device_error(lz_handle *h, int *code);
 /* Test support: store `code` into the device error word (on the handle's
  * stream), as a kernel that gave up a wait would. */
 int lz_debug_set_device_error(lz_handle *h, int code);
+/* Test support: the handle's next distributed solve (lz_block_lanczos_dist /
+ * _halo) fails its set-up with status `code` (nonzero) on this rank only; the
+ * rank still joins the solve's first collective (the ranks' set-up vote), so
+ * every peer returns LZ_E_STATE instead of waiting. */
+int lz_debug_fail_next_setup(lz_handle *h, int code);
 
 /* Test support: fills the LDS of every CU with a 32-bit pattern (0xFFFFFFFF
  * reads back as a double NaN), and the handle's slab and scratch workspaces
@@ -255,19 +260,6 @@ int lz_debug_last_split(lz_handle *h, int64_t out[2]);
  * wavefront step (b = 16 fp64), out[1] = 1 when it also ran the requested rows'
  * pass 2 first and the halo exchange beside the rest of each step. */
 int lz_debug_last_wf(lz_handle *h, int out[2]);
-
-/* Candidate (round 5, measured against lz_csr_spmm at b = 16 fp64; DESIGN.md 4
- * SpMM "column panels"): Y = A X with X staged through LDS in 512-row panels
- * and row accumulators in registers, one 1024-thread block per 2048 rows, from
- * a once-per-operator plan of passes (the Python package's panel_plan builds
- * it): bp0[nblocks + 1] each block's pass range; per pass px0 (first X row of
- * its panel), pe0[npass + 1] (first entry, a multiple of 8), goff (136 uint16
- * per pass: the offsets of the block's 128 groups' entry lists, 129 used);
- * ev / ex the entries' values and (row slot << 9 | panel row) words.  X has nx
- * rows, row-major, ld = 16; Y n rows, ld = 16.  All arrays device. */
-int lz_debug_spmm_panel(lz_handle *h, int64_t n, int64_t nx, const void *X, void *Y, int nblocks,
-                        const int32_t *bp0, const int32_t *px0, const int32_t *pe0, const uint16_t *goff,
-                        const void *ev, const uint16_t *ex);
 
 /* Test hook: the wavefront step's once-per-solve plan of a CSR operator (device
  * arrays), as lz_block_lanczos would make it for these rows. deps_out (device,

@@ -380,28 +380,3 @@ def test_sqrtm_b16_newton_schulz(lz, orc, handle, torch_cuda, monkeypatch, cond)
         # route: the same bits (before round 5, kappa = 1e8 stopped in
         # Newton-Schulz with beta^-1 ~6e-10 off)
         assert np.array_equal(out["1"][0], out["0"][0]) and np.array_equal(out["1"][1], out["0"][1])
-
-
-@pytest.mark.parametrize("n,npr,hw", [(50_021, 10.0, 4096), (20_480, 10.0, 256), (9_000, 30.0, 2000),
-                                      (4_099, 5.0, 3000), (300, 8.0, 100)])
-def test_spmm_panel_candidate(lz, orc, handle, torch_cuda, n, npr, hw):
-    """The column-panel SpMM candidate (lz_debug_spmm_panel; X through LDS in
-    512-row panels, row accumulators in registers, the plan from
-    lz.panel_plan) against the oracle's CSR product: n not a multiple of the
-    2048-row block, panels split over several passes (30 entries per row), a
-    band wider than the panel and narrower, a single short block."""
-    torch = torch_cuda
-    A = lz.gen_banded(n, npr, hw, seed=n % 97)
-    pl = lz.panel_plan(A)
-    assert pl.pe0[-1] >= A.nnz and (np.diff(pl.pe0) <= lz.PANEL_MAX_ENTRIES).all()
-    rng = np.random.default_rng(5)
-    X = rng.uniform(-1, 1, (n, 16))
-    Y = torch.full((n, 16), np.nan, dtype=torch.float64, device="cuda")
-    handle.spmm_panel(pl.device(), n, pl.nblocks, torch.from_numpy(X).cuda(), Y)
-    torch.cuda.synchronize()
-    M = dense_of(A)
-    ref = M @ X
-    bound = abs(M) @ np.abs(X)
-    got = Y.cpu().numpy()
-    assert np.all(np.abs(got - ref) <= 64 * EPS[np.float64] * bound + 1e-300), np.max(np.abs(got - ref))
-    assert np.all(np.abs(got - orc.csr_spmm(A, X)) <= 64 * EPS[np.float64] * bound + 1e-300)

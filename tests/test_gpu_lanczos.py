@@ -235,6 +235,31 @@ def test_block_f32_b32_powerlaw(lz, orc, handle, torch_cuda, monkeypatch, n, cap
     assert handle.device_error() == 0
 
 
+@pytest.mark.parametrize("n,m", [(20_011, 4), (100_003, 3), (33, 2)])
+def test_block_f32_b32_ub_dma_bitwise(lz, handle, torch_cuda, monkeypatch, n, m):
+    """Pass UB with its operands staged through LDS by DMA (k_fused_ub32d, the
+    default) against the register-operand form (LZ_UB_DMA=0): the same products
+    in the same order, so alpha, beta, q and the post-call Q0 / Q1 / W are the
+    same bits, including the ragged last strip (n not a multiple of 32) and the
+    last step's Q store (QO)."""
+    torch = torch_cuda
+    A = lz.gen_powerlaw(n, 10.0, 2.1, max(2, n // 10), seed=n % 89, dtype=np.float32)
+    B = lz.uniform_B(A.n, 32, seed=9, dtype=np.float32)
+    Ad, Bd = lz.CsrDevice.from_host(A), torch.from_numpy(B).cuda()
+    kw = dict(dtype=torch.float32, device="cuda")
+    outs = []
+    for dma in ("1", "0"):
+        monkeypatch.setenv("LZ_UB_DMA", dma)
+        q, al, be = torch.zeros(m * 32, **kw), torch.zeros(m, 32, 32, **kw), torch.zeros(m + 1, 32, 32, **kw)
+        Q0, Q1, W = (torch.full((A.n, 32), float("nan"), **kw) for _ in range(3))
+        handle.block_lanczos_blas(Ad, Bd, m, min(84, A.n - 1), q, al, be, Q0, Q1, W)
+        torch.cuda.synchronize()
+        assert handle.device_error() == 0
+        outs.append([t.cpu().numpy() for t in (q, al, be, Q0, Q1, W)])
+    for x, y in zip(*outs):
+        assert np.array_equal(x, y, equal_nan=True)
+
+
 @pytest.mark.parametrize("b", [1, 3, 4, 5, 8, 32])
 def test_block_fused_any_b_f64(lz, orc, handle, torch_cuda, b):
     """The Q-free iteration at every block width but 16 (separate SpMM + VALU
@@ -562,16 +587,23 @@ def test_prof_class_mask(lz, handle, torch_cuda, monkeypatch, wf):
 
 
 @pytest.mark.parametrize("m", [1, 2, 5])
-@pytest.mark.parametrize("path", ["wavefront", "wavefront_lds", "twopass", "unfused", "sep_b4", "b2_f32_b32"])
+@pytest.mark.parametrize("path", ["wavefront", "shape10", "shape10_lds", "shape12", "twopass", "unfused", "sep_b4",
+                                  "b2_f32_b32"])
 def test_block_final_state(lz, orc, handle, torch_cuda, monkeypatch, path, m):
     """On return Q0 = Q1 = Q_{m-1} and W = the last residual, as the reference
     leaves them (methods/block_lanczos.hpp:145,159,162; Q1 is not written at
-    m = 1): every step form against the oracle's final blocks."""
+    m = 1): every step form against the oracle's final blocks.  The default
+    wavefront shape (111) writes the state in a pass-2-only step launch (QO);
+    the other shapes (LZ_WF_SHAPE 10 / 12) take the final_state pass, by MFMA
+    strips (k_final_state16m) or, LZ_FS_MFMA=0, its LDS form (k_final_state16),
+    each reading the residual buffers the parity of m chose."""
     torch = torch_cuda
     b, dt = (4, np.float64) if path == "sep_b4" else (32, np.float32) if path == "b2_f32_b32" else (16, np.float64)
     if path == "twopass":
         monkeypatch.setenv("LZ_PASS_WF", "0")
-    if path == "wavefront_lds":  # the LDS form of the post-call pass (default: MFMA strips)
+    if path.startswith("shape"):
+        monkeypatch.setenv("LZ_WF_SHAPE", path[5:7])
+    if path == "shape10_lds":  # the LDS form of the post-call pass (default: MFMA strips)
         monkeypatch.setenv("LZ_FS_MFMA", "0")
     A = lz.gen_banded(30_011, 10.0, 700, seed=70 + m, dtype=dt)
     B = lz.uniform_B(A.n, b, seed=71, dtype=dt)

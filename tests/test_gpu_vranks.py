@@ -317,6 +317,57 @@ def test_vranks_argument_error_aborts_group(lz, torch_cuda):
     assert codes[1] == -1 and codes[0] == -3, codes  # LZ_E_ARG on rank 1, LZ_E_COMM on rank 0
 
 
+@pytest.mark.parametrize("form,b", [("halo", 16), ("allgather", 16), ("halo", 4)])
+def test_vranks_setup_failure_votes(lz, torch_cuda, form, b):
+    """A rank whose set-up fails inside the distributed solve (forced by
+    lz_debug_fail_next_setup: as a failed workspace growth or plan) still joins
+    the solve's first collective, the ranks' set-up vote, with ok = 0: its peer
+    returns LZ_E_STATE naming the peer's failure, not the group's abort (over
+    RCCL no abort is issued before a collective, so without the vote the peer
+    would wait in a collective this rank never issues)."""
+    import time
+    torch = torch_cuda
+    A = lz.gen_banded(4_000, 5.0, 100, seed=63)
+    bounds = np.array([0, 2000, 4000], np.int64)
+    out = [None, None]
+
+    def rank_fn(r, h):
+        r0, r1 = int(bounds[r]), int(bounds[r + 1])
+        nl = r1 - r0
+        rp, col, val = _slab(A, r0, r1)
+        kw = dict(dtype=torch.float64, device="cuda")
+        q, al, be = torch.zeros(4 * b, **kw), torch.zeros(4, b, b, **kw), torch.zeros(5, b, b, **kw)
+        Bl = torch.ones(nl, b, **kw)
+        if form == "halo":
+            ccol, cnt, rows = lz.halo_plan(col, bounds, r)
+            h.halo_init(r0, nl, cnt, rows)
+            nh = int(rows.size)
+            Ad = lz.CsrDevice.from_host(lz.CsrHost(nl, rp, ccol, val), n_cols=nl + nh)
+            X0, X1 = torch.zeros(nl + nh, b, **kw), torch.zeros(nl + nh, b, **kw)
+            args = (h.ptr, nl, Ad.nnz, Ad.row_ptr.data_ptr(), Ad.col.data_ptr(), Ad.val.data_ptr(), lz.LZ_F64, b, 4,
+                    0, 0, Bl.data_ptr(), q.data_ptr(), al.data_ptr(), be.data_ptr(), X0.data_ptr(), X1.data_ptr())
+            fn = h.L.lz_block_lanczos_halo
+        else:
+            n_pad = 2000
+            pcol = lz.remap_cols_padded(col, bounds, n_pad)
+            Ad = lz.CsrDevice.from_host(lz.CsrHost(nl, rp, pcol, val), n_cols=2 * n_pad)
+            W, X = torch.zeros(n_pad, b, **kw), torch.zeros(2 * n_pad, b, **kw)
+            args = (h.ptr, nl, n_pad, 2 * n_pad, Ad.nnz, Ad.row_ptr.data_ptr(), Ad.col.data_ptr(), Ad.val.data_ptr(),
+                    lz.LZ_F64, b, 4, 0, 0, Bl.data_ptr(), q.data_ptr(), al.data_ptr(), be.data_ptr(), None, None,
+                    W.data_ptr(), X.data_ptr())
+            fn = h.L.lz_block_lanczos_dist
+        if r == 1:
+            h.debug_fail_next_setup(-2)  # as a failed hipMalloc
+        rc = fn(*args)
+        out[r] = (rc, h.L.lz_last_error().decode())
+
+    t0 = time.time()
+    lz.run_virtual_ranks(2, rank_fn)
+    assert time.time() - t0 < 60
+    assert out[1][0] == -2 and "lz_debug_fail_next_setup" in out[1][1], out
+    assert out[0][0] == -4 and "peer rank failed its set-up" in out[0][1], out
+
+
 def _with_far_entries(lz, A, pairs, v=1e-3):
     """A plus the symmetric entries (r, c), (c, r) of `pairs`, value v."""
     import scipy.sparse as sp
@@ -403,30 +454,48 @@ def test_vranks_barrier_timeout(lz, torch_cuda, monkeypatch):
     assert 1.5 < time.time() - t0 < 60
 
 
-@pytest.mark.timeout(900)
-def test_vranks_c4_full_size_halo(lz, orc, torch_cuda):
-    """BASELINE config C4 at full size: n = 4e7 rows, ~25 entries per row
-    (nnz ~ 1e9), half width 2^16, row-partitioned over 8 virtual ranks in the
-    halo form (the wavefront step with the requested rows' pass 2 first and the
-    exchange beside the rest of each step, asserted), 3 steps against the
-    oracle on the GLOBAL operator (methods/block_lanczos.hpp:131-166).  The 8
-    ranks share one device here; over RCCL each is one MI355X (bench.py --gpus
-    8)."""
+_C4 = {}
+
+
+def _c4_problem(lz, orc):
+    """BASELINE config C4 (n = 4e7, ~25 entries per row, half width 2^16) and
+    the oracle's first 3 steps on it, built once for the module's C4 tests."""
     import time
-    N, n, m, lc = 8, 40_000_000, 3, 84
-    t0 = time.time()
-    A = lz.gen_banded(n, 25.0, 1 << 16, seed=20261015)
-    B = lz.uniform_B(n, 16, seed=20261015)
-    assert 0.99e9 < A.nnz < 1.01e9
-    ref = orc.block_lanczos(A, B, m, lc)
-    t1 = time.time()
+    if not _C4:
+        n, m, lc = 40_000_000, 3, 84
+        t0 = time.time()
+        A = lz.gen_banded(n, 25.0, 1 << 16, seed=20261015)
+        B = lz.uniform_B(n, 16, seed=20261015)
+        assert 0.99e9 < A.nnz < 1.01e9
+        _C4.update(A=A, B=B, m=m, lc=lc, ref=orc.block_lanczos(A, B, m, lc), t_build=time.time() - t0)
+    return _C4
+
+
+@pytest.mark.timeout(900)
+@pytest.mark.parametrize("form", ["halo", "allgather"])
+def test_vranks_c4_full_size(lz, orc, torch_cuda, form):
+    """BASELINE config C4 at full size: n = 4e7 rows, ~25 entries per row
+    (nnz ~ 1e9), half width 2^16, row-partitioned over 8 virtual ranks, 3 steps
+    against the oracle on the GLOBAL operator (methods/block_lanczos.hpp:131-166).
+    halo: the wavefront step with the requested rows' pass 2 first and the
+    exchange beside the rest of each step (asserted).  allgather: the north
+    star's exchange -- every step all-gathers the whole Krylov block into each
+    rank's X_full (5.1 GB per rank here) -- on the two-pass step, its default at
+    N > 1 (asserted).  The 8 ranks share one device here; over RCCL each is one
+    MI355X (bench.py --gpus 8 --config c4)."""
+    import time
+    P = _c4_problem(lz, orc)
+    N, n = 8, P["A"].n
     bounds = np.array([n * g // N for g in range(N + 1)], np.int64)
     wfs = []
-    got, _ = run_dist(lz, torch_cuda, A, B, m, lc, N, "halo", bounds=bounds, wf_out=wfs)
+    t1 = time.time()
+    got, splits = run_dist(lz, torch_cuda, P["A"], P["B"], P["m"], P["lc"], N, form, bounds=bounds, wf_out=wfs)
     t2 = time.time()
-    assert all(w == (True, True) for w in wfs), wfs
-    assert_close_run(lz, m, 16, got, ref)
-    print(f"C4 8 virtual ranks: operator + oracle {t1 - t0:.1f} s, distributed solve {t2 - t1:.1f} s")
+    assert all(w == ((True, True) if form == "halo" else (False, False)) for w in wfs), wfs
+    if form == "allgather":
+        assert all(s is not None for s in splits), splits  # interior pass 1 beside the all-gather
+    assert_close_run(lz, P["m"], 16, got, P["ref"])
+    print(f"C4 8 virtual ranks ({form}): operator + oracle {P['t_build']:.1f} s, distributed solve {t2 - t1:.1f} s")
 
 
 @pytest.mark.parametrize("form", ["halo", "allgather"])
