@@ -135,8 +135,10 @@ HOST_SYMBOLS = [
 ]
 
 
-def _bind(lib, symbols):
+def _bind(lib, symbols, strict=True):
     for name, res, args in symbols:
+        if not strict and not hasattr(lib, name):
+            continue  # (an older build loaded through LZ_HIP_LIB for an A/B: only what it has)
         fn = getattr(lib, name)
         fn.restype = res
         fn.argtypes = args
@@ -176,7 +178,7 @@ def hip_lib():
             import torch  # noqa: F401
         except ImportError:
             pass
-        _hip = _bind(ctypes.CDLL(HIP_LIB), HIP_SYMBOLS)
+        _hip = _bind(ctypes.CDLL(HIP_LIB), HIP_SYMBOLS, strict=not os.environ.get("LZ_HIP_LIB"))
     return _hip
 
 

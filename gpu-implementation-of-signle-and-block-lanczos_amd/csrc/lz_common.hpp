@@ -118,6 +118,8 @@ struct lz_handle {
     hipEvent_t ev_pff = nullptr, ev_pfg = nullptr, ev_pfp = nullptr;
     int *pf_ctl = nullptr;
     int pf_key = -1;
+    int pf_band = 0;                 // the operator's max |column - row| (k_band), for pf_band_key
+    int64_t pf_band_key[3] = {0, 0, -1};
     size_t pairs_cap = 0;         // entries
     void *cm_buf = nullptr;       // column-major SpMM: row-major copies of X and Y
     size_t cm_cap = 0;            // bytes

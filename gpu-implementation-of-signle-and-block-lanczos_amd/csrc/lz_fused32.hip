@@ -281,12 +281,17 @@ template <bool QO>
 __global__ __launch_bounds__(64 * kF32Waves) void k_fused_ub32d(int64_t n, const float *U, const float *Wj,
                                                                 const float *__restrict__ binv,
                                                                 const float *__restrict__ P2, float *__restrict__ Wn,
-                                                                double *__restrict__ part, float *Qa, float *Qb)
+                                                                double *__restrict__ part, float *Qa, float *Qb,
+                                                                int dbg)
 {
     // per wave: two slots x (U strip, W_j strip) of 4 KB; the block slab's
     // reduction reuses the same memory after the loop
     __shared__ __attribute__((aligned(16))) float ust[kF32Waves][2][2][1024];
-    const int lane = threadIdx.x & 63, w = threadIdx.x >> 6, hh = lane >> 5, jr = lane & 31;
+    // w wave-uniform in the compiler's eyes too, so every buffer resource below is
+    // scalar (with w = threadIdx.x >> 6 it built them per lane and wrapped each
+    // buffer access in a readfirstlane loop)
+    const int lane = threadIdx.x & 63, w = __builtin_amdgcn_readfirstlane((int)(threadIdx.x >> 6)), hh = lane >> 5,
+              jr = lane & 31;
     float bo[16], po[16];
     bop32(binv, 1.0f, hh, jr, bo);
     bop32(P2, -1.0f, hh, jr, po);
@@ -312,14 +317,17 @@ __global__ __launch_bounds__(64 * kF32Waves) void k_fused_ub32d(int64_t n, const
             __builtin_amdgcn_raw_ptr_buffer_load_lds(wr, (ws_lds_t *)&ust[w][slot][1][256 * k], 16, goff + 1024 * k, 0, 0, 0);
         }
     };
-    constexpr int ST = QO ? 48 : 16;  // store instructions per strip
     dma(0);
     for (int64_t s = 0; s < nst; ++s) {
         dma(s + 1);
-        // strip s landed: strip s + 1's 8 DMAs, and from s = 1 on strip s - 1's
-        // stores, were issued after it
-        if (s == 0) asm volatile("s_waitcnt vmcnt(8)" ::: "memory");
-        else asm volatile("s_waitcnt vmcnt(%0)" ::"n"(8 + ST) : "memory");
+        // strip s landed: only strip s + 1's 8 DMAs may still be in flight.  (Not
+        // vmcnt(8 + ST) for strip s - 1's ST younger stores: a store can be
+        // acknowledged before an older load returns, so that count could be
+        // reached with strip s's data still on its way -- the first version
+        // read such operands.  Loads return in order, so at most 8 left means
+        // strip s is in.)
+        if (dbg & 1) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        else asm volatile("s_waitcnt vmcnt(8)" ::: "memory");
         const uint32_t sb = ws_lds_addr(reinterpret_cast<int *>(&ust[w][(int)(s & 1)][0][0]));
         float4 u4[4], w4[4];
         const uint32_t o0 = sb + rbase + 16u * (uint32_t)((4 * hh + 0) ^ (jr & 7)),
@@ -357,13 +365,15 @@ __global__ __launch_bounds__(64 * kF32Waves) void k_fused_ub32d(int64_t n, const
         }
 #pragma unroll
         for (int v = 0; v < 16; ++v) acc[v] += acc2[v];
-        // (every strip issues exactly ST stores, rows past n to an out-of-range
-        // offset, so the vmcnt arithmetic above holds for the last strip too)
+        // (rows past n: out-of-range offsets, no write.  __float_as_uint, not
+        // __builtin_bit_cast(uint32_t, acc[v]): hipcc of ROCm 7.2 stored acc[0]
+        // sixteen times for the latter in this unrolled loop)
         const __amdgpu_buffer_rsrc_t nr = ub_rsrc(Wn + (r0 < n ? r0 * 32 : 0), r0 < n ? (n - r0 < 32 ? n - r0 : 32) : 0);
 #pragma unroll
         for (int v = 0; v < 16; ++v) {
             const uint32_t rr = (uint32_t)((v & 3) + 8 * (v >> 2) + 4 * hh);
-            __builtin_amdgcn_raw_buffer_store_b32(__builtin_bit_cast(uint32_t, acc[v]), nr, rr * 128 + 4 * jr, 0, 0);
+            if (dbg & 2) __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(acc[v]), nr, rr * 128 + 4 * jr, 0, 2);
+            else __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(acc[v]), nr, rr * 128 + 4 * jr, 0, 0);
         }
         if constexpr (QO) {
             f16v_t q;
@@ -377,8 +387,8 @@ __global__ __launch_bounds__(64 * kF32Waves) void k_fused_ub32d(int64_t n, const
 #pragma unroll
             for (int v = 0; v < 16; ++v) {
                 const uint32_t rr = (uint32_t)((v & 3) + 8 * (v >> 2) + 4 * hh);
-                __builtin_amdgcn_raw_buffer_store_b32(__builtin_bit_cast(uint32_t, q[v]), qa, rr * 128 + 4 * jr, 0, 0);
-                __builtin_amdgcn_raw_buffer_store_b32(__builtin_bit_cast(uint32_t, q[v]), qb, rr * 128 + 4 * jr, 0, 0);
+                __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(q[v]), qa, rr * 128 + 4 * jr, 0, 0);
+                __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(q[v]), qb, rr * 128 + 4 * jr, 0, 0);
             }
         }
 #pragma unroll
@@ -431,12 +441,14 @@ int fused_ub32(lz_handle *h, int64_t n, const float *U, const float *Wj, const f
     const int ev = prof_begin(h, PROF_UPDATE_PASS);
     const char *ud = getenv("LZ_UB_DMA");  // "0": the register-operand form (A/B; read per call)
     const bool dma = !(ud && ud[0] == '0');
+    // (A/B: LZ_UB_DMA=3 drains every load before each strip, 5 stores W'' non-temporal)
+    const int dbg = ud ? atoi(ud) >> 1 : 0;
     if (dma && Qa)
         hipLaunchKernelGGL(k_fused_ub32d<true>, dim3(grid), dim3(64 * kF32Waves), 0, h->stream, n, U, Wj, binv, P2, Wn,
-                           h->partials, Qa, Qb);
+                           h->partials, Qa, Qb, dbg);
     else if (dma)
         hipLaunchKernelGGL(k_fused_ub32d<false>, dim3(grid), dim3(64 * kF32Waves), 0, h->stream, n, U, Wj, binv, P2,
-                           Wn, h->partials, nullptr, nullptr);
+                           Wn, h->partials, nullptr, nullptr, dbg);
     else if (Qa)
         hipLaunchKernelGGL(k_fused_ub32<true>, dim3(grid), dim3(64 * kF32Waves), 0, h->stream, n, U, Wj, binv, P2, Wn,
                            h->partials, Qa, Qb);

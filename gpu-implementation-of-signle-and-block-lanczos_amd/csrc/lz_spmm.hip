@@ -784,26 +784,30 @@ __global__ __launch_bounds__(256) void k_spmm_seg(int64_t n, const int64_t *__re
 // the XCD it reads from HW_REG_XCC_ID: the XCD's tiles (xcd_remap's range for
 // its block group) are cut into chunks of C tiles, claimed in order by ticket;
 // chunk c waits until the XCD has started c*C - D tile blocks (never more than
-// D tiles ahead of the dispatch front), skips itself when the front has
-// passed it, and otherwise loads its row pointers, CSR run (every column, for
-// the chunk's column range; values one 4-B load per 64 B) and the X rows
-// above the XCD's frontier that its columns reach (at most maxspan rows: a
-// band, not a random operator).  The loaded data is dropped: it only has to
-// sit in the XCD's L2 when the tile blocks read it.  Every wait is bounded,
-// and nothing here affects results.
+// D tiles ahead of the dispatch front) and skips itself when the front has
+// passed it.  A chunk's rows [ra, rb) read four contiguous byte ranges: their
+// row pointers, their CSR columns and values, and the X rows their band first
+// reaches on this XCD, [ra + hw, rb + hw) (hw: the operator's largest
+// |column - row|, once per operator; the XCD's first chunk also the band
+// below, [ra - hw, ra + hw)).  The block streams them by LDS-DMA into a
+// scratch slot it never reads (1 KB per wave-instruction, no register
+// destinations, no waits but the last): the data only has to be in the XCD's
+// L2 when the tile blocks read it.  Every wait is bounded, and nothing here
+// affects results.
 template <int TR>
 __global__ __launch_bounds__(256) void k_spmm_pf(int64_t n, int64_t ntiles, const int64_t *__restrict__ rp,
                                                  const int32_t *__restrict__ col, const char *__restrict__ val,
-                                                 int vsz, const char *__restrict__ X, int rowb,
-                                                 int *__restrict__ ctl, int C, int D, int maxspan,
-                                                 uint32_t *__restrict__ sink)
+                                                 int vsz, const char *__restrict__ X, int64_t nx, int rowb,
+                                                 int *__restrict__ ctl, int C, int D, int64_t hw)
 {
-    __shared__ int s_g, s_min, s_max, s_lo;
+    __shared__ __attribute__((aligned(16))) char trash[4][1024];
+    __shared__ int s_g;
     __shared__ int64_t s_c;
-    const int tid = threadIdx.x, x = xcc_id();
+    const int tid = threadIdx.x, lane = tid & 63, x = xcc_id();
+    const int w = __builtin_amdgcn_readfirstlane(tid >> 6);
     if (tid == 0) {
         int g = -1;
-        for (int it = 0; it < (1 << 20); ++it) {
+        for (int it = 0; it < (1 << 14); ++it) {
             g = __hip_atomic_fetch_add(&ctl[32 * x + 1], 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
             if (g >= 0) break;
             __builtin_amdgcn_s_sleep(8);
@@ -811,89 +815,78 @@ __global__ __launch_bounds__(256) void k_spmm_pf(int64_t n, int64_t ntiles, cons
         s_g = g;
     }
     __syncthreads();
-    const int g = s_g;
+    const int g = __builtin_amdgcn_readfirstlane(s_g);
     if (g < 0) return;  // the XCD ran no tile block in time (bounded wait)
     const int64_t q = ntiles >> 3, r8 = ntiles & 7;
     const int64_t t0 = g < r8 ? g * (q + 1) : r8 * (q + 1) + (g - r8) * q, len = q + (g < r8 ? 1 : 0);
     const int64_t nch = (len + C - 1) / C;
-    uint32_t acc = 0;
+    // the block's pieces of one byte range [b0, b1), 1 KB per wave-instruction
+    auto stream = [&](const char *base, int64_t b0, int64_t b1) {
+        if (b1 <= b0) return;
+        b0 &= ~(int64_t)15;
+        const int64_t pieces = (b1 - b0 + 1023) >> 10;
+        const __amdgpu_buffer_rsrc_t r = __builtin_amdgcn_make_buffer_rsrc(
+            const_cast<char *>(base + b0), (short)0, (int)(b1 - b0), 0x00020000);
+        for (int64_t p = w; p < pieces; p += 4)
+            __builtin_amdgcn_raw_ptr_buffer_load_lds(r, (ws_lds_t *)&trash[w][0], 16, (uint32_t)(p * 1024 + 16 * lane),
+                                                     0, 0, 0);
+    };
     for (;;) {
         if (tid == 0) {
-            s_c = __hip_atomic_fetch_add(&ctl[32 * x + 2], 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
-            s_min = 0x7fffffff;
-            s_max = -1;
-            const int64_t need = s_c * C - D;
-            bool ok = s_c >= nch;
-            for (int it = 0; it < (1 << 18) && !ok; ++it) {
+            int64_t c = __hip_atomic_fetch_add(&ctl[32 * x + 2], 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+            const int64_t need = c * C - D;
+            bool ok = c >= nch;
+            for (int it = 0; it < (1 << 14) && !ok; ++it) {
                 ok = __hip_atomic_fetch_add(&ctl[32 * x], 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP) >= need;
                 if (!ok) __builtin_amdgcn_s_sleep(2);
             }
-            if (!ok) s_c = nch;  // the tile blocks stopped advancing: give up (bounded)
+            if (!ok) c = nch;  // the tile blocks stopped advancing: give up (bounded)
             // the front has passed the whole chunk: nothing left to pull ahead
-            if (s_c < nch &&
-                __hip_atomic_fetch_add(&ctl[32 * x], 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP) >= (s_c + 1) * C)
-                s_c = -1 - s_c;
+            if (c < nch &&
+                __hip_atomic_fetch_add(&ctl[32 * x], 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP) >= (c + 1) * C)
+                c = -1 - c;
+            s_c = c;
         }
         __syncthreads();
-        const int64_t c = s_c;
+        // (wave-uniform in the compiler's eyes too: scalar resources below, no
+        // readfirstlane loops around the DMAs)
+        const int64_t c = (int64_t)(((uint64_t)(uint32_t)__builtin_amdgcn_readfirstlane((int)((uint64_t)s_c >> 32)) << 32) |
+                                    (uint32_t)__builtin_amdgcn_readfirstlane((int)(uint32_t)s_c));
+        __syncthreads();  // (s_c is rewritten by the next claim)
         if (c >= nch) break;
-        if (c >= 0) {
-            const int64_t ta = t0 + c * C, tb = (c + 1) * C < len ? ta + C : t0 + len;
-            const int64_t ra = ta * TR, rb = tb * TR < n ? tb * TR : n;
-            const int64_t ka = rp[ra], kb = rp[rb];
-            // row pointers: one 4-B load per 64 B
-            for (int64_t o = ((ra * 8) & ~(int64_t)63) + 64 * tid; o < (rb + 1) * 8; o += 64 * 256)
-                acc ^= *reinterpret_cast<const uint32_t *>(reinterpret_cast<const char *>(rp) + o);
-            // values: one 4-B load per 64 B
-            for (int64_t o = ((ka * vsz) & ~(int64_t)63) + 64 * tid; o < kb * vsz; o += 64 * 256)
-                acc ^= *reinterpret_cast<const uint32_t *>(val + o);
-            // columns: all of them, 16 B per lane (their range sets the X rows)
-            int lmin = 0x7fffffff, lmax = -1;
-            const int64_t a4 = ka & ~(int64_t)3;
-            for (int64_t k = a4 + 4 * tid; k < kb; k += 4 * 256) {
-                int cv[4] = {0, 0, 0, 0};
-                if (k + 4 <= kb) {
-                    const int4 v = *reinterpret_cast<const int4 *>(col + k);
-                    cv[0] = v.x; cv[1] = v.y; cv[2] = v.z; cv[3] = v.w;
-                } else {
-                    for (int e = 0; e < 4 && k + e < kb; ++e) cv[e] = col[k + e];
-                }
-#pragma unroll
-                for (int e = 0; e < 4; ++e)
-                    if (k + e >= ka && k + e < kb) {
-                        lmin = cv[e] < lmin ? cv[e] : lmin;
-                        lmax = cv[e] > lmax ? cv[e] : lmax;
-                    }
-            }
-#pragma unroll
-            for (int o = 32; o > 0; o >>= 1) {
-                const int a = __shfl_xor(lmin, o, 64), b2 = __shfl_xor(lmax, o, 64);
-                lmin = a < lmin ? a : lmin;
-                lmax = b2 > lmax ? b2 : lmax;
-            }
-            if ((tid & 63) == 0) {
-                atomicMin(&s_min, lmin);
-                atomicMax(&s_max, lmax);
-            }
-            __syncthreads();
-            if (tid == 0) {
-                int lo = -1;
-                if (s_max >= 0) {
-                    const int old =
-                        __hip_atomic_fetch_max(&ctl[32 * x + 3], s_max, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
-                    lo = old + 1 > s_min ? old + 1 : s_min;
-                    if (s_max - lo >= maxspan) lo = -1;  // not a band: leave X alone
-                }
-                s_lo = lo;
-            }
-            __syncthreads();
-            if (s_lo >= 0 && s_lo <= s_max)
-                for (int64_t o = (int64_t)s_lo * rowb + 64 * tid; o < ((int64_t)s_max + 1) * rowb; o += 64 * 256)
-                    acc ^= *reinterpret_cast<const uint32_t *>(X + o);
-        }
-        __syncthreads();  // s_c / s_min / s_max / s_lo are rewritten by the next claim
+        if (c < 0) continue;
+        const int64_t ta = t0 + c * C, tb = (c + 1) * C < len ? ta + C : t0 + len;
+        const int64_t ra = ta * TR, rb = tb * TR < n ? tb * TR : n;
+        const int64_t ka = rp[ra], kb = rp[rb];
+        stream(reinterpret_cast<const char *>(rp), ra * 8, (rb + 1) * 8);
+        stream(reinterpret_cast<const char *>(col), ka * 4, kb * 4);
+        stream(val, ka * vsz, kb * vsz);
+        int64_t x0 = c == 0 ? ra - hw : ra + hw, x1 = rb + hw;
+        x0 = x0 < 0 ? 0 : x0;
+        x1 = x1 > nx ? nx : x1;
+        stream(X, x0 * rowb, x1 * rowb);
     }
-    if (acc == 0x9e3779b9u) sink[tid] = acc;  // (keeps the loads)
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // (no DMA into LDS the block has released)
+}
+
+// the operator's band: max |column - row| (the prefetcher's X lead), atomics
+// on one word
+__global__ __launch_bounds__(256) void k_band(int64_t n, const int64_t *__restrict__ rp,
+                                              const int32_t *__restrict__ col, int *__restrict__ out)
+{
+    int m = 0;
+    for (int64_t r = (int64_t)blockIdx.x * 256 + threadIdx.x; r < n; r += (int64_t)gridDim.x * 256)
+        for (int64_t k = rp[r]; k < rp[r + 1]; ++k) {
+            const int64_t d = (int64_t)col[k] - r;
+            const int a = (int)(d < 0 ? -d : d);
+            m = a > m ? a : m;
+        }
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) {
+        const int v = __shfl_xor(m, o, 64);
+        m = v > m ? v : m;
+    }
+    if ((threadIdx.x & 63) == 0) atomicMax(out, m);
 }
 
 __global__ void k_pf_init(int *ctl)
@@ -1314,9 +1307,9 @@ static int ensure_longq(lz_handle *h, int64_t st)
 }
 
 // LZ_SPMM_PF = "k[,C[,D[,span]]]" (read per call): the CU-partitioned SpMM with k
-// of every 8 CUs of each XCD prefetching (0: off), chunks of C tiles, at most
-// D tiles ahead of the XCD's dispatch front, X rows only for column spans
-// under `span` rows.  LZ_SPMM_PF_MAP selects which mask bits are an XCD's
+// of every 8 CUs of each XCD prefetching (0: off), chunks of C tiles (0: no
+// prefetch kernel, the tile kernel alone on its CUs), at most D tiles ahead of
+// the XCD's dispatch front, X rows only for a band under `span` rows.  LZ_SPMM_PF_MAP selects which mask bits are an XCD's
 // CUs (0: bit i is CU i / 8 of XCC i % 8).
 static bool pf_config(int *k, int *C, int *D, int *span)
 {
@@ -1324,7 +1317,7 @@ static bool pf_config(int *k, int *C, int *D, int *span)
     if (!e || !*e) return false;
     int v[4] = {0, *C, *D, *span};
     const int got = sscanf(e, "%d,%d,%d,%d", &v[0], &v[1], &v[2], &v[3]);
-    if (got < 1 || v[0] < 0 || v[0] > 7 || v[1] < 1 || v[2] < 0 || v[3] < 1) return false;
+    if (got < 1 || v[0] < 0 || v[0] > 7 || v[1] < 0 || v[2] < 0 || v[3] < 1) return false;
     *k = v[0];
     *C = v[1];
     *D = v[2];
@@ -1365,19 +1358,37 @@ static int launch_seg_pf(lz_handle *h, int64_t n, const int64_t *rp, const int32
 {
     const int64_t st = ceil_div(n, (int64_t)TR);
     LZ_TRY(pf_setup(h, k));
+    // the operator's band, once per operator (keyed by its arrays and sizes)
+    if (C > 0 && !(h->pf_band_key[0] == (int64_t)(uintptr_t)rp && h->pf_band_key[1] == (int64_t)(uintptr_t)col &&
+                   h->pf_band_key[2] == n)) {
+        int *band = h->pf_ctl + kPfCtl;
+        LZ_HIP_TRY(hipMemsetAsync(band, 0, sizeof(int), h->stream));
+        hipLaunchKernelGGL(k_band, dim3((unsigned)std::max<int64_t>(1, std::min<int64_t>(ceil_div(n, 256), 2048))),
+                           dim3(256), 0, h->stream, n, rp, col, band);
+        LZ_HIP_TRY(hipMemcpyAsync(&h->pf_band, band, sizeof(int), hipMemcpyDeviceToHost, h->stream));
+        LZ_HIP_TRY(hipStreamSynchronize(h->stream));
+        h->pf_band_key[0] = (int64_t)(uintptr_t)rp;
+        h->pf_band_key[1] = (int64_t)(uintptr_t)col;
+        h->pf_band_key[2] = n;
+    }
     const int parity = h->longq_parity;
     h->longq_parity ^= 1;
     hipLaunchKernelGGL(k_pf_init, dim3(1), dim3(kPfCtl), 0, h->stream, h->pf_ctl);
     LZ_HIP_TRY(hipEventRecord(h->ev_pff, h->stream));
     LZ_HIP_TRY(hipStreamWaitEvent(h->pf_sg, h->ev_pff, 0));
     LZ_HIP_TRY(hipStreamWaitEvent(h->pf_sp, h->ev_pff, 0));
-    // 4 blocks per prefetching CU (4 k CUs per XCD)
-    const int gp = 8 * 4 * k * 4;
-    hipLaunchKernelGGL((k_spmm_pf<TR>), dim3(gp), dim3(256), 0, h->pf_sp, n, st, rp, col,
-                       reinterpret_cast<const char *>(val), (int)sizeof(T), reinterpret_cast<const char *>(X),
-                       (int)(ldx * sizeof(T)), h->pf_ctl, C, D, span, reinterpret_cast<uint32_t *>(h->pf_ctl + kPfCtl));
+    // the tile kernel first (the two masked streams have queues of their own:
+    // profiles/r06h_pf_trace.csv shows both kernels running at once)
     hipLaunchKernelGGL((k_spmm_seg<T, B, TR, CAP, false, 0, false, false, true>), dim3((unsigned)st), dim3(256), 0,
                        h->pf_sg, n, rp, col, val, X, ldx, nx, Y, ldy, h->longq, parity, nullptr, nullptr, 0, h->pf_ctl);
+    // C = 0: the tile kernel alone on its CUs (the masked launch's own cost);
+    // 8 blocks per prefetching CU (4 k CUs per XCD); a band wider than `span`
+    // rows gets no X prefetch
+    if (C > 0)
+        hipLaunchKernelGGL((k_spmm_pf<TR>), dim3(8 * 4 * k * 8), dim3(256), 0, h->pf_sp, n, st, rp, col,
+                           reinterpret_cast<const char *>(val), (int)sizeof(T), reinterpret_cast<const char *>(X),
+                           h->pf_band < span ? nx : (int64_t)0, (int)(ldx * sizeof(T)), h->pf_ctl, C, D,
+                           (int64_t)h->pf_band);
     const int g2 = (int)std::max<int64_t>(1, std::min<int64_t>(st, (int64_t)h->n_cu * 4));
     hipLaunchKernelGGL((k_spmm_seg<T, B, TR, CAP, false, 1>), dim3(g2), dim3(256), 0, h->pf_sg, n, rp, col, val, X, ldx,
                        nx, Y, ldy, h->longq, parity, nullptr, nullptr, 0, nullptr);
@@ -1533,7 +1544,10 @@ int spmm_b2_stage(lz_handle *h, int64_t n, const int64_t *rp, int *cap)
     *cap = 768;
     if (n <= 0) return LZ_OK;
     const int64_t tiles = ceil_div(n, (int64_t)48);
-    int *dcount = reinterpret_cast<int *>(h->scratch + 4 * kMaxB * kMaxB - 1);  // (one spare word)
+    // a named slot of the handle's flag block ([0] the device error word, [8], [9]
+    // and [12..15] the plans' words), not a word of the scratch the solve's b x b
+    // matrices use
+    int *dcount = h->err_flag + 4;
     LZ_HIP_TRY(hipMemsetAsync(dcount, 0, sizeof(int), h->stream));
     hipLaunchKernelGGL(k_tile_overflow, dim3((unsigned)ceil_div(tiles, (int64_t)256)), dim3(256), 0, h->stream, n, rp,
                        1024, dcount);

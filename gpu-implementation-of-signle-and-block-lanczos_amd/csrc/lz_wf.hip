@@ -761,16 +761,35 @@ __global__ __launch_bounds__(64 * (NC + NL + NU)) void k_wf16(
     }
 }
 
+// The step shape wf_plan16 takes for rows of this density, read from the
+// same knobs by wf_plan16 and wf_first_gram (one rule): 200 the
+// wide shape (more than 10.2 entries per row), 111 the default one (1 loader
+// + 11 consumers + 4 updaters), 0 a measurement shape LZ_WF_SHAPE = 10 / 11 /
+// 12 (2 loaders, NC consumers, 14 - NC updaters; *nc = NC); *allowed = false
+// when LZ_PASS_WF=0 selects the two-pass step or the rows reach 2^24.  Read
+// per call.
+static int wf_shape(int64_t n, int64_t nnz, int *nc, bool *allowed)
+{
+    const char *e = getenv("LZ_PASS_WF");  // "0": the two-pass step (A/B)
+    const char *sh = getenv("LZ_WF_SHAPE");  // consumers per block (A/B)
+    const int want = sh ? atoi(sh) : 111;
+    const bool wide = (double)nnz > 10.2 * (double)n;
+    const int var = wide ? 200 : (want == 10 || want == 11 || want == 12) ? 0 : 111;
+    *nc = var == 200 ? 10 : var ? 11 : want;
+    *allowed = !(e && e[0] == '0') && n < (1 << 24);
+    return var;
+}
+
 // Whether wf_plan16 will most likely pick the default wavefront shape, whose
 // first launch can sum beta_0's Gram (XO 1): the solve then skips the separate
-// Gram (it would share the fabric with the plan).
+// Gram (it would share the fabric with the plan).  (The plan may still refuse
+// the rows -- too few, or columns out of reach -- and the solve then runs the
+// Gram itself: correct, only not beside the plan.)
 bool wf_first_gram(int64_t n, int64_t nnz)
 {
-    const char *e = getenv("LZ_PASS_WF");
-    const char *sh = getenv("LZ_WF_SHAPE");
-    const int want = sh ? atoi(sh) : 111;
-    return !(e && e[0] == '0') && n < (1 << 24) && !((double)nnz > 10.2 * (double)n) &&
-           !(want == 10 || want == 11 || want == 12);
+    int nc = 0;
+    bool allowed = false;
+    return wf_shape(n, nnz, &nc, &allowed) == 111 && allowed;
 }
 
 int wf_plan16(lz_handle *h, int64_t n, int64_t nnz, const int64_t *rp, const int32_t *col, WfPlan *pl, int64_t nx,
@@ -780,21 +799,15 @@ int wf_plan16(lz_handle *h, int64_t n, int64_t nnz, const int64_t *rp, const int
     pl->ok = false;
     pl->planned = false;
     pl->col16 = nullptr;
-    const char *e = getenv("LZ_PASS_WF");  // "0": the two-pass step (A/B); read per call
     // rows of about 11 entries or fewer on average: the tile's CSR run fits the
     // kWfCapPerRow-entry-per-row stage; up to kWfWideRow: the wide shape (longer
     // runs take a slow global-gather path)
-    const char *sh = getenv("LZ_WF_SHAPE");  // consumers per block (A/B); read per call
-    const int want = sh ? atoi(sh) : 111;
-    // 111 (default): 1 loader, 11 consumers, 4 updaters; 10 / 11 / 12: 2
-    // loaders, NC consumers, 14 - NC updaters
-    const bool wide = (double)nnz > 10.2 * (double)n;
-    pl->var = wide ? 200 : (want == 10 || want == 11 || want == 12) ? 0 : 111;
-    pl->nc = pl->var == 200 ? 10 : pl->var ? 11 : want;
+    bool allowed = false;
+    pl->var = wf_shape(n, nnz, &pl->nc, &allowed);
     pl->tr = 16 * pl->nc;
     // (a gather source of 2^24+ rows is read through per-strip windows: the
     // plan below checks that every column falls inside its strip's)
-    if ((e && e[0] == '0') || n < pl->tr || n >= (1 << 24) || xoff < 0 || xoff + n > nx ||
+    if (!allowed || n < pl->tr || xoff < 0 || xoff + n > nx ||
         (double)nnz > kWfWideRow * (double)n)
         return LZ_OK;
     const int64_t T = ceil_div(n, (int64_t)pl->tr);

@@ -37,7 +37,7 @@ def main():
     q, al, be = torch.zeros(m * b, **kw), torch.zeros(m, b, b, **kw), torch.zeros(m + 1, b, b, **kw)
     P = [torch.zeros(n, b, **kw) for _ in range(3)]
     base = dict(os.environ)
-    res = {c: {"it": [], "spmm": []} for c in args.cfgs}
+    res = {c: {"it": [], "spmm": [], "el": [], "ub": []} for c in args.cfgs}
     ref = None
     for rnd in range(args.rounds):
         for c in args.cfgs:
@@ -56,6 +56,8 @@ def main():
             e1.record()
             torch.cuda.synchronize()
             sp, cnt = h.prof_read(h.PROF_SPMM)
+            el, cel = h.prof_read(h.PROF_SPMM_PASS)  # pass EL (beta^2 form) / pass E
+            ub, cub = h.prof_read(h.PROF_UPDATE_PASS)  # pass UB / pass U
             h.prof_enable(False)
             a = al.cpu().numpy()
             if ref is None:
@@ -65,7 +67,10 @@ def main():
                 raise RuntimeError(f"alpha differs under {c}: {d}")
             res[c]["it"].append(e0.elapsed_time(e1) / m)
             res[c]["spmm"].append(sp / max(cnt, 1))
-            print(f"round {rnd} [{c}] step {res[c]['it'][-1]:.4f} ms  spmm {res[c]['spmm'][-1]:.4f} ms  d {d:.1e}", flush=True)
+            res[c]["el"].append(el / max(cel, 1))
+            res[c]["ub"].append(ub / max(cub, 1))
+            print(f"round {rnd} [{c}] step {res[c]['it'][-1]:.4f} ms  spmm {res[c]['spmm'][-1]:.4f} ms  "
+                  f"el {res[c]['el'][-1]:.4f} ms  ub {res[c]['ub'][-1]:.4f} ms  d {d:.1e}", flush=True)
     print(json.dumps({c: {k: round(float(np.median(v)), 4) for k, v in r.items()} for c, r in res.items()}, indent=1))
 
 
