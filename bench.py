@@ -49,6 +49,7 @@ import __graft_entry__ as ge  # noqa: E402
 HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec (MI355X_MICROARCH.md)
 FP64_MFMA_PEAK_TFS = 78.6  # v_mfma_f64_16x16x4f64: 32 FLOP/clk/SIMD x 1024 SIMDs x 2.4 GHz
 RITZ_TOL = 1e-10  # BASELINE.json north star: Ritz values within 1e-10 of the reference
+SPMM_ALL_L2_MS = 0.770  # the plain SpMM's all-L2 diagnostic at C3, round 6 (profiles/r06l_spmm_l2_ceiling.log)
 
 
 def log(*a):
@@ -553,6 +554,15 @@ def main():
                              "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": round(gbs / HBM_PEAK_GBS, 4),
                              "traffic": trp, "traffic_source": srcp, "avg_ms": round(ms / cnt, 4),
                              "bytes_per_launch": spmm_bytes(n, A.nnz, b)}
+        if n == 10_000_000 and args.nnz_per_row == 10.0 and args.halfwidth == 4096:
+            # the tile structure's own ceiling at C3 (DESIGN.md 4 SpMM): the same kernel and instruction
+            # stream with every input L2-resident (diagnostic build, LZ_SPMM_DIAG=64) -- what no HBM
+            # schedule can beat without fewer gathered lines per nonzero
+            plain["ceiling_frac"] = round(spmm_bytes(n, A.nnz, b) / SPMM_ALL_L2_MS * 1e-6 / HBM_PEAK_GBS, 4)
+            plain["ceiling_ms"] = SPMM_ALL_L2_MS
+            plain["ceiling_source"] = ("profiles/r06l_spmm_l2_ceiling.log: k_spmm_seg with every row pointer, CSR "
+                                       "entry and X row L2-resident (LZ_SPMM_DIAG=64, lib/liblz_hip_diag.so), "
+                                       "0.767-0.773 ms against 1.189 ms as it runs, same box")
         if not args.no_cpu_baseline:  # the CPU SpMM on the same operator and block
             orc = ge.load_oracle()
             Yc, tc = orc.csr_spmm_timed(A, B, reps=3)

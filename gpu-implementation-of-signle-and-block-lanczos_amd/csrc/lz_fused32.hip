@@ -372,8 +372,10 @@ __global__ __launch_bounds__(64 * kF32Waves) void k_fused_ub32d(int64_t n, const
 #pragma unroll
         for (int v = 0; v < 16; ++v) {
             const uint32_t rr = (uint32_t)((v & 3) + 8 * (v >> 2) + 4 * hh);
-            if (dbg & 2) __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(acc[v]), nr, rr * 128 + 4 * jr, 0, 2);
-            else __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(acc[v]), nr, rr * 128 + 4 * jr, 0, 0);
+            // non-temporal: the next step's SpMM gathers these rows at random (C5:
+            // SpMM 2.800 -> 2.787 ms, step 4.133 -> 4.112 ms, profiles/r06i_c5_ub_nt_ab.log)
+            if (dbg & 2) __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(acc[v]), nr, rr * 128 + 4 * jr, 0, 0);
+            else __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(acc[v]), nr, rr * 128 + 4 * jr, 0, 2);
         }
         if constexpr (QO) {
             f16v_t q;
@@ -399,6 +401,188 @@ __global__ __launch_bounds__(64 * kF32Waves) void k_fused_ub32d(int64_t n, const
     block_slab32<kF32Waves>(reinterpret_cast<double (*)[1024]>(&ust[0][0][0][0]), g, lane, w, part);
 }
 
+// The same staging for the pass-E form's two passes (round 6; LZ_UB_DMA=0
+// selects k_fused_e32 / k_fused_u32): every 32 x 32 fp32 operand strip a wave
+// reads comes in by LDS-DMA one strip ahead, swizzled as above; A-operands by
+// ds_read_b128, result-layout operands (row (v & 3) + 8 (v >> 2) + 4 hh,
+// column jr) by ds_read_b32.  The same products in the same order as the
+// register forms: the same bits.
+__device__ __forceinline__ void dma_strip32(const float *M, int64_t r0, int64_t rows, float *slot, uint32_t goff)
+{
+    const __amdgpu_buffer_rsrc_t r = ub_rsrc(M + (rows ? r0 * 32 : 0), rows);
+#pragma unroll
+    for (int k = 0; k < 4; ++k)  // rows past the strip's end: out of range, land as zeros
+        __builtin_amdgcn_raw_ptr_buffer_load_lds(r, (ws_lds_t *)&slot[256 * k], 16, goff + 1024 * k, 0, 0, 0);
+}
+
+// a[s] = strip row jr, float 16 hh + s (the MFMA A-operand), from a swizzled slot
+__device__ __forceinline__ void aop_slot(uint32_t sb, int jr, int hh, float a[16])
+{
+    const uint32_t rb = sb + (uint32_t)(jr * 128);
+    float4 x[4];
+    asm volatile(
+        "ds_read_b128 %0, %4\n\t"
+        "ds_read_b128 %1, %5\n\t"
+        "ds_read_b128 %2, %6\n\t"
+        "ds_read_b128 %3, %7\n\t"
+        "s_waitcnt lgkmcnt(0)"
+        : "=&v"(x[0]), "=&v"(x[1]), "=&v"(x[2]), "=&v"(x[3])
+        : "v"(rb + 16u * (uint32_t)((4 * hh + 0) ^ (jr & 7))), "v"(rb + 16u * (uint32_t)((4 * hh + 1) ^ (jr & 7))),
+          "v"(rb + 16u * (uint32_t)((4 * hh + 2) ^ (jr & 7))), "v"(rb + 16u * (uint32_t)((4 * hh + 3) ^ (jr & 7)))
+        : "memory");
+#pragma unroll
+    for (int c = 0; c < 4; ++c) {
+        a[4 * c] = x[c].x; a[4 * c + 1] = x[c].y; a[4 * c + 2] = x[c].z; a[4 * c + 3] = x[c].w;
+    }
+}
+
+// r[v] = strip row (v & 3) + 8 (v >> 2) + 4 hh, column jr (the MFMA result
+// layout; row rr's chunk jr / 4 sits at position 8 rr + ((jr / 4) ^ (rr & 7))).
+// Two asm statements of eight reads and their wait each: the values may be
+// used only after the wait, which the compiler cannot see across statements.
+__device__ __forceinline__ void rop_slot(uint32_t sb, int jr, int hh, f16v_t &r)
+{
+    uint32_t a[16];
+#pragma unroll
+    for (int i = 0; i < 16; ++i) {
+        const int rr = (i & 3) + 8 * (i >> 2) + 4 * hh;
+        a[i] = sb + (uint32_t)(rr * 128) + 16u * (uint32_t)((jr >> 2) ^ (rr & 7)) + 4u * (uint32_t)(jr & 3);
+    }
+    float v[16];
+#pragma unroll
+    for (int hf = 0; hf < 2; ++hf)
+        asm volatile(
+            "ds_read_b32 %0, %8\n\t"
+            "ds_read_b32 %1, %9\n\t"
+            "ds_read_b32 %2, %10\n\t"
+            "ds_read_b32 %3, %11\n\t"
+            "ds_read_b32 %4, %12\n\t"
+            "ds_read_b32 %5, %13\n\t"
+            "ds_read_b32 %6, %14\n\t"
+            "ds_read_b32 %7, %15\n\t"
+            "s_waitcnt lgkmcnt(0)"
+            : "=&v"(v[8 * hf]), "=&v"(v[8 * hf + 1]), "=&v"(v[8 * hf + 2]), "=&v"(v[8 * hf + 3]),
+              "=&v"(v[8 * hf + 4]), "=&v"(v[8 * hf + 5]), "=&v"(v[8 * hf + 6]), "=&v"(v[8 * hf + 7])
+            : "v"(a[8 * hf]), "v"(a[8 * hf + 1]), "v"(a[8 * hf + 2]), "v"(a[8 * hf + 3]), "v"(a[8 * hf + 4]),
+              "v"(a[8 * hf + 5]), "v"(a[8 * hf + 6]), "v"(a[8 * hf + 7])
+            : "memory");
+#pragma unroll
+    for (int i = 0; i < 16; ++i) r[i] = v[i];
+}
+
+// Pass U (DMA form): Wn <- Wn - Wj P2, slabs of Wn^T Wn
+__global__ __launch_bounds__(64 * kF32Waves) void k_fused_u32d(int64_t n, float *__restrict__ Wn,
+                                                               const float *__restrict__ Wj,
+                                                               const float *__restrict__ P2,
+                                                               double *__restrict__ part)
+{
+    __shared__ __attribute__((aligned(16))) float ust[kF32Waves][2][2][1024];  // slots x (W_j, Wn) strips
+    const int lane = threadIdx.x & 63, w = __builtin_amdgcn_readfirstlane((int)(threadIdx.x >> 6)), hh = lane >> 5,
+              jr = lane & 31;
+    float bo[16];
+    bop32(P2, -1.0f, hh, jr, bo);
+    f16v_t g;
+#pragma unroll
+    for (int v = 0; v < 16; ++v) g[v] = 0.0f;
+    XcdSched sch(ceil_div(n, (int64_t)(32 * kF32Waves)));
+    const int64_t nst = sch.end > sch.begin ? (sch.end - sch.begin + sch.step - 1) / sch.step : 0;
+    const uint32_t goff = (uint32_t)((lane >> 3) * 128 + 16 * ((lane & 7) ^ ((lane >> 3) & 7)));
+    auto rows_of = [&](int64_t s, int64_t *r0) {
+        *r0 = (sch.begin + s * sch.step) * (32 * kF32Waves) + 32 * w;
+        return s < nst && *r0 < n ? (n - *r0 < 32 ? n - *r0 : (int64_t)32) : (int64_t)0;
+    };
+    auto dma = [&](int64_t s) {
+        int64_t r0;
+        const int64_t rows = rows_of(s, &r0);
+        dma_strip32(Wj, r0, rows, &ust[w][s & 1][0][0], goff);
+        dma_strip32(Wn, r0, rows, &ust[w][s & 1][1][0], goff);
+    };
+    dma(0);
+    for (int64_t s = 0; s < nst; ++s) {
+        dma(s + 1);
+        asm volatile("s_waitcnt vmcnt(8)" ::: "memory");  // strip s in (loads return in order)
+        const uint32_t sb = ws_lds_addr(reinterpret_cast<int *>(&ust[w][(int)(s & 1)][0][0]));
+        float wa[16];
+        aop_slot(sb, jr, hh, wa);
+        f16v_t acc;  // W' in result layout
+        rop_slot(sb + 4096, jr, hh, acc);
+#pragma unroll
+        for (int s2 = 0; s2 < 16; ++s2) acc = mfma32(wa[s2], bo[s2], acc);
+        int64_t r0;
+        const int64_t rows = rows_of(s, &r0);
+        const __amdgpu_buffer_rsrc_t nr = ub_rsrc(Wn + (rows ? r0 * 32 : 0), rows);
+#pragma unroll
+        for (int v = 0; v < 16; ++v) {
+            const uint32_t rr = (uint32_t)((v & 3) + 8 * (v >> 2) + 4 * hh);
+            __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(acc[v]), nr, rr * 128 + 4 * jr, 0, 0);
+        }
+#pragma unroll
+        for (int v = 0; v < 16; ++v) g = mfma32(acc[v], acc[v], g);
+    }
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+    block_slab32<kF32Waves>(reinterpret_cast<double (*)[1024]>(&ust[0][0][0][0]), g, lane, w, part);
+}
+
+// Pass E (DMA form).  Wprev may alias Wn: strip s's rows are in LDS before the
+// wave stores them, and the other strips' rows are not its.  One strip slot
+// per wave (three operand strips, 12 KB; 2 blocks per CU at 190 registers).
+__global__ __launch_bounds__(64 * kF32Waves) void k_fused_e32d(int64_t n, const float *__restrict__ Y,
+                                                               const float *__restrict__ Wj, const float *Wprev,
+                                                               float *Wn, const float *__restrict__ binv,
+                                                               const float *__restrict__ P1, int64_t lc,
+                                                               float *__restrict__ qrow, double *__restrict__ part)
+{
+    __shared__ __attribute__((aligned(16))) float ust[kF32Waves][3][1024];
+    const int lane = threadIdx.x & 63, w = __builtin_amdgcn_readfirstlane((int)(threadIdx.x >> 6)), hh = lane >> 5,
+              jr = lane & 31;
+    const bool has_prev = P1 != nullptr;
+    float bo[16], po[16];
+    bop32(binv, 1.0f, hh, jr, bo);
+    if (has_prev) bop32(P1, -1.0f, hh, jr, po);
+    f16v_t slab;
+#pragma unroll
+    for (int v = 0; v < 16; ++v) slab[v] = 0.0f;
+    XcdSched sch(ceil_div(n, (int64_t)(32 * kF32Waves)));
+    const uint32_t goff = (uint32_t)((lane >> 3) * 128 + 16 * ((lane & 7) ^ ((lane >> 3) & 7)));
+    const uint32_t sb = ws_lds_addr(reinterpret_cast<int *>(&ust[w][0][0]));
+    for (int64_t u = sch.begin; u < sch.end; u += sch.step) {
+        const int64_t r0 = u * (32 * kF32Waves) + 32 * w;
+        const int64_t rows = r0 < n ? (n - r0 < 32 ? n - r0 : (int64_t)32) : (int64_t)0;
+        dma_strip32(Wj, r0, rows, &ust[w][0][0], goff);
+        dma_strip32(Y, r0, rows, &ust[w][1][0], goff);
+        dma_strip32(has_prev ? Wprev : Wj, r0, has_prev ? rows : 0, &ust[w][2][0], goff);
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        float wa[16], ya[16], pa[16];
+        aop_slot(sb, jr, hh, wa);
+        aop_slot(sb + 4096, jr, hh, ya);
+        if (has_prev) aop_slot(sb + 8192, jr, hh, pa);
+        f16v_t q, wn;
+#pragma unroll
+        for (int v = 0; v < 16; ++v) q[v] = wn[v] = 0.0f;
+#pragma unroll
+        for (int s = 0; s < 16; ++s) q = mfma32(wa[s], bo[s], q);     // Q_j = W_j beta^-1
+#pragma unroll
+        for (int s = 0; s < 16; ++s) wn = mfma32(ya[s], bo[s], wn);   // Y beta^-1
+        if (has_prev) {
+#pragma unroll
+            for (int s = 0; s < 16; ++s) wn = mfma32(pa[s], po[s], wn);  // - W_{j-1} P1
+        }
+        const __amdgpu_buffer_rsrc_t nr = ub_rsrc(Wn + (rows ? r0 * 32 : 0), rows);
+#pragma unroll
+        for (int v = 0; v < 16; ++v) {
+            const int64_t rr = (v & 3) + 8 * (v >> 2) + 4 * hh;
+            __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(wn[v]), nr, (uint32_t)(rr * 128 + 4 * jr), 0, 0);
+            if (r0 + rr == lc && rr < rows) qrow[jr] = q[v];
+        }
+#pragma unroll
+        for (int v = 0; v < 16; ++v) slab = mfma32(q[v], wn[v], slab);  // Q_j^T W' (rows past n: 0)
+    }
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+    block_slab32<kF32Waves>(reinterpret_cast<double (*)[1024]>(&ust[0][0][0]), slab, lane, w, part);
+}
+
 // blocks per CU: pass E (190 registers: 2 waves per SIMD) 2; pass U 4.
 // Measured at C5 (ms, E / U): grid 1x 1.12 / 0.91, 2x 0.96 / 0.78, 3x 1.20 / 0.78, 4x - / 0.76.
 static int f32_grid(lz_handle *h, int64_t n, int mult)
@@ -412,8 +596,13 @@ int fused_e32(lz_handle *h, int64_t n, const float *Y, const float *Wj, const fl
     const int grid = f32_grid(h, n, 2);
     LZ_TRY(ensure_partials(h, (size_t)grid * 1024));
     const int ev = prof_begin(h, PROF_SPMM_PASS);
-    hipLaunchKernelGGL(k_fused_e32, dim3(grid), dim3(64 * kF32Waves), 0, h->stream, n, Y, Wj, Wprev, Wn, binv, P1,
-                       lc, qrow, h->partials);
+    const char *ud = getenv("LZ_UB_DMA");  // "0": the register-operand forms (A/B; read per call)
+    if (!(ud && ud[0] == '0'))
+        hipLaunchKernelGGL(k_fused_e32d, dim3(grid), dim3(64 * kF32Waves), 0, h->stream, n, Y, Wj, Wprev, Wn, binv, P1,
+                           lc, qrow, h->partials);
+    else
+        hipLaunchKernelGGL(k_fused_e32, dim3(grid), dim3(64 * kF32Waves), 0, h->stream, n, Y, Wj, Wprev, Wn, binv, P1,
+                           lc, qrow, h->partials);
     prof_end(h, ev);
     LZ_LAUNCH_CHECK();
     *nparts = grid;
@@ -441,7 +630,7 @@ int fused_ub32(lz_handle *h, int64_t n, const float *U, const float *Wj, const f
     const int ev = prof_begin(h, PROF_UPDATE_PASS);
     const char *ud = getenv("LZ_UB_DMA");  // "0": the register-operand form (A/B; read per call)
     const bool dma = !(ud && ud[0] == '0');
-    // (A/B: LZ_UB_DMA=3 drains every load before each strip, 5 stores W'' non-temporal)
+    // (A/B: LZ_UB_DMA=3 drains every load before each strip, 5 stores W'' with the default policy)
     const int dbg = ud ? atoi(ud) >> 1 : 0;
     if (dma && Qa)
         hipLaunchKernelGGL(k_fused_ub32d<true>, dim3(grid), dim3(64 * kF32Waves), 0, h->stream, n, U, Wj, binv, P2, Wn,
@@ -466,7 +655,11 @@ int fused_u32(lz_handle *h, int64_t n, float *Wn, const float *Wj, const float *
     const int grid = f32_grid(h, n, 4);
     LZ_TRY(ensure_partials(h, (size_t)grid * 1024));
     const int ev = prof_begin(h, PROF_UPDATE_PASS);
-    hipLaunchKernelGGL(k_fused_u32, dim3(grid), dim3(64 * kF32Waves), 0, h->stream, n, Wn, Wj, P2, h->partials);
+    const char *ud = getenv("LZ_UB_DMA");  // "0": the register-operand forms (A/B; read per call)
+    if (!(ud && ud[0] == '0'))
+        hipLaunchKernelGGL(k_fused_u32d, dim3(grid), dim3(64 * kF32Waves), 0, h->stream, n, Wn, Wj, P2, h->partials);
+    else
+        hipLaunchKernelGGL(k_fused_u32, dim3(grid), dim3(64 * kF32Waves), 0, h->stream, n, Wn, Wj, P2, h->partials);
     prof_end(h, ev);
     LZ_LAUNCH_CHECK();
     *nparts = grid;

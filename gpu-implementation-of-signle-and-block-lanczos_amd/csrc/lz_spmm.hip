@@ -386,7 +386,8 @@ __device__ __forceinline__ Vec<T, VEC> epi_piece(Vec<T, VEC> y, const T *__restr
     return y;
 }
 
-// ---- CU-partitioned SpMM (LZ_SPMM_PF; DESIGN.md 4 SpMM "Round 6") ----
+// ---- CU-partitioned SpMM (LZ_SPMM_PF, diagnostic build only: measured and
+// dropped in round 6, DESIGN.md 4 SpMM "Round 6") ----
 // The tile kernel runs on a stream masked to most of each XCD's CUs; a
 // prefetch kernel on the rest pulls the CSR runs, row pointers and the X rows
 // the XCD's next tiles touch first into that XCD's L2, paced by the number of
@@ -399,7 +400,7 @@ __device__ __forceinline__ Vec<T, VEC> epi_piece(Vec<T, VEC> y, const T *__restr
 //   [32 x + 1]  XCC x's block group blockIdx % 8    (tile kernel; -1 until known)
 //   [32 x + 2]  prefetch chunk ticket
 //   [32 x + 3]  highest X row prefetched (-1 at the start)
-constexpr int kPfCtl = 256;
+[[maybe_unused]] constexpr int kPfCtl = 256;
 
 __device__ __forceinline__ int xcc_id()
 {
@@ -780,6 +781,7 @@ __global__ __launch_bounds__(256) void k_spmm_seg(int64_t n, const int64_t *__re
     }  // MODE 0
 }
 
+#ifdef LZ_DIAG  // (measured and dropped in round 6: the diagnostic build only)
 // The prefetch side of the CU-partitioned SpMM.  Persistent blocks, each on
 // the XCD it reads from HW_REG_XCC_ID: the XCD's tiles (xcd_remap's range for
 // its block group) are cut into chunks of C tiles, claimed in order by ticket;
@@ -894,6 +896,7 @@ __global__ void k_pf_init(int *ctl)
     const int i = threadIdx.x;
     if (i < kPfCtl) ctl[i] = (i % 32 == 1 || i % 32 == 3) ? -1 : 0;
 }
+#endif  // LZ_DIAG
 
 // Row-major SpMM at a block width off the tuned set (b not a power of two):
 // thread (r, c) sums row r in CSR order; the b threads of a row read the same
@@ -1306,6 +1309,7 @@ static int ensure_longq(lz_handle *h, int64_t st)
     return LZ_OK;
 }
 
+#ifdef LZ_DIAG  // (measured and dropped in round 6: the diagnostic build only)
 // LZ_SPMM_PF = "k[,C[,D[,span]]]" (read per call): the CU-partitioned SpMM with k
 // of every 8 CUs of each XCD prefetching (0: off), chunks of C tiles (0: no
 // prefetch kernel, the tile kernel alone on its CUs), at most D tiles ahead of
@@ -1339,12 +1343,20 @@ static int pf_setup(lz_handle *h, int k)
         }
     uint32_t mg[8] = {}, mpf[8] = {};
     for (int i = 0; i < 256; ++i) {
-        // map 0: bit i -> CU i / 8 of XCC i % 8; map 1: bit i -> CU i % 32 of XCC i / 32
-        const int j = map == 0 ? i / 8 : i % 32;
-        (j % 8 < k ? mpf : mg)[i / 32] |= 1u << (i % 32);
+        // bit i -> XCC i % 8, local CU j = i / 8, which sits in shader engine
+        // j % 4 (scripts/gprobe/cumask_probe.hip, profiles/r06a_cumask_probe.log).
+        // The dispatcher deals workgroups evenly over the shader engines, so
+        // the prefetch CUs are taken evenly from each engine (map 0: slot
+        // j / 4 < k, k of each engine's 8); map 1 takes them from the low
+        // engines (j % 8 < k: an engine left with 4 of its 8 CUs at k = 2 --
+        // the tile kernel alone took 2.16 ms instead of 1.30 there,
+        // profiles/r06j_spmm_masked_stream_ab.log)
+        const int j = i / 8;
+        const bool pf = map == 0 ? (j / 4) < k : (j % 8) < k;
+        (pf ? mpf : mg)[i / 32] |= 1u << (i % 32);
     }
     LZ_HIP_TRY(hipExtStreamCreateWithCUMask(&h->pf_sg, 8, mg));
-    LZ_HIP_TRY(hipExtStreamCreateWithCUMask(&h->pf_sp, 8, mpf));
+    if (k > 0) LZ_HIP_TRY(hipExtStreamCreateWithCUMask(&h->pf_sp, 8, mpf));  // (k = 0: every CU on the tile stream)
     for (hipEvent_t *e : {&h->ev_pff, &h->ev_pfg, &h->ev_pfp})
         if (!*e) LZ_HIP_TRY(hipEventCreateWithFlags(e, hipEventDisableTiming));
     if (!h->pf_ctl) LZ_HIP_TRY(hipMalloc(&h->pf_ctl, sizeof(int) * (kPfCtl + 256)));
@@ -1359,7 +1371,7 @@ static int launch_seg_pf(lz_handle *h, int64_t n, const int64_t *rp, const int32
     const int64_t st = ceil_div(n, (int64_t)TR);
     LZ_TRY(pf_setup(h, k));
     // the operator's band, once per operator (keyed by its arrays and sizes)
-    if (C > 0 && !(h->pf_band_key[0] == (int64_t)(uintptr_t)rp && h->pf_band_key[1] == (int64_t)(uintptr_t)col &&
+    if (C > 0 && k > 0 && !(h->pf_band_key[0] == (int64_t)(uintptr_t)rp && h->pf_band_key[1] == (int64_t)(uintptr_t)col &&
                    h->pf_band_key[2] == n)) {
         int *band = h->pf_ctl + kPfCtl;
         LZ_HIP_TRY(hipMemsetAsync(band, 0, sizeof(int), h->stream));
@@ -1376,7 +1388,7 @@ static int launch_seg_pf(lz_handle *h, int64_t n, const int64_t *rp, const int32
     hipLaunchKernelGGL(k_pf_init, dim3(1), dim3(kPfCtl), 0, h->stream, h->pf_ctl);
     LZ_HIP_TRY(hipEventRecord(h->ev_pff, h->stream));
     LZ_HIP_TRY(hipStreamWaitEvent(h->pf_sg, h->ev_pff, 0));
-    LZ_HIP_TRY(hipStreamWaitEvent(h->pf_sp, h->ev_pff, 0));
+    if (k > 0) LZ_HIP_TRY(hipStreamWaitEvent(h->pf_sp, h->ev_pff, 0));
     // the tile kernel first (the two masked streams have queues of their own:
     // profiles/r06h_pf_trace.csv shows both kernels running at once)
     hipLaunchKernelGGL((k_spmm_seg<T, B, TR, CAP, false, 0, false, false, true>), dim3((unsigned)st), dim3(256), 0,
@@ -1384,7 +1396,7 @@ static int launch_seg_pf(lz_handle *h, int64_t n, const int64_t *rp, const int32
     // C = 0: the tile kernel alone on its CUs (the masked launch's own cost);
     // 8 blocks per prefetching CU (4 k CUs per XCD); a band wider than `span`
     // rows gets no X prefetch
-    if (C > 0)
+    if (C > 0 && k > 0)
         hipLaunchKernelGGL((k_spmm_pf<TR>), dim3(8 * 4 * k * 8), dim3(256), 0, h->pf_sp, n, st, rp, col,
                            reinterpret_cast<const char *>(val), (int)sizeof(T), reinterpret_cast<const char *>(X),
                            h->pf_band < span ? nx : (int64_t)0, (int)(ldx * sizeof(T)), h->pf_ctl, C, D,
@@ -1393,11 +1405,15 @@ static int launch_seg_pf(lz_handle *h, int64_t n, const int64_t *rp, const int32
     hipLaunchKernelGGL((k_spmm_seg<T, B, TR, CAP, false, 1>), dim3(g2), dim3(256), 0, h->pf_sg, n, rp, col, val, X, ldx,
                        nx, Y, ldy, h->longq, parity, nullptr, nullptr, 0, nullptr);
     LZ_HIP_TRY(hipEventRecord(h->ev_pfg, h->pf_sg));
-    LZ_HIP_TRY(hipEventRecord(h->ev_pfp, h->pf_sp));
     LZ_HIP_TRY(hipStreamWaitEvent(h->stream, h->ev_pfg, 0));
-    LZ_HIP_TRY(hipStreamWaitEvent(h->stream, h->ev_pfp, 0));
+    if (k > 0) {
+        LZ_HIP_TRY(hipEventRecord(h->ev_pfp, h->pf_sp));
+        LZ_HIP_TRY(hipStreamWaitEvent(h->stream, h->ev_pfp, 0));
+    }
     return LZ_OK;
 }
+
+#endif  // LZ_DIAG
 
 // nnz-split SpMM with the long-tile queue: the main kernel, then a persistent
 // kernel over the queued tiles (an empty queue costs one short launch).
@@ -1431,10 +1447,13 @@ static int launch_seg(lz_handle *h, int64_t n, const int64_t *rp, const int32_t 
         LZ_HIP_TRY(hipStreamWaitEvent(h->stream, h->ev_ljoin, 0));
         return LZ_OK;
     }
+#ifdef LZ_DIAG
     if constexpr (!WIN && !YCM && !EPI) {
         int k = 0, C = 8, D = 96, span = 65536;
-        if (pf_config(&k, &C, &D, &span) && k > 0) return launch_seg_pf<T, B, TR, CAP>(h, n, rp, col, val, X, ldx, nx, Y, ldy, k, C, D, span);
+        if (pf_config(&k, &C, &D, &span) && (k > 0 || C == 0))
+            return launch_seg_pf<T, B, TR, CAP>(h, n, rp, col, val, X, ldx, nx, Y, ldy, k, C, D, span);
     }
+#endif
     const int parity = h->longq_parity;
     h->longq_parity ^= 1;
     if (slot_out) *slot_out = parity;

@@ -504,6 +504,8 @@ __global__ __launch_bounds__(64 * (NC + NL + NU)) void k_wf16(
                     const int row = 4 * (2 * h2 + (ev ? 0 : 1)) + g;
                     const uint32_t off = r0b + (uint32_t)(row * 128 + (ev ? c : c - 1) * 8);
                     if (cpol & 8) __builtin_amdgcn_raw_buffer_store_b128(*reinterpret_cast<const v4u32_t *>(&v), Or, off, 0, SA | 2);
+                    else if (dbg & 128)  // (diagnostic: plain stores keep the line in this XCD's L2)
+                        __builtin_amdgcn_raw_buffer_store_b128(*reinterpret_cast<const v4u32_t *>(&v), Or, off, 0, 0);
                     else __builtin_amdgcn_raw_buffer_store_b128(*reinterpret_cast<const v4u32_t *>(&v), Or, off, 0, SA);
                 }
                 if constexpr (QO) {  // Q = V_j beta^-1, the same pair swap, two outputs
@@ -895,7 +897,9 @@ int wf_step16(lz_handle *h, int64_t n, const int64_t *rp, const int32_t *col, co
     // dbg: timing diagnostics (results are wrong), only in a -DLZ_DIAG build
     // (LZ_WF_DBG): bit 0 skips the loaders' flag polls, bit 1 the updaters'
     // work, bit 2 the pass-1 tiles; bit 3 / bit 6 run the updaters at issue
-    // priority 0 / 3 (default 2).  The shipped library always passes 0.
+    // priority 0 / 3 (default 2); bit 7 stores V_{j+1} plain instead of sc1
+    // (rows another XCD gathers then read stale).  The shipped library always
+    // passes 0.
 #ifdef LZ_DIAG
     const char *dg = getenv("LZ_WF_DBG");
     const int dbg = dg ? atoi(dg) : 0;

@@ -235,14 +235,18 @@ def test_block_f32_b32_powerlaw(lz, orc, handle, torch_cuda, monkeypatch, n, cap
     assert handle.device_error() == 0
 
 
+@pytest.mark.parametrize("form", ["b2", "e"])
 @pytest.mark.parametrize("n,m", [(20_011, 4), (100_003, 3), (33, 2)])
-def test_block_f32_b32_ub_dma_bitwise(lz, handle, torch_cuda, monkeypatch, n, m):
-    """Pass UB with its operands staged through LDS by DMA (k_fused_ub32d, the
-    default) against the register-operand form (LZ_UB_DMA=0): the same products
-    in the same order, so alpha, beta, q and the post-call Q0 / Q1 / W are the
-    same bits, including the ragged last strip (n not a multiple of 32) and the
-    last step's Q store (QO)."""
+def test_block_f32_b32_ub_dma_bitwise(lz, handle, torch_cuda, monkeypatch, n, m, form):
+    """The b = 32 fp32 dense passes with their operands staged through LDS by
+    DMA (the default: pass UB k_fused_ub32d in the beta^2 form; passes E and U,
+    k_fused_e32d / k_fused_u32d, in the pass-E form, LZ_C5_B2=0) against the
+    register-operand forms (LZ_UB_DMA=0): the same products in the same order,
+    so alpha, beta, q and the post-call Q0 / Q1 / W are the same bits, including
+    the ragged last strip (n not a multiple of 32) and the last step's Q store."""
     torch = torch_cuda
+    if form == "e":
+        monkeypatch.setenv("LZ_C5_B2", "0")
     A = lz.gen_powerlaw(n, 10.0, 2.1, max(2, n // 10), seed=n % 89, dtype=np.float32)
     B = lz.uniform_B(A.n, 32, seed=9, dtype=np.float32)
     Ad, Bd = lz.CsrDevice.from_host(A), torch.from_numpy(B).cuda()
