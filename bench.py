@@ -145,7 +145,7 @@ def spmm_kernel(nnz, n):
     """The plain SpMM kernel lz_csr_spmm launches for b = 16 fp64 (lz_spmm.hip launch_spmm_rm)."""
     cap = 1536 if nnz > 13.0 * n else 768
     win = n >= (1 << 24)
-    return f"k_spmm_seg<double,16,48,{cap},{'true' if win else 'false'},0,false,false>"
+    return f"k_spmm_seg<double,16,48,{cap},{'true' if win else 'false'},0,false,false,false>"
 
 
 # the source file of each profiled kernel: a committed counter file is used only
@@ -709,7 +709,7 @@ def main():
             # step 0 has no W_{j-1} term: A + 2 nbs, later steps A + 3 nbs
             sp5_b = k5p * (a5 + 2 * nbs5) + (k5p - 1) * nbs5
             t5 = sp5_ms * 1e-3
-            kn5 = "k_spmm_seg<float,32,48,1024,false,0,false,true>"
+            kn5 = "k_spmm_seg<float,32,48,1024,false,0,false,true,false>"
             tr5, src5 = pmc_traffic("k_spmm_seg_c5", n5, A5.nnz, 0, kn5)
             c5["roofline"] = {"bound": "hbm", "kernel": kn5 + " (+ its long-tile pass, MODE 1)",
                               "bytes_per_launch": round(sp5_b / k5p), "avg_ms": round(t5 / k5p * 1e3, 4),
