@@ -31,6 +31,7 @@
 namespace lz {
 
 typedef float f16v_t __attribute__((ext_vector_type(16)));
+typedef unsigned u4v_t __attribute__((ext_vector_type(4)));
 
 __device__ __forceinline__ f16v_t mfma32(float a, float b, f16v_t c)
 {
@@ -277,6 +278,31 @@ __device__ __forceinline__ __amdgpu_buffer_rsrc_t ub_rsrc(const float *p, int64_
     return __builtin_amdgcn_make_buffer_rsrc(const_cast<float *>(p), (short)0, (int)(rows * 128), 0x00020000);
 }
 
+// Store a 32 x 32 fp32 strip held in the MFMA result layout (lane (hh, jr):
+// row (v & 3) + 8 (v >> 2) + 4 hh, column jr) as whole rows: through a 4-KB
+// LDS slot of the wave's that it no longer reads (sixteen ds_write_b32, row
+// rr's chunk c at position 8 rr + (c ^ (rr & 7)) as the DMA layout), back as
+// four ds_read_b128 of 8 whole rows each, out as four 16-B stores (1 KB per
+// instruction) instead of sixteen 4-B ones.  Rows past the resource's end are
+// dropped.  The wave's reads of `slot` must be done before the call (they
+// are: their values feed the MFMAs that made `acc`).
+template <int AUX>
+__device__ __forceinline__ void rstore_slot(float *slot, const f16v_t &acc, int jr, int hh, int lane,
+                                            __amdgpu_buffer_rsrc_t nr)
+{
+#pragma unroll
+    for (int v = 0; v < 16; ++v) {
+        const int rr = (v & 3) + 8 * (v >> 2) + 4 * hh;
+        slot[rr * 32 + 4 * ((jr >> 2) ^ (rr & 7)) + (jr & 3)] = acc[v];
+    }
+    const int r8 = lane >> 3, c = lane & 7;
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+        const u4v_t x = *reinterpret_cast<const u4v_t *>(&slot[4 * (64 * k + 8 * r8 + (c ^ (r8 & 7)))]);
+        __builtin_amdgcn_raw_buffer_store_b128(x, nr, (uint32_t)(1024 * k + 128 * r8 + 16 * c), 0, AUX);
+    }
+}
+
 template <bool QO>
 __global__ __launch_bounds__(64 * kF32Waves) void k_fused_ub32d(int64_t n, const float *U, const float *Wj,
                                                                 const float *__restrict__ binv,
@@ -369,13 +395,19 @@ __global__ __launch_bounds__(64 * kF32Waves) void k_fused_ub32d(int64_t n, const
         // __builtin_bit_cast(uint32_t, acc[v]): hipcc of ROCm 7.2 stored acc[0]
         // sixteen times for the latter in this unrolled loop)
         const __amdgpu_buffer_rsrc_t nr = ub_rsrc(Wn + (r0 < n ? r0 * 32 : 0), r0 < n ? (n - r0 < 32 ? n - r0 : 32) : 0);
+        // non-temporal: the next step's SpMM gathers these rows at random (C5:
+        // SpMM 2.800 -> 2.787 ms, step 4.133 -> 4.112 ms, profiles/r06i_c5_ub_nt_ab.log)
+        if (dbg & 4) {  // (A/B: 4-B stores straight from the result layout)
 #pragma unroll
-        for (int v = 0; v < 16; ++v) {
-            const uint32_t rr = (uint32_t)((v & 3) + 8 * (v >> 2) + 4 * hh);
-            // non-temporal: the next step's SpMM gathers these rows at random (C5:
-            // SpMM 2.800 -> 2.787 ms, step 4.133 -> 4.112 ms, profiles/r06i_c5_ub_nt_ab.log)
-            if (dbg & 2) __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(acc[v]), nr, rr * 128 + 4 * jr, 0, 0);
-            else __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(acc[v]), nr, rr * 128 + 4 * jr, 0, 2);
+            for (int v = 0; v < 16; ++v) {
+                const uint32_t rr = (uint32_t)((v & 3) + 8 * (v >> 2) + 4 * hh);
+                if (dbg & 2) __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(acc[v]), nr, rr * 128 + 4 * jr, 0, 0);
+                else __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(acc[v]), nr, rr * 128 + 4 * jr, 0, 2);
+            }
+        } else if (dbg & 2) {
+            rstore_slot<0>(&ust[w][(int)(s & 1)][0][0], acc, jr, hh, lane, nr);
+        } else {
+            rstore_slot<2>(&ust[w][(int)(s & 1)][0][0], acc, jr, hh, lane, nr);  // (U strip s: read above)
         }
         if constexpr (QO) {
             f16v_t q;
@@ -474,7 +506,7 @@ __device__ __forceinline__ void rop_slot(uint32_t sb, int jr, int hh, f16v_t &r)
 __global__ __launch_bounds__(64 * kF32Waves) void k_fused_u32d(int64_t n, float *__restrict__ Wn,
                                                                const float *__restrict__ Wj,
                                                                const float *__restrict__ P2,
-                                                               double *__restrict__ part)
+                                                               double *__restrict__ part, int dbg)
 {
     __shared__ __attribute__((aligned(16))) float ust[kF32Waves][2][2][1024];  // slots x (W_j, Wn) strips
     const int lane = threadIdx.x & 63, w = __builtin_amdgcn_readfirstlane((int)(threadIdx.x >> 6)), hh = lane >> 5,
@@ -511,10 +543,14 @@ __global__ __launch_bounds__(64 * kF32Waves) void k_fused_u32d(int64_t n, float 
         int64_t r0;
         const int64_t rows = rows_of(s, &r0);
         const __amdgpu_buffer_rsrc_t nr = ub_rsrc(Wn + (rows ? r0 * 32 : 0), rows);
+        if (dbg & 4) {  // (A/B: 4-B stores straight from the result layout)
 #pragma unroll
-        for (int v = 0; v < 16; ++v) {
-            const uint32_t rr = (uint32_t)((v & 3) + 8 * (v >> 2) + 4 * hh);
-            __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(acc[v]), nr, rr * 128 + 4 * jr, 0, 0);
+            for (int v = 0; v < 16; ++v) {
+                const uint32_t rr = (uint32_t)((v & 3) + 8 * (v >> 2) + 4 * hh);
+                __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(acc[v]), nr, rr * 128 + 4 * jr, 0, 0);
+            }
+        } else {
+            rstore_slot<0>(&ust[w][(int)(s & 1)][1][0], acc, jr, hh, lane, nr);  // (Wn strip s: read above)
         }
 #pragma unroll
         for (int v = 0; v < 16; ++v) g = mfma32(acc[v], acc[v], g);
@@ -531,7 +567,8 @@ __global__ __launch_bounds__(64 * kF32Waves) void k_fused_e32d(int64_t n, const 
                                                                const float *__restrict__ Wj, const float *Wprev,
                                                                float *Wn, const float *__restrict__ binv,
                                                                const float *__restrict__ P1, int64_t lc,
-                                                               float *__restrict__ qrow, double *__restrict__ part)
+                                                               float *__restrict__ qrow, double *__restrict__ part,
+                                                               int dbg)
 {
     __shared__ __attribute__((aligned(16))) float ust[kF32Waves][3][1024];
     const int lane = threadIdx.x & 63, w = __builtin_amdgcn_readfirstlane((int)(threadIdx.x >> 6)), hh = lane >> 5,
@@ -569,10 +606,18 @@ __global__ __launch_bounds__(64 * kF32Waves) void k_fused_e32d(int64_t n, const 
             for (int s = 0; s < 16; ++s) wn = mfma32(pa[s], po[s], wn);  // - W_{j-1} P1
         }
         const __amdgpu_buffer_rsrc_t nr = ub_rsrc(Wn + (rows ? r0 * 32 : 0), rows);
+        if (dbg & 4) {  // (A/B: 4-B stores straight from the result layout)
+#pragma unroll
+            for (int v = 0; v < 16; ++v) {
+                const int64_t rr = (v & 3) + 8 * (v >> 2) + 4 * hh;
+                __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(wn[v]), nr, (uint32_t)(rr * 128 + 4 * jr), 0, 0);
+            }
+        } else {
+            rstore_slot<0>(&ust[w][1][0], wn, jr, hh, lane, nr);  // (the Y strip: read above)
+        }
 #pragma unroll
         for (int v = 0; v < 16; ++v) {
             const int64_t rr = (v & 3) + 8 * (v >> 2) + 4 * hh;
-            __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(wn[v]), nr, (uint32_t)(rr * 128 + 4 * jr), 0, 0);
             if (r0 + rr == lc && rr < rows) qrow[jr] = q[v];
         }
 #pragma unroll
@@ -599,7 +644,7 @@ int fused_e32(lz_handle *h, int64_t n, const float *Y, const float *Wj, const fl
     const char *ud = getenv("LZ_UB_DMA");  // "0": the register-operand forms (A/B; read per call)
     if (!(ud && ud[0] == '0'))
         hipLaunchKernelGGL(k_fused_e32d, dim3(grid), dim3(64 * kF32Waves), 0, h->stream, n, Y, Wj, Wprev, Wn, binv, P1,
-                           lc, qrow, h->partials);
+                           lc, qrow, h->partials, ud ? atoi(ud) >> 1 : 0);
     else
         hipLaunchKernelGGL(k_fused_e32, dim3(grid), dim3(64 * kF32Waves), 0, h->stream, n, Y, Wj, Wprev, Wn, binv, P1,
                            lc, qrow, h->partials);
@@ -630,7 +675,9 @@ int fused_ub32(lz_handle *h, int64_t n, const float *U, const float *Wj, const f
     const int ev = prof_begin(h, PROF_UPDATE_PASS);
     const char *ud = getenv("LZ_UB_DMA");  // "0": the register-operand form (A/B; read per call)
     const bool dma = !(ud && ud[0] == '0');
-    // (A/B: LZ_UB_DMA=3 drains every load before each strip, 5 stores W'' with the default policy)
+    // (A/B: LZ_UB_DMA=3 drains every load before each strip, 5 stores W'' with the default policy,
+    // 9 stores it by 4-B stores from the result layout instead of whole rows through LDS; 9 in
+    // passes E and U too)
     const int dbg = ud ? atoi(ud) >> 1 : 0;
     if (dma && Qa)
         hipLaunchKernelGGL(k_fused_ub32d<true>, dim3(grid), dim3(64 * kF32Waves), 0, h->stream, n, U, Wj, binv, P2, Wn,
@@ -657,7 +704,8 @@ int fused_u32(lz_handle *h, int64_t n, float *Wn, const float *Wj, const float *
     const int ev = prof_begin(h, PROF_UPDATE_PASS);
     const char *ud = getenv("LZ_UB_DMA");  // "0": the register-operand forms (A/B; read per call)
     if (!(ud && ud[0] == '0'))
-        hipLaunchKernelGGL(k_fused_u32d, dim3(grid), dim3(64 * kF32Waves), 0, h->stream, n, Wn, Wj, P2, h->partials);
+        hipLaunchKernelGGL(k_fused_u32d, dim3(grid), dim3(64 * kF32Waves), 0, h->stream, n, Wn, Wj, P2, h->partials,
+                           ud ? atoi(ud) >> 1 : 0);
     else
         hipLaunchKernelGGL(k_fused_u32, dim3(grid), dim3(64 * kF32Waves), 0, h->stream, n, Wn, Wj, P2, h->partials);
     prof_end(h, ev);

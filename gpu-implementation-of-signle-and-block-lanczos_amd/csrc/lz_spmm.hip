@@ -575,10 +575,10 @@ __global__ __launch_bounds__(256) void k_spmm_seg(int64_t n, const int64_t *__re
     // (diag bit 30: the Y rows stored stay the block's own, so only the reads
     // are L2-resident)
     const int64_t tdx = xcd_remap(blockIdx.x, gridDim.x);
-    const int dmod = diag & 0x3fffffff;
+    const int dmod = diag > 0 ? diag & 0x3fffffff : 0;  // (diag < 0: the LZ_SPMM_HOT probe below)
     const int64_t dmid = dmod > 0 ? ((int64_t)gridDim.x / 2 / dmod) * dmod : 0;
     const int64_t r0 = (dmod > 0 ? tdx % dmod + dmid : tdx) * TR;
-    const int64_t ry = (diag & (1 << 30)) ? tdx * TR : r0;  // the Y tile's first row
+    const int64_t ry = (diag > 0 && (diag & (1 << 30))) ? tdx * TR : r0;  // the Y tile's first row
     const int nrows = (int)((n - r0) < TR ? (n - r0) : TR);
     const int64_t kA = rp[r0];
     if (tid <= nrows) rel[tid] = (int)(rp[r0 + tid] - kA);
@@ -720,6 +720,16 @@ __global__ __launch_bounds__(256) void k_spmm_seg(int64_t n, const int64_t *__re
             for (int t = 0; t < UNR; ++t) {
                 const uint32_t off =
                     s0 + t < end ? __umul24((unsigned)cc[t] - wb, rowb) + lane_off : 0x80000000u;
+#ifdef LZ_DIAG
+                if (diag < 0) {  // (LZ_SPMM_HOT: columns < K gathered with the default policy, the rest with aux)
+                    const int hk = (-diag) & 0xffffff, ha = ((-diag) >> 24) & 3;
+                    if (cc[t] < hk) xs[t] = ldbuf<T, VEC>(xr, off);
+                    else if (ha == 1) xs[t] = ldbuf<T, VEC, 2>(xr, off);
+                    else if (ha == 2) xs[t] = ldbuf<T, VEC, 16>(xr, off);
+                    else xs[t] = ldbuf<T, VEC, 18>(xr, off);
+                    continue;
+                }
+#endif
                 xs[t] = ldbuf<T, VEC>(xr, off);
             }
 #pragma unroll
@@ -1464,7 +1474,15 @@ static int launch_seg(lz_handle *h, int64_t n, const int64_t *rp, const int32_t 
 #ifdef LZ_DIAG
     const char *dg = getenv("LZ_SPMM_DIAG");
     const char *dy = getenv("LZ_SPMM_DIAG_Y");
-    const int diag = (dg ? atoi(dg) : 0) | (dy && dy[0] == '1' ? 1 << 30 : 0);
+    int diag = (dg ? atoi(dg) : 0) | (dy && dy[0] == '1' ? 1 << 30 : 0);
+    // LZ_SPMM_HOT = "K,a": gathers of columns < K with the default cache policy,
+    // the others with a = 1: nt, 2: sc1, 3: sc1 nt (the Infinity-Cache residency
+    // probe, scripts/hot_probe.py; K < 2^24)
+    if (const char *hs = getenv("LZ_SPMM_HOT")) {
+        int hk = 0, ha = 1;
+        if (sscanf(hs, "%d,%d", &hk, &ha) >= 1 && hk >= 0 && hk < (1 << 24) && ha >= 1 && ha <= 3)
+            diag = -(hk | (ha << 24));
+    }
 #else
     constexpr int diag = 0;
 #endif
