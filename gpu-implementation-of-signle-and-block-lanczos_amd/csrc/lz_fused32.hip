@@ -350,8 +350,10 @@ __global__ __launch_bounds__(64 * kF32Waves) void k_fused_ub32d(int64_t n, const
         // vmcnt(8 + ST) for strip s - 1's ST younger stores: a store can be
         // acknowledged before an older load returns, so that count could be
         // reached with strip s's data still on its way -- the first version
-        // read such operands.  Loads return in order, so at most 8 left means
-        // strip s is in.)
+        // read such operands, and round 6 re-checked it: vmcnt(12) with the
+        // four row stores of strip s - 1 in flight gave NaN alphas at once,
+        // profiles/r06w_ub_wait_ab.log.  Loads return in order, so at most 8
+        // left means strip s is in.)
         if (dbg & 1) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
         else asm volatile("s_waitcnt vmcnt(8)" ::: "memory");
         const uint32_t sb = ws_lds_addr(reinterpret_cast<int *>(&ust[w][(int)(s & 1)][0][0]));
