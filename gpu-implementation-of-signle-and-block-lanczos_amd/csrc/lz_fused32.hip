@@ -343,9 +343,16 @@ __global__ __launch_bounds__(64 * kF32Waves) void k_fused_ub32d(int64_t n, const
             __builtin_amdgcn_raw_ptr_buffer_load_lds(wr, (ws_lds_t *)&ust[w][slot][1][256 * k], 16, goff + 1024 * k, 0, 0, 0);
         }
     };
-    dma(0);
+#ifdef LZ_DIAG
+    // timing diagnostics (results wrong; diagnostic build only): dbg 16 skips the
+    // MFMAs, 32 the DMAs, their waits and the W'' stores
+    const bool no_mfma = dbg & 16, no_mem = dbg & 32;
+#else
+    constexpr bool no_mfma = false, no_mem = false;
+#endif
+    if (!no_mem) dma(0);
     for (int64_t s = 0; s < nst; ++s) {
-        dma(s + 1);
+        if (!no_mem) dma(s + 1);
         // strip s landed: only strip s + 1's 8 DMAs may still be in flight.  (Not
         // vmcnt(8 + ST) for strip s - 1's ST younger stores: a store can be
         // acknowledged before an older load returns, so that count could be
@@ -355,7 +362,7 @@ __global__ __launch_bounds__(64 * kF32Waves) void k_fused_ub32d(int64_t n, const
         // profiles/r06w_ub_wait_ab.log.  Loads return in order, so at most 8
         // left means strip s is in.)
         if (dbg & 1) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-        else asm volatile("s_waitcnt vmcnt(8)" ::: "memory");
+        else if (!no_mem) asm volatile("s_waitcnt vmcnt(8)" ::: "memory");
         const uint32_t sb = ws_lds_addr(reinterpret_cast<int *>(&ust[w][(int)(s & 1)][0][0]));
         float4 u4[4], w4[4];
         const uint32_t o0 = sb + rbase + 16u * (uint32_t)((4 * hh + 0) ^ (jr & 7)),
@@ -386,10 +393,15 @@ __global__ __launch_bounds__(64 * kF32Waves) void k_fused_ub32d(int64_t n, const
         f16v_t acc, acc2;  // two independent chains (each MFMA waits on its predecessor)
 #pragma unroll
         for (int v = 0; v < 16; ++v) acc[v] = acc2[v] = 0.0f;
+        if (no_mfma) {
 #pragma unroll
-        for (int s2 = 0; s2 < 16; ++s2) {
-            acc = mfma32(ua[s2], bo[s2], acc);    // U beta^-1
-            acc2 = mfma32(wa[s2], po[s2], acc2);  // - W_j P2
+            for (int v = 0; v < 16; ++v) acc[v] = ua[v] - wa[v];
+        } else {
+#pragma unroll
+            for (int s2 = 0; s2 < 16; ++s2) {
+                acc = mfma32(ua[s2], bo[s2], acc);    // U beta^-1
+                acc2 = mfma32(wa[s2], po[s2], acc2);  // - W_j P2
+            }
         }
 #pragma unroll
         for (int v = 0; v < 16; ++v) acc[v] += acc2[v];
@@ -406,6 +418,7 @@ __global__ __launch_bounds__(64 * kF32Waves) void k_fused_ub32d(int64_t n, const
                 if (dbg & 2) __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(acc[v]), nr, rr * 128 + 4 * jr, 0, 0);
                 else __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(acc[v]), nr, rr * 128 + 4 * jr, 0, 2);
             }
+        } else if (no_mem) {
         } else if (dbg & 2) {
             rstore_slot<0>(&ust[w][(int)(s & 1)][0][0], acc, jr, hh, lane, nr);
         } else {
@@ -427,8 +440,10 @@ __global__ __launch_bounds__(64 * kF32Waves) void k_fused_ub32d(int64_t n, const
                 __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(q[v]), qb, rr * 128 + 4 * jr, 0, 0);
             }
         }
+        if (!no_mfma) {
 #pragma unroll
-        for (int v = 0; v < 16; ++v) g = mfma32(acc[v], acc[v], g);  // rows past n: 0
+            for (int v = 0; v < 16; ++v) g = mfma32(acc[v], acc[v], g);  // rows past n: 0
+        }
     }
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     __syncthreads();  // every wave is done with its slots: the reduction reuses them
