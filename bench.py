@@ -50,6 +50,16 @@ HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec (MI355X_MICROARCH.md)
 FP64_MFMA_PEAK_TFS = 78.6  # v_mfma_f64_16x16x4f64: 32 FLOP/clk/SIMD x 1024 SIMDs x 2.4 GHz
 RITZ_TOL = 1e-10  # BASELINE.json north star: Ritz values within 1e-10 of the reference
 SPMM_ALL_L2_MS = 0.770  # the plain SpMM's all-L2 diagnostic at C3, round 6 (profiles/r06l_spmm_l2_ceiling.log)
+# What plain streaming kernels reach on this hardware (scripts/gprobe/stream_probe.hip, 2 GiB arrays,
+# 16-B accesses, best of its shapes and cache policies; one box, round 6): the practical HBM ceilings
+# per read:write mix, beside the 8 TB/s nominal peak the roofline fractions are quoted against
+STREAM_GBS = {"read": 6590.0, "write": 4940.0, "copy": 4970.0, "r2w1": 5040.0, "r3w2": 4880.0, "r3w3": 4750.0}
+STREAM_SRC = "profiles/r06ac_stream_probe.log (scripts/gprobe/stream_probe.hip)"
+
+
+def stream_ceiling(achieved_gbs, mix):
+    """The achieved rate against the streaming probe's rate for the same read:write mix."""
+    return {"mix": mix, "GBs": STREAM_GBS[mix], "frac": round(achieved_gbs / STREAM_GBS[mix], 4), "source": STREAM_SRC}
 
 
 def log(*a):
@@ -553,7 +563,9 @@ def main():
         plain["roofline"] = {"bound": "hbm", "kernel": spmm_kernel(A.nnz, n), "achieved": round(gbs, 1),
                              "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": round(gbs / HBM_PEAK_GBS, 4),
                              "traffic": trp, "traffic_source": srcp, "avg_ms": round(ms / cnt, 4),
-                             "bytes_per_launch": spmm_bytes(n, A.nnz, b)}
+                             "bytes_per_launch": spmm_bytes(n, A.nnz, b),
+                             # A and X read, Y written: 2 : 1
+                             "stream_ceiling": stream_ceiling(gbs, "r2w1")}
         if n == 10_000_000 and args.nnz_per_row == 10.0 and args.halfwidth == 4096:
             # the tile structure's own ceiling at C3 (DESIGN.md 4 SpMM): the same kernel and instruction
             # stream with every input L2-resident (diagnostic build, LZ_SPMM_DIAG=64) -- what no HBM
@@ -836,6 +848,8 @@ def main():
                     "traffic": traffic, "traffic_unit": "bytes/launch (mean over the profiled solve's launches)",
                     "traffic_source": tsrc, "avg_ms": round(t_pass * 1e3, 4),
                     "bytes_per_launch": round(tot / spmm_cnt),
+                    # a steady launch reads A + 3nbs and writes 2nbs: ~2 : 1
+                    "stream_ceiling": stream_ceiling(ach, "r2w1"),
                     "bytes_note": f"{K} steps per solve in {spmm_cnt} launches: the first step pass 1 only (A + 2nbs), "
                                   f"the others pass 2 of step j + pass 1 of step j+1 (A + 5nbs); A with {cb}-byte "
                                   f"columns"}
